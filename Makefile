@@ -1,0 +1,30 @@
+# Top-level build: the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+#   make            -> voxelraytracer_amd/_lib/libvrt.so + oracle/build/liboracle.so
+# Numerics flags are part of the parity contract (DESIGN.md "Numerics"): no FP contraction,
+# correctly rounded f32 div/sqrt on the device.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+LIBDIR := voxelraytracer_amd/_lib
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Wall
+SRC := voxelraytracer_amd/csrc/vrt_render.hip voxelraytracer_amd/csrc/vrt_host.cpp
+
+all: $(LIBDIR)/libvrt.so oracle
+
+$(LIBDIR)/libvrt.so: $(SRC) include/vrt.h
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC) -Wl,-rpath,/opt/rocm/lib
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(SRC) include/vrt.h
+	mkdir -p build/asm
+	$(HIPCC) $(HIPFLAGS) -c --cuda-device-only -S -o build/asm/vrt_render.s voxelraytracer_amd/csrc/vrt_render.hip
+	$(HIPCC) $(HIPFLAGS) -c --cuda-device-only -Rpass-analysis=kernel-resource-usage -o /dev/null voxelraytracer_amd/csrc/vrt_render.hip
+
+clean:
+	rm -rf $(LIBDIR) build
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle asm clean

@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s + achieved algorithmic GB/s of the voxel ray-trace pass.
+
+Workload (BASELINE.json metric "1920x1080 @ 128^3 voxels, 4 bounces"): configs[3], the
+_REFRACTION scene at 128^3, 1920x1080, reflect+refract 4 bounces (MAX_REFLECTIONS =
+MAX_TRANSPARENCIES = 4), colour-only, noise 0, camera/sun of SURVEY.md §8d. A step = one frame.
+
+Multi-GPU (one process per GPU, torchrun): the frame is split into cyclic row bands (rank r owns
+rows r, r+N, ...); every rank renders its band into HBM and rank 0 gathers the RGBA bands over
+RCCL each frame (the only exchange of the path). The total work is the fixed frame: strong
+scaling.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (scene, N, W, H, R, T, description)
+    "C0": ("glass_cube", 16, 400, 400, 1, 2, "_GLASS_CUBE 16^3 400x400 (R,T)=(1,2)"),
+    "C1": ("glass_cube", 128, 1920, 1080, 1, 2, "_GLASS_CUBE 128^3 1920x1080 1 reflection (R,T)=(1,2)"),
+    "C2": ("terrain", 128, 1920, 1080, 4, 2, "_TERRAIN 128^3 1920x1080 4 reflection bounces (R,T)=(4,2)"),
+    "C3": ("refraction", 128, 1920, 1080, 4, 4,
+           "_REFRACTION 128^3 1920x1080 reflect+refract 4 bounces (R,T)=(4,4)"),
+    "C4": ("terrain", 512, 3840, 2160, 4, 2, "_TERRAIN 512^3 3840x2160 4 bounces (R,T)=(4,2)"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the oracle CPU baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(cam, vox, n, params, budget_s, threads):
+    """The oracle (scalar C restatement, `port`) on host cores over a bounded sample of the same
+    frame: whole frames if they fit the budget, else every k-th row band."""
+    import oracle
+
+    h = cam.height
+    t0 = time.perf_counter()
+    _, _, c = oracle.render(cam, vox, n, params, row0=0, rows=h // 16, row_step=16, threads=threads)
+    probe = time.perf_counter() - t0
+    est_frame = probe * 16
+    rays = 0
+    frames = 0
+    t0 = time.perf_counter()
+    if est_frame * 1.5 <= budget_s:
+        while True:
+            _, _, c = oracle.render(cam, vox, n, params, threads=threads)
+            rays += c["primary_rays"] + c["secondary_rays"] + c["shadow_rays"]
+            frames += 1
+            if time.perf_counter() - t0 + est_frame > budget_s:
+                break
+        sample = f"{frames} full frame(s)"
+    else:
+        step = max(2, int(est_frame / budget_s) + 1)
+        _, _, c = oracle.render(cam, vox, n, params, row0=0, rows=h // step, row_step=step,
+                                threads=threads)
+        rays = c["primary_rays"] + c["secondary_rays"] + c["shadow_rays"]
+        sample = f"every {step}th row of one frame ({h // step} rows)"
+    dt = time.perf_counter() - t0
+    return dict(value=rays / dt / 1e6, unit="Mrays/s", cores=threads, kind="port",
+                sample=f"oracle/vrt_oracle.c -O3, {threads} threads, {sample}, {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import voxelraytracer_amd as vrt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    scene, n, w, h, R, T, desc = CONFIGS[args.config]
+    cam = vrt.make_camera(w, h)
+    params = vrt.default_params(R, T)
+    # Volume: built once on rank 0 (main.cpp:218-288) and broadcast over RCCL to every GPU.
+    vox_host = vrt.build_scene(scene, n) if rank == 0 else np.empty(n ** 3, np.uint8)
+    if world > 1:
+        t = torch.from_numpy(vox_host).to(dev)
+        dist.broadcast(t, 0)
+        vox_host = t.cpu().numpy()
+    ren = vrt.Renderer(local)
+    ren.upload_volume(vox_host, n)
+
+    if h % world:
+        raise SystemExit(f"height {h} not divisible by {world} GPUs")
+    rows = h // world
+    band = torch.empty((rows, w, 4), dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(band) for _ in range(world)] if (rank == 0 and world > 1) else None
+    # on one GPU the band IS the frame; with N ranks rank 0 assembles the frame from the gather
+    frame = torch.empty((h, w, 4), dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    # One counted frame (outside the timed region) gives the rays and algorithmic bytes per frame.
+    cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device=dev)
+    ren.render_rows_async(cam, params, rank, rows, world, band.data_ptr(), 0, cnt.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.all_reduce(cnt)
+    counters = vrt.counters_dict(cnt.cpu().tolist())
+    rays_per_frame = vrt.total_rays(counters)
+    bytes_per_frame = vrt.algorithmic_bytes(counters)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        ren.render_rows_async(cam, params, rank, rows, world, band.data_ptr(), 0, 0, sptr)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.gather(band, gather, dst=0)
+            if rank == 0:   # re-interleave the cyclic bands into the frame (frame row = i*N + r)
+                torch.stack(gather, 1, out=frame.view(rows, world, w, 4))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    t = torch.tensor([elapsed, float(np.mean(kernel_ms))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = t.tolist()
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = rays_per_frame * args.steps / elapsed / 1e6
+        # roofline of the dominant kernel on this rank: algorithmic bytes of its band per launch
+        own_bytes = bytes_per_frame / world
+        achieved = own_bytes / (float(np.mean(kernel_ms)) * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc) and world == 1:
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(cam, vox_host, n, params, args.cpu_seconds, args.cpu_threads)
+        out = {
+            "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}: {desc}",
+                "scene": scene,
+                "volume_n": n,
+                "width": w,
+                "height": h,
+                "max_reflections": R,
+                "max_transparencies": T,
+                "parallelism": f"row-band x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "rays_per_frame": rays_per_frame,
+                "algorithmic_bytes_per_frame": bytes_per_frame,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "kernel_ms": round(float(np.mean(kernel_ms)), 4),
+                "kernel_ms_max_over_ranks": round(kern_ms_max, 4),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

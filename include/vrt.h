@@ -1,0 +1,164 @@
+/*
+ * vrt.h — C-ABI drop-in boundary of the MI355X-native voxel ray tracer.
+ *
+ * Replaces the reference's GL boundary for the per-pixel ray-trace pass:
+ *   - 3D-texture upload      src/main.cpp:315-319  (glTexImage3D GL_RED/UNSIGNED_BYTE, NEAREST)
+ *   - uniforms + quad draw    src/main.cpp:325-361  (u_PVInvMatrix, u_Size, u_SunDir, u_Time, noises)
+ *   - RGB colour FBO          src/FrameBuffer.cpp:5-19
+ * and executes the program in res/shaders/voxel.glsl (fragment :1-452, vertex :454-475)
+ * as a hand-written gfx950 HIP kernel.
+ *
+ * Conventions
+ *   - Plain C types only; no exceptions cross the ABI; every entry point returns a vrt_status
+ *     (0 = ok, <0 = error) and sets a per-context message readable with vrt_last_error().
+ *   - Not thread-safe per context: one context per host thread (as the GL context was).
+ *   - Volumes are N^3 bytes, x fastest: idx = x + y*N + z*N*N   (main.cpp:227).
+ *   - Images are W*H RGBA float, row 0 = bottom row (GL window convention).
+ */
+#ifndef VRT_H
+#define VRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VRT_ABI_VERSION 1
+
+typedef struct vrt_ctx vrt_ctx;
+
+typedef enum {
+  VRT_OK = 0,
+  VRT_ERR_INVALID = -1,      /* bad argument (null pointer, size, unsupported N) */
+  VRT_ERR_DEVICE = -2,       /* HIP runtime error (message has the hipError string) */
+  VRT_ERR_NO_VOLUME = -3,    /* vrt_render before vrt_upload_volume */
+  VRT_ERR_OOM = -4,          /* device allocation failed */
+  VRT_ERR_UNSUPPORTED = -5   /* parameter combination not built (see vrt_last_error) */
+} vrt_status;
+
+/* Camera: u_PVInvMatrix (voxel.glsl:464, set at main.cpp:333) plus the FBO size. */
+typedef struct {
+  float inv_pv[16];   /* column-major, GL convention: m[col*4 + row] */
+  int32_t width;
+  int32_t height;
+} vrt_camera;
+
+/* Volume: the bytes main.cpp:218-288 builds and :318 uploads. */
+typedef struct {
+  const uint8_t* voxels; /* host pointer, N^3 bytes, x fastest */
+  int32_t n;             /* u_Size (voxel.glsl:18) */
+} vrt_volume;
+
+/* Per-frame parameters: the remaining uniforms (main.cpp:335-348) and compile-time switches. */
+typedef struct {
+  float sun_dir[3];           /* u_SunDir (main.cpp:346-348); the shader re-normalises it */
+  float time;                 /* u_Time, the frame counter as float (main.cpp:343-345) */
+  float ray_noise;            /* u_RayNoise        [0, 0.05] */
+  float reflection_noise;     /* u_ReflectionNoise [0, 0.05] */
+  float refraction_noise;     /* u_RefractionNoise [0, 0.01] */
+  float max_ray_length;       /* u_MaxRayLength, default 100 (voxel.glsl:17) */
+  int32_t max_reflections;    /* MAX_REFLECTIONS   (voxel.glsl:4), 0..8 */
+  int32_t max_transparencies; /* MAX_TRANSPARENCIES (voxel.glsl:5), 0..8 */
+  int32_t color_only;         /* _COLOR_ONLY (voxel.glsl:6): must be 1 in ABI v1 */
+  int32_t reserved0;
+  const uint8_t* atlas_rgba;  /* textured mode (not in ABI v1): u_TextureUnit atlas */
+  int32_t atlas_size;         /* u_AtlasSize */
+  int32_t atlas_texture_size; /* u_AtlasTextureSize */
+} vrt_params;
+
+/* Per-pixel record of the PRIMARY ray (the first stack pop, voxel.glsl:430-437). Parity key:
+ * bit-exact between the HIP kernel and the CPU oracle. */
+typedef struct {
+  int32_t voxel_index;  /* linear index of the hit voxel (the texel GetVoxel read), -1 = no hit */
+  float ray_length;     /* RayIntersection.rayLength of the primary hit (0 if none) */
+  uint32_t steps;       /* DDA + shadow-DDA iterations spent on the whole pixel */
+  uint32_t flags;       /* VRT_HIT_FLAG_* */
+} vrt_hit;
+
+#define VRT_HIT_FLAG_TIE3 1u        /* a y+z (or x+y+z) zero-t tie read intersectionAxis[3] (clamped to 2) */
+#define VRT_HIT_FLAG_STEP_CAP 2u    /* a march hit VRT_MAX_STEPS (the GLSL would spin) */
+#define VRT_HIT_FLAG_STACK_FULL 4u  /* a push was dropped (cannot happen for stack = R+T+1) */
+
+#define VRT_MAX_STEPS 4096          /* per RayMarch / RayMarchShadow call */
+
+/* Counter slots (uint64 each) accumulated by a render. Algorithmic bytes of a frame:
+ *   DDA_STEPS + SHADOW_STEPS + 2*REFRACTION_PROBES + 16*PIXELS */
+enum {
+  VRT_CNT_PIXELS = 0,
+  VRT_CNT_PRIMARY_RAYS,
+  VRT_CNT_SECONDARY_RAYS,     /* stack pops after the primary */
+  VRT_CNT_SHADOW_RAYS,        /* RayMarchShadow calls */
+  VRT_CNT_DDA_STEPS,          /* RayMarch iterations that called GetVoxel */
+  VRT_CNT_SHADOW_STEPS,       /* RayMarchShadow iterations that called GetVoxel */
+  VRT_CNT_REFRACTION_PROBES,  /* GetRefractionRay calls (2 voxel reads each) */
+  VRT_CNT_TIE3,               /* index==3 tie events */
+  VRT_CNT_STEP_CAP,           /* marches cut by VRT_MAX_STEPS */
+  VRT_CNT_COUNT
+};
+
+typedef struct {
+  uint64_t counters[VRT_CNT_COUNT];
+  float kernel_ms;            /* hipEvent time of the render kernel(s) */
+  float reserved[3];
+} vrt_stats;
+
+/* ---- context / device ---------------------------------------------------------------------- */
+
+/* Create a context on HIP device `device` (ordinal). */
+int vrt_create(int device, vrt_ctx** out);
+void vrt_destroy(vrt_ctx* ctx);
+const char* vrt_last_error(const vrt_ctx* ctx);  /* never NULL; "" when no error */
+int vrt_abi_version(void);
+
+/* Copy the volume to device memory (replaces glTexImage3D, main.cpp:315-318). The caller keeps
+ * ownership of `vol->voxels`. N must be a power of two in [2, 1024]. */
+int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol);
+
+/* Device pointer of the resident volume (N^3 bytes), e.g. for a broadcast. NULL if none. */
+const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
+
+/* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats
+ * (alpha = 1, voxel.glsl:451) to the HOST buffer out_rgba. out_hit (W*H records) and stats may
+ * be NULL. */
+int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
+               float* out_rgba, vrt_hit* out_hit, vrt_stats* stats);
+
+/* Asynchronous band render into DEVICE buffers on `hip_stream` (hipStream_t, NULL = default).
+ * Renders frame rows row0 + i*row_step for i in [0, rows) at full width; output row i of
+ * d_out_rgba / d_out_hit holds frame row row0 + i*row_step. d_out_hit and d_counters
+ * (VRT_CNT_COUNT uint64, accumulated with atomics, caller zeroes) may be NULL. No host sync,
+ * no allocation: capturable in a hipGraph. */
+int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
+                          int32_t row0, int32_t rows, int32_t row_step,
+                          float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
+                          void* hip_stream);
+
+/* ---- host-side scene harness (mirrors src/main.cpp; no GPU needed) ----------------------- */
+
+enum { VRT_SCENE_TERRAIN = 0, VRT_SCENE_GLASS_CUBE = 1, VRT_SCENE_REFRACTION = 2 };
+
+/* Build-defined seeded heightfield in [0,1) replacing Greet::Noise::GenNoise (main.cpp:185,195);
+ * out has n*n floats, index x + z*n. See DESIGN.md "Terrain noise". */
+int vrt_terrain_noise(int32_t n, uint32_t seed, float* out);
+
+/* Fill out[n^3] exactly as main.cpp:218-288 does for _TERRAIN / _GLASS_CUBE / _REFRACTION. */
+int vrt_build_scene(int32_t scene, int32_t n, uint32_t seed, uint8_t* out);
+
+/* invPV = inverse(P * V) with P = Perspective(aspect, fov_deg, near, far) and
+ * V = RotateX(-rot_x) * RotateY(-rot_y) * Translate(-pos)   (main.cpp:67-76, 161). Angles in
+ * degrees. Computed in double, rounded to float. */
+int vrt_camera_make(const float pos[3], const float rot_deg[3], int32_t width, int32_t height,
+                    float fov_deg, float near_plane, float far_plane, vrt_camera* out);
+
+/* u_SunDir from the day/night clock (main.cpp:346-348). */
+void vrt_sun_dir(float time_of_day, float day_time, float out[3]);
+
+/* Default params for the bench configs (noise 0, max_ray_length 100, colour-only, time 1). */
+void vrt_params_default(vrt_params* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VRT_H */

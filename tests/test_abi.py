@@ -1,0 +1,90 @@
+"""The C-ABI boundary on the CPU: the library loads, exports every symbol include/vrt.h declares,
+the ctypes mirror matches the header's layout, and the host harness (scene builders, camera, sun)
+agrees with the oracle's independent restatement. No compute call touches a GPU here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import voxelraytracer_amd as vrt
+from voxelraytracer_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "vrt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(vrt_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("vrt_create", "vrt_upload_volume", "vrt_render", "vrt_render_rows_async",
+                 "vrt_destroy", "vrt_last_error"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol(built):
+    lib = C.CDLL(abi.LIB_PATH)
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    assert set(header_functions()) == set(abi.SIGNATURES), "ctypes mirror out of sync with vrt.h"
+
+
+def test_struct_layouts():
+    assert C.sizeof(abi.Camera) == 72
+    assert C.sizeof(abi.Hit) == 16
+    assert C.sizeof(abi.Params) == 64
+    assert C.sizeof(abi.Stats) == 8 * abi.VRT_CNT_COUNT + 16
+    assert np.dtype(abi.HIT_DTYPE).itemsize == C.sizeof(abi.Hit)
+
+
+def test_abi_version(built):
+    assert vrt.lib().vrt_abi_version() == 1
+
+
+@pytest.mark.parametrize("scene", [0, 1, 2])
+@pytest.mark.parametrize("n", [8, 16, 32, 64, 128, 256])
+def test_scene_builders_match_oracle(built, scene, n):
+    a = vrt.build_scene(scene, n)
+    b = oracle.build_scene(scene, n)
+    assert np.array_equal(a, b)
+
+
+def test_terrain_noise_matches_oracle(built):
+    for n in (16, 32, 128, 512):
+        assert np.array_equal(vrt.terrain_noise(n), oracle.terrain_noise(n))
+
+
+def test_invalid_scene_rejected(built):
+    with pytest.raises(vrt.VrtError):
+        vrt.build_scene(7, 16)
+
+
+def test_camera_looks_into_the_volume(built):
+    cam = vrt.make_camera(64, 36)
+    m = np.array(cam.inv_pv, np.float64).reshape(4, 4).T   # row-major view of column-major data
+    near = m @ np.array([0, 0, -1, 1.0])
+    near = near[:3] / near[3]
+    # the near-plane centre sits 0.01 in front of the camera at main.cpp:171's position
+    assert np.linalg.norm(near - np.array(vrt.DEFAULT_CAM_POS)) == pytest.approx(0.01, rel=1e-3)
+
+
+def test_sun_direction_make_day(built):
+    s = np.array(vrt.sun_dir(0.9 * 50.0, 50.0))
+    assert abs(np.linalg.norm(s) - 1) < 1e-6
+    assert s[1] > 0.7    # daytime: the sky term max(u_SunDir.y, 0) is on (voxel.glsl:391)
+    assert s[2] > 0
+
+
+def test_create_without_gpu_fails_loudly(built):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(vrt.VrtError):
+        vrt.Renderer(0)

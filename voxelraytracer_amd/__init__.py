@@ -1,0 +1,165 @@
+"""voxelraytracer_amd — MI355X-native drop-in for the per-pixel ray tracer of
+Thraix/VoxelRayTracer (res/shaders/voxel.glsl).
+
+The product is the C-ABI library voxelraytracer_amd/_lib/libvrt.so (include/vrt.h): a gfx950
+HIP kernel plus the host harness that mirrors src/main.cpp. This module is a thin Python host
+over that ABI with the reference's vocabulary (scene, camera, sun, frame, volume).
+There is no CPU fallback: constructing a Renderer without the HIP library or a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .abi import (  # noqa: F401  (re-exported vocabulary)
+    COUNTER_NAMES,
+    HIT_DTYPE,
+    SCENE_GLASS_CUBE,
+    SCENE_REFRACTION,
+    SCENE_TERRAIN,
+    SCENES,
+    Camera,
+    Params,
+    VrtError,
+)
+
+# Camera pose of AppScene (main.cpp:171-172) and projection (main.cpp:161): 90 deg, 0.01..100.
+DEFAULT_CAM_POS = (-3.45, 2.17, 3.53)
+DEFAULT_CAM_ROT = (-33.0, -48.0, 0.0)
+FOV_DEG, NEAR, FAR = 90.0, 0.01, 100.0
+
+
+def lib():
+    return abi.load_library()
+
+
+def build_scene(scene, n: int, seed: int = 0) -> np.ndarray:
+    """N^3 uint8 volume, x fastest (main.cpp:218-288). `scene` is a name or SCENE_* id."""
+    sid = SCENES[scene] if isinstance(scene, str) else int(scene)
+    out = np.zeros(n * n * n, dtype=np.uint8)
+    rc = lib().vrt_build_scene(sid, n, seed, out.ctypes.data)
+    if rc != 0:
+        raise VrtError(rc, "vrt_build_scene")
+    return out
+
+
+def terrain_noise(n: int, seed: int = 0) -> np.ndarray:
+    out = np.zeros(n * n, dtype=np.float32)
+    rc = lib().vrt_terrain_noise(n, seed, out.ctypes.data)
+    if rc != 0:
+        raise VrtError(rc, "vrt_terrain_noise")
+    return out
+
+
+def make_camera(width: int, height: int, pos=DEFAULT_CAM_POS, rot=DEFAULT_CAM_ROT,
+                fov=FOV_DEG, near=NEAR, far=FAR) -> Camera:
+    cam = Camera()
+    p = (C.c_float * 3)(*pos)
+    r = (C.c_float * 3)(*rot)
+    rc = lib().vrt_camera_make(C.byref(p), C.byref(r), width, height, fov, near, far, C.byref(cam))
+    if rc != 0:
+        raise VrtError(rc, "vrt_camera_make")
+    return cam
+
+
+def sun_dir(time_of_day: float, day_time: float = 50.0):
+    out = (C.c_float * 3)()
+    lib().vrt_sun_dir(time_of_day, day_time, C.byref(out))
+    return tuple(out)
+
+
+def default_params(max_reflections: int = 1, max_transparencies: int = 2, **kw) -> Params:
+    """Bench defaults: "Make day" sun, u_Time=1, noise 0, 100 max length."""
+    p = Params()
+    lib().vrt_params_default(C.byref(p))
+    p.max_reflections = max_reflections
+    p.max_transparencies = max_transparencies
+    for k, v in kw.items():
+        if k == "sun_dir":
+            p.sun_dir = (C.c_float * 3)(*v)
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def counters_dict(values) -> dict:
+    return {name: int(values[i]) for i, name in enumerate(COUNTER_NAMES)}
+
+
+def algorithmic_bytes(c: dict) -> int:
+    """1 B per DDA step (both marches) + 2 B per refraction probe + 16 B per RGBA pixel."""
+    return c["dda_steps"] + c["shadow_steps"] + 2 * c["refraction_probes"] + 16 * c["pixels"]
+
+
+def total_rays(c: dict) -> int:
+    return c["primary_rays"] + c["secondary_rays"] + c["shadow_rays"]
+
+
+class Renderer:
+    """One vrt_ctx on one HIP device (replaces the GL context + FrameBuffer of the reference)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = lib()
+        h = C.c_void_p()
+        rc = self._lib.vrt_create(device, C.byref(h))
+        if rc != 0:
+            raise VrtError(rc, f"vrt_create(device={device}) failed (no GPU?)")
+        self._h = h
+        self.n = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.vrt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._lib.vrt_last_error(self._h)
+            raise VrtError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def upload_volume(self, voxels: np.ndarray, n: int):
+        v = np.ascontiguousarray(voxels, dtype=np.uint8).reshape(-1)
+        if v.size != n * n * n:
+            raise ValueError("volume size mismatch")
+        vol = abi.Volume(v.ctypes.data_as(C.POINTER(C.c_uint8)), n)
+        self._check(self._lib.vrt_upload_volume(self._h, C.byref(vol)), "vrt_upload_volume")
+        self.n = n
+
+    def volume_device_ptr(self) -> int:
+        return self._lib.vrt_volume_device_ptr(self._h) or 0
+
+    def render(self, cam: Camera, params: Params, want_hits: bool = True):
+        """Synchronous frame: returns (rgba[H,W,4] float32, hits[H,W] structured or None, stats)."""
+        w, h = cam.width, cam.height
+        rgba = np.empty((h, w, 4), dtype=np.float32)
+        hits = np.empty((h, w), dtype=HIT_DTYPE) if want_hits else None
+        st = abi.Stats()
+        self._check(
+            self._lib.vrt_render(self._h, C.byref(cam), C.byref(params), rgba.ctypes.data,
+                                 hits.ctypes.data if want_hits else None, C.byref(st)),
+            "vrt_render",
+        )
+        stats = counters_dict(st.counters)
+        stats["kernel_ms"] = float(st.kernel_ms)
+        return rgba, hits, stats
+
+    def render_rows_async(self, cam: Camera, params: Params, row0: int, rows: int, row_step: int,
+                          d_out: int, d_hit: int = 0, d_counters: int = 0, stream: int = 0):
+        """Band render into device pointers (e.g. torch tensors' data_ptr()) on a HIP stream."""
+        self._check(
+            self._lib.vrt_render_rows_async(self._h, C.byref(cam), C.byref(params), row0, rows,
+                                            row_step, d_out, d_hit or None, d_counters or None,
+                                            stream or None),
+            "vrt_render_rows_async",
+        )

@@ -1,0 +1,670 @@
+// vrt_render.hip — gfx950 HIP kernel for the per-pixel program of res/shaders/voxel.glsl and
+// the C-ABI context around it (include/vrt.h).
+//
+// One work-item per pixel; a 256-thread workgroup covers a 16x16 pixel tile and each wave64 an
+// 8x8 sub-tile, so the 64 rays of a wave start coherent. Every float operation of the DDA is
+// replayed in the reference's order with -ffp-contract=off and correctly rounded div/sqrt, which
+// makes hit records bit-exact against the CPU oracle (DESIGN.md "Numerics").
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "vrt.h"
+
+namespace vrt {
+
+// ------------------------------------------------------------------------ kernel arguments --
+
+struct KArgs {
+  float inv_pv[16];
+  float sun[3];
+  float time, ray_noise, refl_noise, refr_noise, max_len;
+  float fn;
+  int32_t n, width, height;
+  int32_t row0, rows, row_step;
+  int32_t max_refl, max_transp;
+};
+
+// ------------------------------------------------------------------ GLSL vector semantics --
+
+struct f3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+__device__ __forceinline__ void set_comp(f3& a, int i, float f) {
+  if (i == 0) a.x = f;
+  else if (i == 1) a.y = f;
+  else a.z = f;
+}
+__device__ __forceinline__ f3 normalize3(f3 v) {
+  const float inv = 1.0f / __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+  return v * inv;
+}
+__device__ __forceinline__ float gsign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+__device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
+__device__ __forceinline__ float gmax(float x, float y) { return __builtin_fmaxf(x, y); }
+__device__ __forceinline__ float gpow(float x, float y) { return exp2f(y * log2f(x)); }
+__device__ __forceinline__ float mixf(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+__device__ __forceinline__ f3 reflect3(f3 i, f3 n) {
+  const float s = 2.0f * dot3(n, i);
+  return i - s * n;
+}
+__device__ __forceinline__ f3 refract3(f3 i, f3 n, float eta) {
+  const float d = dot3(n, i);
+  const float k = 1.0f - eta * eta * (1.0f - d * d);
+  if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+  const float s = eta * d + __builtin_sqrtf(k);
+  return eta * i - s * n;
+}
+
+// Jenkins one-at-a-time mix, voxel.glsl:98-125
+__device__ __forceinline__ uint32_t hash1(uint32_t x) {
+  x += (x << 10u);
+  x ^= (x >> 6u);
+  x += (x << 3u);
+  x ^= (x >> 11u);
+  x += (x << 15u);
+  return x;
+}
+__device__ __forceinline__ float random4(float x, float y, float z, float w) {
+  const uint32_t h = hash1(__float_as_uint(x) ^ hash1(__float_as_uint(y)) ^
+                           hash1(__float_as_uint(z)) ^ hash1(__float_as_uint(w)));
+  return __uint_as_float((h & 0x007FFFFFu) | 0x3F800000u) - 1.0f;
+}
+// RandomizeDirection, voxel.glsl:132-140 (runs even at noise 0: it decides the sign of zeros)
+__device__ __forceinline__ f3 randomize(f3 dir, f3 pos, float randomness, float seed) {
+  const f3 p = mk((pos.x + dir.x) + seed, (pos.y + dir.y) + seed, (pos.z + dir.z) + seed);
+  const float dx = random4(p.x, p.y, p.z, 0.0f + seed);
+  const float dy = random4(p.x, p.y, p.z, 0.5f + seed);
+  const float dz = random4(p.x, p.y, p.z, 1.0f + seed);
+  const f3 r = mk((dx + -0.5f) * randomness, (dy + -0.5f) * randomness, (dz + -0.5f) * randomness);
+  return normalize3(dir + r);
+}
+
+// ------------------------------------------------------- materials (_COLOR_ONLY, :71-91) ----
+
+__device__ __forceinline__ float mat_refr(uint32_t b) { return b == 2 ? 1.5f : 1.0f; }
+__device__ __forceinline__ bool mat_transparent(uint32_t b) { return b == 0 || b == 2; }
+__device__ __forceinline__ bool mat_reflective(uint32_t b) { return b == 2; }
+__device__ __forceinline__ float mat_kd(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 0.4f); }
+__device__ __forceinline__ float mat_ks(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 0.2f); }
+__device__ __forceinline__ float mat_exp(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 10.0f); }
+__device__ __forceinline__ float4 mat_color(uint32_t b) {
+  if (b == 1) return make_float4(0.5f, 0.5f, 0.5f, 1.0f);
+  if (b >= 3) return make_float4(0.05f, 0.5f, 0.1f, 1.0f);
+  return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+__device__ __forceinline__ uint32_t mat_id(uint32_t b) { return b > 3 ? 3 : b; }
+
+constexpr float kAmbient = 0.3f;
+
+// ----------------------------------------------------------------------------- ray state --
+
+struct Ray {
+  f3 pos, dir;
+  float len, energy;
+  uint32_t voxel;  // byte value of the medium the ray travels in (0 = air)
+  int32_t rdepth, tdepth;
+};
+
+struct Hit {
+  f3 point, normal;
+  float len;
+  uint32_t voxel;
+  int32_t vidx;
+  bool found;
+};
+
+struct Counters {
+  uint32_t c[VRT_CNT_COUNT];
+};
+
+struct Ctx {
+  const uint8_t* __restrict__ vox;
+  int32_t n;
+  float fn;
+  float max_len;
+  f3 sun, sun_n;
+  float time, refl_noise, refr_noise;
+};
+
+// GetVoxel (voxel.glsl:149-154): `>` bounds test, NEAREST + GL_REPEAT, NaN reads 0.
+__device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p, int32_t& vidx) {
+  if (!(p.x >= 0.0f && p.y >= 0.0f && p.z >= 0.0f && p.x <= c.fn && p.y <= c.fn && p.z <= c.fn)) {
+    vidx = -1;
+    return 0u;
+  }
+  int32_t i = int32_t(__builtin_floorf(p.x));
+  int32_t j = int32_t(__builtin_floorf(p.y));
+  int32_t k = int32_t(__builtin_floorf(p.z));
+  i = i >= c.n ? i - c.n : i;
+  j = j >= c.n ? j - c.n : j;
+  k = k >= c.n ? k - c.n : k;
+  vidx = i + (j + k * c.n) * c.n;
+  return c.vox[vidx];
+}
+
+__device__ __forceinline__ bool test_cube(f3 p, f3 d, float fn) {
+  const float hi = fn * 0.5f + fn / 2.0f, lo = fn * 0.5f - fn / 2.0f;
+  return !((p.x > hi && d.x > 0.0f) || (p.x < lo && d.x < 0.0f) || (p.y > hi && d.y > 0.0f) ||
+           (p.y < lo && d.y < 0.0f) || (p.z > hi && d.z > 0.0f) || (p.z < lo && d.z < 0.0f));
+}
+
+__device__ __forceinline__ float next_plane(float d, float p) {
+  return d < 0.0f ? __builtin_ceilf(p - 1.0f) : __builtin_floorf(p + 1.0f);
+}
+
+__device__ __forceinline__ f3 initial_t(f3 dir, f3 cur, f3 pos) {
+  return mk((next_plane(dir.x, cur.x) - pos.x) / dir.x, (next_plane(dir.y, cur.y) - pos.y) / dir.y,
+            (next_plane(dir.z, cur.z) - pos.z) / dir.z);
+}
+
+__device__ __forceinline__ f3 sign3(f3 d) { return mk(gsign(d.x), gsign(d.y), gsign(d.z)); }
+
+// GetReflectionRay (voxel.glsl:203-215)
+__device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
+  Ray r;
+  r.voxel = 0;
+  r.pos = h.point;
+  r.dir = randomize(reflect3(ray.dir, h.normal), h.point, c.refl_noise, c.time);
+  r.len = h.len;
+  r.energy = ray.energy * (1.0f - dot3(mk(-h.normal.x, -h.normal.y, -h.normal.z), ray.dir));
+  r.rdepth = ray.rdepth + 1;
+  r.tdepth = ray.tdepth;
+  return r;
+}
+
+// GetRefractionRay (voxel.glsl:217-246)
+__device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counters& k) {
+  int32_t dummy;
+  const uint32_t outv = get_voxel(c, h.point + h.normal * 0.5f, dummy);
+  const uint32_t inv = get_voxel(c, h.point - h.normal * 0.5f, dummy);
+  k.c[VRT_CNT_REFRACTION_PROBES]++;
+  const float eta = mat_refr(outv) / mat_refr(inv);
+  Ray r;
+  r.voxel = h.voxel;
+  r.pos = h.point;
+  r.dir = refract3(normalize3(ray.dir), h.normal, eta);
+  if (r.dir.x == 0.0f && r.dir.y == 0.0f && r.dir.z == 0.0f) {  // total internal reflection
+    r = reflection_ray(c, ray, h);
+    r.voxel = ray.voxel;
+    r.energy = ray.energy;
+  } else {
+    r.dir = randomize(r.dir, r.pos, c.refr_noise, c.time);
+    r.energy = ray.energy;
+    if (ray.voxel == 0) r.energy *= 1.0f - mat_color(mat_id(h.voxel)).w;
+  }
+  r.len = h.len;
+  r.rdepth = ray.rdepth;
+  r.tdepth = ray.tdepth + 1;
+  return r;
+}
+
+// RayMarchShadow (voxel.glsl:259-300)
+__device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
+                             uint32_t& flags) {
+  float len = ray.len;
+  f3 cur = ray.pos;
+  f3 t = initial_t(ray.dir, cur, ray.pos);
+  const f3 step = sign3(ray.dir);
+  for (uint32_t it = 0; len < c.max_len; ++it) {
+    if (!test_cube(cur, ray.dir, c.fn)) return false;
+    if (it >= VRT_MAX_STEPS) {
+      k.c[VRT_CNT_STEP_CAP]++;
+      flags |= VRT_HIT_FLAG_STEP_CAP;
+      return false;
+    }
+    steps++;
+    k.c[VRT_CNT_SHADOW_STEPS]++;
+    const float tmin = gmin(t.x, gmin(t.y, t.z));
+    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+    len += tmin;
+    const float s = len - ray.len;
+    cur = ray.pos + s * ray.dir;
+    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
+    const f3 smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
+                      cur.z + (0.5f * float(ez)) * step.z);
+    int32_t vidx;
+    const uint32_t v = get_voxel(c, smp, vidx);
+    int index = int(ey) + 2 * int(ez);
+    if (index > 2) {
+      index = 2;
+      k.c[VRT_CNT_TIE3]++;
+      flags |= VRT_HIT_FLAG_TIE3;
+    }
+    if (v != 0 && !mat_transparent(v)) return true;
+    const float q = ((comp(cur, index) + comp(step, index)) - comp(ray.pos, index)) /
+                        comp(ray.dir, index) - s;
+    set_comp(t, index, q);
+  }
+  return false;
+}
+
+// RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
+__device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
+  Hit miss;
+  miss.found = false;
+  miss.vidx = -1;
+  miss.len = 0.0f;
+  miss.voxel = 0;
+  miss.point = mk(0.0f, 0.0f, 0.0f);
+  miss.normal = miss.point;
+  float len = ray.len;
+  f3 cur = ray.pos;
+  f3 t = initial_t(ray.dir, cur, ray.pos);
+  f3 step = sign3(ray.dir);
+  uint32_t ray_voxel = ray.voxel;
+  int internal = 0;
+  for (uint32_t it = 0; len < c.max_len; ++it) {
+    if (!test_cube(cur, ray.dir, c.fn)) return miss;
+    if (it >= VRT_MAX_STEPS) {
+      k.c[VRT_CNT_STEP_CAP]++;
+      flags |= VRT_HIT_FLAG_STEP_CAP;
+      return miss;
+    }
+    steps++;
+    k.c[VRT_CNT_DDA_STEPS]++;
+    const float tmin = gmin(t.x, gmin(t.y, t.z));
+    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+    len += tmin;
+    const float s = len - ray.len;
+    cur = ray.pos + s * ray.dir;
+    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
+    const f3 smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
+                      cur.z + (0.5f * float(ez)) * step.z);
+    int32_t vidx;
+    const uint32_t v = get_voxel(c, smp, vidx);
+    int index = int(ey) + 2 * int(ez);
+    if (index > 2) {
+      index = 2;
+      k.c[VRT_CNT_TIE3]++;
+      flags |= VRT_HIT_FLAG_TIE3;
+    }
+    if (v != 0 && v != ray_voxel) {
+      Hit h;
+      h.found = true;
+      h.voxel = v;
+      h.vidx = vidx;
+      h.point = cur;
+      h.len = len;
+      h.normal = mk(0.0f, 0.0f, 0.0f);
+      set_comp(h.normal, index, -gsign(comp(ray.dir, index)));
+      return h;
+    } else if (ray_voxel != 0 && v == 0) {  // leaving a transparent voxel (:357-380)
+      Hit h;
+      h.found = true;
+      h.voxel = 0;
+      h.vidx = vidx;
+      h.point = cur;
+      h.len = len;
+      h.normal = mk(0.0f, 0.0f, 0.0f);
+      set_comp(h.normal, index, -gsign(comp(ray.dir, index)));
+      const f3 old_dir = ray.dir;
+      ray = refraction_ray(c, ray, h, k);
+      ray.tdepth--;
+      if (ray.voxel == ray_voxel) {
+        internal++;
+        if (internal > 10) {
+          ray.dir = old_dir;
+          ray.voxel = 0;
+        }
+      }
+      ray_voxel = ray.voxel;
+      t = initial_t(ray.dir, cur, ray.pos);
+      step = sign3(ray.dir);
+    }
+    const float q = ((comp(cur, index) + comp(step, index)) - comp(ray.pos, index)) /
+                        comp(ray.dir, index) - (len - ray.len);
+    set_comp(t, index, q);
+  }
+  return miss;
+}
+
+constexpr int kMaxStack = 17;
+
+// fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
+__global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __restrict__ vox,
+                                                     float4* __restrict__ out,
+                                                     vrt_hit* __restrict__ hits,
+                                                     unsigned long long* __restrict__ counters) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+  const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const bool valid = px < a.width && li < a.rows;
+
+  Counters k;
+#pragma unroll
+  for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
+
+  if (valid) {
+    Ctx c;
+    c.vox = vox;
+    c.n = a.n;
+    c.fn = a.fn;
+    c.max_len = a.max_len;
+    c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
+    c.sun_n = normalize3(c.sun);
+    c.time = a.time;
+    c.refl_noise = a.refl_noise;
+    c.refr_noise = a.refr_noise;
+
+    const int py = a.row0 + li * a.row_step;
+    const float ndx = (2.0f * (float(px) + 0.5f)) / float(a.width) - 1.0f;
+    const float ndy = (2.0f * (float(py) + 0.5f)) / float(a.height) - 1.0f;
+    float n4[4], f4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float base = a.inv_pv[0 * 4 + i] * ndx + a.inv_pv[1 * 4 + i] * ndy;
+      n4[i] = (base + a.inv_pv[2 * 4 + i] * -1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
+      f4[i] = (base + a.inv_pv[2 * 4 + i] * 1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
+    }
+    const f3 vnear = mk(n4[0] / n4[3], n4[1] / n4[3], n4[2] / n4[3]);
+    const f3 vdir = mk(f4[0] / f4[3], f4[1] / f4[3], f4[2] / f4[3]) - vnear;
+
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    Ray stack[kMaxStack];
+    const int cap = a.max_refl + a.max_transp + 1;
+    stack[0].pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
+    stack[0].dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);
+    stack[0].len = 0.0f;
+    stack[0].energy = 1.0f;
+    stack[0].voxel = 0;
+    stack[0].rdepth = 0;
+    stack[0].tdepth = 0;
+    int sp = 1;
+    uint32_t steps = 0, flags = 0;
+    int32_t hit_vidx = -1;
+    float hit_len = 0.0f;
+    bool first = true;
+    k.c[VRT_CNT_PIXELS] = 1;
+    k.c[VRT_CNT_PRIMARY_RAYS] = 1;
+    while (sp > 0) {
+      Ray ray = stack[--sp];
+      if (!first) k.c[VRT_CNT_SECONDARY_RAYS]++;
+      // TraceWithShadow (voxel.glsl:395-423)
+      const Hit h = march(c, ray, k, steps, flags);
+      if (h.found) {
+        Ray sr;
+        sr.voxel = h.voxel;
+        sr.pos = h.point;
+        sr.dir = c.sun_n;
+        sr.len = h.len;
+        sr.energy = ray.energy;
+        sr.rdepth = 0;
+        sr.tdepth = 0;
+        k.c[VRT_CNT_SHADOW_RAYS]++;
+        const bool in_shadow = march_shadow(c, sr, k, steps, flags);
+        const uint32_t m = mat_id(h.voxel);
+        float brightness;
+        if (in_shadow) {
+          brightness = kAmbient;
+        } else {
+          const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sr.dir), 0.0f);
+          const float specular =
+              mat_ks(m) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m));
+          brightness = kAmbient + diffuse + specular;
+        }
+        const float4 col = mat_color(m);
+        const float e = ray.energy;
+        color.x = mixf(color.x, col.x * col.w * brightness, e);
+        color.y = mixf(color.y, col.y * col.w * brightness, e);
+        color.z = mixf(color.z, col.z * col.w * brightness, e);
+      } else {
+        // GetSkyboxColor (:386-393), then the second mix at :420
+        const f3 u = normalize3(ray.dir);
+        const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
+        const float grad = (u.y + 1.0f) * 0.5f;
+        const float sy = gmax(c.sun.y, 0.0f);
+        const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
+        const float a1 = 1.0f - ray.energy;
+        const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
+        color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
+      }
+      if (first) {
+        if (h.found) {
+          hit_vidx = h.vidx;
+          hit_len = h.len;
+        }
+        first = false;
+      }
+      if (h.found) {
+        const uint32_t m = mat_id(h.voxel);
+        if (mat_reflective(m) && ray.rdepth < a.max_refl) {
+          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
+          else flags |= VRT_HIT_FLAG_STACK_FULL;
+        }
+        if (mat_transparent(m) && ray.tdepth < a.max_transp && mat_color(m).w != 1.0f) {
+          if (sp < cap) stack[sp++] = refraction_ray(c, ray, h, k);
+          else flags |= VRT_HIT_FLAG_STACK_FULL;
+        }
+      }
+    }
+    const size_t o = size_t(li) * size_t(a.width) + size_t(px);
+    out[o] = make_float4(color.x, color.y, color.z, 1.0f);
+    if (hits) {
+      vrt_hit hr;
+      hr.voxel_index = hit_vidx;
+      hr.ray_length = hit_len;
+      hr.steps = steps;
+      hr.flags = flags;
+      hits[o] = hr;
+    }
+  }
+
+  if (counters) {
+#pragma unroll
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) {
+      unsigned long long v = k.c[q];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0 && v) atomicAdd(counters + q, v);
+    }
+  }
+}
+
+}  // namespace vrt
+
+// ---------------------------------------------------------------------------- C-ABI context --
+
+struct vrt_ctx {
+  int device = 0;
+  uint8_t* d_vox = nullptr;
+  int32_t n = 0;
+  float4* d_out = nullptr;
+  vrt_hit* d_hit = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  size_t out_pixels = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+};
+
+namespace {
+
+int fail(vrt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(vrt_ctx* c, hipError_t e, const char* what) {
+  return fail(c, VRT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define VRT_HIP(ctx, call)                                      \
+  do {                                                          \
+    hipError_t e_ = (call);                                     \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);    \
+  } while (0)
+
+int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) {
+  if (!cam || !p) return fail(ctx, VRT_ERR_INVALID, "null camera or params");
+  if (!ctx->d_vox) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
+  if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
+    return fail(ctx, VRT_ERR_INVALID, "bad image size");
+  if (!p->color_only)
+    return fail(ctx, VRT_ERR_UNSUPPORTED, "textured mode is not in ABI v1 (color_only must be 1)");
+  if (p->max_reflections < 0 || p->max_transparencies < 0 ||
+      p->max_reflections + p->max_transparencies + 1 > vrt::kMaxStack)
+    return fail(ctx, VRT_ERR_UNSUPPORTED, "max_reflections + max_transparencies must be <= 16");
+  return VRT_OK;
+}
+
+vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                     int32_t rows, int32_t row_step) {
+  vrt::KArgs a;
+  std::memcpy(a.inv_pv, cam->inv_pv, sizeof(a.inv_pv));
+  std::memcpy(a.sun, p->sun_dir, sizeof(a.sun));
+  a.time = p->time;
+  a.ray_noise = p->ray_noise;
+  a.refl_noise = p->reflection_noise;
+  a.refr_noise = p->refraction_noise;
+  a.max_len = p->max_ray_length;
+  a.n = ctx->n;
+  a.fn = float(ctx->n);
+  a.width = cam->width;
+  a.height = cam->height;
+  a.row0 = row0;
+  a.rows = rows;
+  a.row_step = row_step;
+  a.max_refl = p->max_reflections;
+  a.max_transp = p->max_transparencies;
+  return a;
+}
+
+void launch(const vrt::KArgs& a, const uint8_t* vox, float4* out, vrt_hit* hit,
+            unsigned long long* cnt, hipStream_t s) {
+  dim3 grid((a.width + 15) / 16, (a.rows + 15) / 16);
+  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(256), 0, s, a, vox, out, hit, cnt);
+}
+
+}  // namespace
+
+extern "C" {
+
+int vrt_create(int device, vrt_ctx** out) {
+  if (!out) return VRT_ERR_INVALID;
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) return VRT_ERR_DEVICE;
+  if (device < 0 || device >= count) return VRT_ERR_INVALID;
+  vrt_ctx* c = new vrt_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipEventCreate(&c->ev0) != hipSuccess ||
+      hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return VRT_ERR_DEVICE;
+  }
+  *out = c;
+  return VRT_OK;
+}
+
+void vrt_destroy(vrt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->d_vox) (void)hipFree(c->d_vox);
+  if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_hit) (void)hipFree(c->d_hit);
+  if (c->d_cnt) (void)hipFree(c->d_cnt);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+}
+
+const char* vrt_last_error(const vrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!vol || !vol->voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
+  const int32_t n = vol->n;
+  if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
+    return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t bytes = size_t(n) * n * n;
+  if (ctx->d_vox && ctx->n != n) {
+    (void)hipFree(ctx->d_vox);
+    ctx->d_vox = nullptr;
+  }
+  if (!ctx->d_vox) {
+    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess) {
+      ctx->d_vox = nullptr;
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume");
+    }
+  }
+  ctx->n = n;
+  VRT_HIP(ctx, hipMemcpy(ctx->d_vox, vol->voxels, bytes, hipMemcpyHostToDevice));
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->d_vox : nullptr; }
+
+int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                          int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,
+                          uint64_t* d_counters, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
+  if (rows < 0 || row_step < 1 || row0 < 0 ||
+      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
+    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
+  if (rows == 0) return VRT_OK;
+  const vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
+  launch(a, ctx->d_vox, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
+         reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* out_rgba,
+               vrt_hit* out_hit, vrt_stats* stats) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t pixels = size_t(cam->width) * cam->height;
+  if (pixels > ctx->out_pixels) {
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    if (ctx->d_hit) (void)hipFree(ctx->d_hit);
+    ctx->d_out = nullptr;
+    ctx->d_hit = nullptr;
+    ctx->out_pixels = 0;
+    if (hipMalloc(&ctx->d_out, pixels * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&ctx->d_hit, pixels * sizeof(vrt_hit)) != hipSuccess)
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc frame buffers");
+    ctx->out_pixels = pixels;
+  }
+  if (!ctx->d_cnt) VRT_HIP(ctx, hipMalloc(&ctx->d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT));
+  VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
+  const vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
+  VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
+  launch(a, ctx->d_vox, ctx->d_out, out_hit ? ctx->d_hit : nullptr, ctx->d_cnt, nullptr);
+  VRT_HIP(ctx, hipGetLastError());
+  VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
+  VRT_HIP(ctx, hipMemcpy(out_rgba, ctx->d_out, pixels * sizeof(float4), hipMemcpyDeviceToHost));
+  if (out_hit)
+    VRT_HIP(ctx, hipMemcpy(out_hit, ctx->d_hit, pixels * sizeof(vrt_hit), hipMemcpyDeviceToHost));
+  if (stats) {
+    unsigned long long h[VRT_CNT_COUNT];
+    VRT_HIP(ctx, hipMemcpy(h, ctx->d_cnt, sizeof(h), hipMemcpyDeviceToHost));
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) stats->counters[q] = h[q];
+    float ms = 0.0f;
+    VRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    stats->kernel_ms = ms;
+  }
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+}  // extern "C"

@@ -153,6 +153,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
             f"{path} is missing: build it with `make` (or __graft_entry__.build()); "
             "the voxel ray tracer has no CPU fallback"
         )
+    # One HIP runtime per process: if PyTorch is installed, let it load its libamdhip64.so.7 first
+    # so the library binds to the same runtime (same soname) instead of /opt/rocm's copy; torch
+    # tensors' device pointers are then valid in vrt_render_rows_async.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

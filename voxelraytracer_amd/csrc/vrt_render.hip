@@ -131,14 +131,15 @@ struct Counters {
 
 struct Ctx {
   const uint8_t* __restrict__ vox;
-  int32_t n;
+  int32_t n, lg;  // N and log2(N)
   float fn;
   float max_len;
   f3 sun, sun_n;
   float time, refl_noise, refr_noise;
 };
 
-// GetVoxel (voxel.glsl:149-154): `>` bounds test, NEAREST + GL_REPEAT, NaN reads 0.
+// GetVoxel (voxel.glsl:149-154): `>` bounds test, NEAREST + GL_REPEAT, NaN reads 0. Reference
+// form, used off the hot loop (refraction probes).
 __device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p, int32_t& vidx) {
   if (!(p.x >= 0.0f && p.y >= 0.0f && p.z >= 0.0f && p.x <= c.fn && p.y <= c.fn && p.z <= c.fn)) {
     vidx = -1;
@@ -154,10 +155,12 @@ __device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p, int32_t& vidx)
   return c.vox[vidx];
 }
 
+// TestCube (voxel.glsl:248-257) with centre N/2 and size N; bitwise ops, no short-circuit branches.
 __device__ __forceinline__ bool test_cube(f3 p, f3 d, float fn) {
   const float hi = fn * 0.5f + fn / 2.0f, lo = fn * 0.5f - fn / 2.0f;
-  return !((p.x > hi && d.x > 0.0f) || (p.x < lo && d.x < 0.0f) || (p.y > hi && d.y > 0.0f) ||
-           (p.y < lo && d.y < 0.0f) || (p.z > hi && d.z > 0.0f) || (p.z < lo && d.z < 0.0f));
+  const bool out = (p.x > hi & d.x > 0.0f) | (p.x < lo & d.x < 0.0f) | (p.y > hi & d.y > 0.0f) |
+                   (p.y < lo & d.y < 0.0f) | (p.z > hi & d.z > 0.0f) | (p.z < lo & d.z < 0.0f);
+  return !out;
 }
 
 __device__ __forceinline__ float next_plane(float d, float p) {
@@ -170,6 +173,171 @@ __device__ __forceinline__ f3 initial_t(f3 dir, f3 cur, f3 pos) {
 }
 
 __device__ __forceinline__ f3 sign3(f3 d) { return mk(gsign(d.x), gsign(d.y), gsign(d.z)); }
+
+__device__ __forceinline__ float sel3(int axis, float x, float y, float z) {
+  return axis == 2 ? z : (axis == 1 ? y : x);
+}
+
+// a / d correctly rounded, given y = RN(1/d) (Markstein's theorem: q1 is within one ulp of a/d,
+// so r1 = a - d*q1 is exact and RN(q1 + r1*y) = RN(a/d); no over/underflow for the fast-path
+// operand ranges, see fast_path_ok). Bit-identical to IEEE division, 5 VALU ops instead of the
+// ~11 of the scaled div_scale/div_fmas/div_fixup sequence.
+__device__ __forceinline__ float div_rn(float a, float d, float y) {
+  const float q0 = a * y;
+  const float r0 = __builtin_fmaf(-d, q0, a);
+  const float q1 = __builtin_fmaf(r0, y, q0);
+  const float r1 = __builtin_fmaf(-d, q1, a);
+  return __builtin_fmaf(r1, y, q1);
+}
+
+// The fast walk needs every direction component normal and not tiny: then every t stays finite
+// and non-negative-zero (so v_min3 == GLSL min) and div_rn is exact. Otherwise (a +-0 component:
+// +-inf / NaN t values, where the GLSL would spin) the walk replays the reference literally.
+__device__ __forceinline__ bool fast_path_ok(f3 d) {
+  const float lo = 0x1p-64f;
+  return __builtin_fabsf(d.x) >= lo && __builtin_fabsf(d.y) >= lo && __builtin_fabsf(d.z) >= lo &&
+         __builtin_fabsf(d.x) <= 1.0e4f && __builtin_fabsf(d.y) <= 1.0e4f &&
+         __builtin_fabsf(d.z) <= 1.0e4f;
+}
+
+struct WalkState {
+  f3 t;            // distance to the next plane per axis, relative to the current step
+  f3 cur;          // currentPos
+  float len;       // rayLength
+  uint32_t it;     // iterations of this RayMarch/RayMarchShadow call (VRT_MAX_STEPS cap)
+  uint32_t ties;   // index==3 events
+  bool check_cube; // TestCube can only fail after a sample outside [0,N]^3
+};
+
+enum : int { WALK_MISS = 0, WALK_EVENT = 1, WALK_CAP = 2 };
+
+// floor(x) -> int in one VALU op; x is already clamped to [0, N] by the caller
+__device__ __forceinline__ uint32_t cvt_flr(float x) {
+  int32_t r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return uint32_t(r);
+}
+
+// keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
+__device__ __forceinline__ float opaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// The DDA loop of RayMarch / RayMarchShadow (voxel.glsl:273-298, :317-382) up to the first event.
+// Event: SHADOW -> an opaque voxel (HasVoxel && !transparent); otherwise the sampled byte differs
+// from the ray's medium, which covers both the hit (:353) and the leave-transparent case (:357).
+// Every float op of a step is the reference's, in its order; only their scheduling differs: the
+// t update of a step (which does not depend on the voxel) is issued before the voxel test so it
+// overlaps the load, and is simply not used when the step ends in an event.
+template <bool SHADOW, bool EXACT>
+__device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir, float len0,
+                                        uint32_t medium, WalkState& w, int& axis_out,
+                                        int32_t& vidx_out, uint32_t& v_out) {
+  const f3 step = sign3(dir);
+  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
+  f3 rcp = mk(1.0f, 1.0f, 1.0f);
+  if (!EXACT) rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
+  // TestCube per axis as one compare: sign(d)*p > bound (bound = +inf on a zero axis)
+  const float hi = c.fn * 0.5f + c.fn / 2.0f, lo = c.fn * 0.5f - c.fn / 2.0f;
+  const f3 cb = mk(dir.x > 0.0f ? hi : (dir.x < 0.0f ? -lo : __builtin_inff()),
+                   dir.y > 0.0f ? hi : (dir.y < 0.0f ? -lo : __builtin_inff()),
+                   dir.z > 0.0f ? hi : (dir.z < 0.0f ? -lo : __builtin_inff()));
+  const f3 cs = mk(dir.x < 0.0f ? -1.0f : 1.0f, dir.y < 0.0f ? -1.0f : 1.0f,
+                   dir.z < 0.0f ? -1.0f : 1.0f);
+  const uint32_t m = uint32_t(c.n - 1);
+  const uint32_t lg = uint32_t(c.lg);
+  f3 t = w.t, cur = w.cur;
+  float len = w.len;
+  uint32_t it = w.it, ties = w.ties;
+  // loop-top tests of the reference for the first iteration: length, TestCube, (step cap)
+  bool cube_out = w.check_cube && !test_cube(cur, dir, c.fn);
+  if (!(len < c.max_len) | cube_out | (it >= VRT_MAX_STEPS)) {
+    w.check_cube = cube_out;
+    return (len < c.max_len && !cube_out) ? WALK_CAP : WALK_MISS;
+  }
+  // live-out state kept in VGPRs (a bool live out of a divergent loop costs SALU mask merges
+  // every iteration): status = event | inb << 1 | cube_out << 2
+  uint32_t status, v, idx;
+  int axis;
+  for (;;) {
+    ++it;
+    float tmin;
+    if (EXACT) tmin = gmin(t.x, gmin(t.y, t.z));
+    else tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
+    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+    len += tmin;
+    const float s = len - len0;
+    cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
+    f3 smp;
+    if (EXACT) {
+      smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
+               cur.z + (0.5f * float(ez)) * step.z);
+    } else {  // same voxel: the +-0 added on an un-crossed axis only flips the sign of a zero
+      smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f), cur.z + (ez ? hs.z : 0.0f));
+    }
+    // branch-free fetch: clamp to [0,N] (med3; NaN -> in range), floor, wrap N -> 0 (GL_REPEAT,
+    // power-of-two N); the sample is inside iff clamping left it unchanged (NaN: outside)
+    const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+    const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+    const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+    const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
+    idx = (cvt_flr(qx) & m) | ((cvt_flr(qy) & m) << lg) | ((cvt_flr(qz) & m) << (2u * lg));
+    v = c.vox[idx];
+    ties += (ey & ez) ? 1u : 0u;
+    axis = ez ? 2 : (ey ? 1 : 0);
+    // t update for the crossed axis (voxel.glsl:296/381), computed while the load is in flight
+    // (unconditionally: after an event t is dead)
+    const float pa = sel3(axis, pos.x, pos.y, pos.z);
+    const float da = sel3(axis, dir.x, dir.y, dir.z);
+    const float ca = sel3(axis, cur.x, cur.y, cur.z);
+    const float sa = sel3(axis, step.x, step.y, step.z);
+    const float num = (ca + sa) - pa;
+    float q;
+    if (EXACT) q = num / da;
+    else q = div_rn(num, da, sel3(axis, rcp.x, rcp.y, rcp.z));
+    q = q - s;
+    t = mk(axis == 0 ? q : t.x, axis == 1 ? q : t.y, axis == 2 ? q : t.z);
+    // loop-top tests of the NEXT iteration; TestCube can only fail after an outside sample
+    bool cube_next;
+    if (EXACT) cube_next = !inb && !test_cube(cur, dir, c.fn);
+    else cube_next = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
+    const bool stop = !(len < c.max_len) | cube_next | (it >= VRT_MAX_STEPS);
+    // outside samples read 0 (GetVoxel :151-152)
+    bool event;
+    if (SHADOW) event = inb & (v != 0u) & (v != 2u);
+    else event = inb ? (v != medium) : (medium != 0u);
+    status = (event ? 1u : 0u) | (inb ? 2u : 0u) | (cube_next ? 4u : 0u);
+    asm volatile("" : "+v"(status));
+    if (event | stop) break;
+  }
+  w.t = t;
+  w.cur = cur;
+  w.len = len;
+  w.it = it;
+  w.ties = ties;
+  const bool inb = (status & 2u) != 0u;
+  if (status & 1u) {
+    axis_out = axis;
+    vidx_out = inb ? int32_t(idx) : -1;
+    v_out = inb ? v : 0u;
+    w.check_cube = !inb;  // on re-entry (new direction after a refraction): re-test iff outside
+    return WALK_EVENT;
+  }
+  cube_out = (status & 4u) != 0u;
+  w.check_cube = cube_out;
+  return (len < c.max_len && !cube_out) ? WALK_CAP : WALK_MISS;
+}
+
+template <bool SHADOW>
+__device__ __forceinline__ int walk(const Ctx& c, const f3 pos, const f3 dir, float len0,
+                                    uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
+                                    uint32_t& v) {
+  if (__builtin_expect(fast_path_ok(dir), 1))
+    return dda_walk<SHADOW, false>(c, pos, dir, len0, medium, w, axis, vidx, v);
+  return dda_walk<SHADOW, true>(c, pos, dir, len0, medium, w, axis, vidx, v);
+}
 
 // GetReflectionRay (voxel.glsl:203-215)
 __device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
@@ -210,124 +378,101 @@ __device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counte
   return r;
 }
 
-// RayMarchShadow (voxel.glsl:259-300)
+// RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
-  float len = ray.len;
-  f3 cur = ray.pos;
-  f3 t = initial_t(ray.dir, cur, ray.pos);
-  const f3 step = sign3(ray.dir);
-  for (uint32_t it = 0; len < c.max_len; ++it) {
-    if (!test_cube(cur, ray.dir, c.fn)) return false;
-    if (it >= VRT_MAX_STEPS) {
-      k.c[VRT_CNT_STEP_CAP]++;
-      flags |= VRT_HIT_FLAG_STEP_CAP;
-      return false;
-    }
-    steps++;
-    k.c[VRT_CNT_SHADOW_STEPS]++;
-    const float tmin = gmin(t.x, gmin(t.y, t.z));
-    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
-    len += tmin;
-    const float s = len - ray.len;
-    cur = ray.pos + s * ray.dir;
-    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
-    const f3 smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
-                      cur.z + (0.5f * float(ez)) * step.z);
-    int32_t vidx;
-    const uint32_t v = get_voxel(c, smp, vidx);
-    int index = int(ey) + 2 * int(ez);
-    if (index > 2) {
-      index = 2;
-      k.c[VRT_CNT_TIE3]++;
-      flags |= VRT_HIT_FLAG_TIE3;
-    }
-    if (v != 0 && !mat_transparent(v)) return true;
-    const float q = ((comp(cur, index) + comp(step, index)) - comp(ray.pos, index)) /
-                        comp(ray.dir, index) - s;
-    set_comp(t, index, q);
+  WalkState w;
+  w.len = ray.len;
+  w.cur = ray.pos;
+  w.t = initial_t(ray.dir, ray.pos, ray.pos);
+  w.it = 0;
+  w.ties = 0;
+  w.check_cube = true;
+  int axis;
+  int32_t vidx;
+  uint32_t v;
+  const int r = walk<true>(c, ray.pos, ray.dir, ray.len, 0u, w, axis, vidx, v);
+  steps += w.it;
+  k.c[VRT_CNT_SHADOW_STEPS] += w.it;
+  k.c[VRT_CNT_TIE3] += w.ties;
+  if (w.ties) flags |= VRT_HIT_FLAG_TIE3;
+  if (r == WALK_CAP) {
+    k.c[VRT_CNT_STEP_CAP]++;
+    flags |= VRT_HIT_FLAG_STEP_CAP;
   }
-  return false;
+  return r == WALK_EVENT;
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
-  Hit miss;
-  miss.found = false;
-  miss.vidx = -1;
-  miss.len = 0.0f;
-  miss.voxel = 0;
-  miss.point = mk(0.0f, 0.0f, 0.0f);
-  miss.normal = miss.point;
-  float len = ray.len;
-  f3 cur = ray.pos;
-  f3 t = initial_t(ray.dir, cur, ray.pos);
-  f3 step = sign3(ray.dir);
-  uint32_t ray_voxel = ray.voxel;
+  Hit h;
+  h.found = false;
+  h.vidx = -1;
+  h.len = 0.0f;
+  h.voxel = 0;
+  h.point = mk(0.0f, 0.0f, 0.0f);
+  h.normal = h.point;
+  WalkState w;
+  w.len = ray.len;
+  w.cur = ray.pos;
+  w.t = initial_t(ray.dir, ray.pos, ray.pos);
+  w.it = 0;
+  w.ties = 0;
+  w.check_cube = true;
+  uint32_t medium = ray.voxel;
   int internal = 0;
-  for (uint32_t it = 0; len < c.max_len; ++it) {
-    if (!test_cube(cur, ray.dir, c.fn)) return miss;
-    if (it >= VRT_MAX_STEPS) {
-      k.c[VRT_CNT_STEP_CAP]++;
-      flags |= VRT_HIT_FLAG_STEP_CAP;
-      return miss;
-    }
-    steps++;
-    k.c[VRT_CNT_DDA_STEPS]++;
-    const float tmin = gmin(t.x, gmin(t.y, t.z));
-    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
-    len += tmin;
-    const float s = len - ray.len;
-    cur = ray.pos + s * ray.dir;
-    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
-    const f3 smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
-                      cur.z + (0.5f * float(ez)) * step.z);
+  int r;
+  for (;;) {
+    int axis;
     int32_t vidx;
-    const uint32_t v = get_voxel(c, smp, vidx);
-    int index = int(ey) + 2 * int(ez);
-    if (index > 2) {
-      index = 2;
-      k.c[VRT_CNT_TIE3]++;
-      flags |= VRT_HIT_FLAG_TIE3;
-    }
-    if (v != 0 && v != ray_voxel) {
-      Hit h;
+    uint32_t v;
+    r = walk<false>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    if (r != WALK_EVENT) break;
+    f3 normal = mk(0.0f, 0.0f, 0.0f);
+    set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
+    if (v != 0u) {  // HasVoxel(voxel) && voxel != rayVoxel (:353)
       h.found = true;
       h.voxel = v;
       h.vidx = vidx;
-      h.point = cur;
-      h.len = len;
-      h.normal = mk(0.0f, 0.0f, 0.0f);
-      set_comp(h.normal, index, -gsign(comp(ray.dir, index)));
-      return h;
-    } else if (ray_voxel != 0 && v == 0) {  // leaving a transparent voxel (:357-380)
-      Hit h;
-      h.found = true;
-      h.voxel = 0;
-      h.vidx = vidx;
-      h.point = cur;
-      h.len = len;
-      h.normal = mk(0.0f, 0.0f, 0.0f);
-      set_comp(h.normal, index, -gsign(comp(ray.dir, index)));
-      const f3 old_dir = ray.dir;
-      ray = refraction_ray(c, ray, h, k);
-      ray.tdepth--;
-      if (ray.voxel == ray_voxel) {
-        internal++;
-        if (internal > 10) {
-          ray.dir = old_dir;
-          ray.voxel = 0;
-        }
-      }
-      ray_voxel = ray.voxel;
-      t = initial_t(ray.dir, cur, ray.pos);
-      step = sign3(ray.dir);
+      h.point = w.cur;
+      h.len = w.len;
+      h.normal = normal;
+      break;
     }
-    const float q = ((comp(cur, index) + comp(step, index)) - comp(ray.pos, index)) /
-                        comp(ray.dir, index) - (len - ray.len);
-    set_comp(t, index, q);
+    // rayVoxel != 0 && voxel == 0: leaving a transparent voxel, refract in place (:357-380)
+    Hit e;
+    e.found = true;
+    e.voxel = 0;
+    e.vidx = vidx;
+    e.point = w.cur;
+    e.len = w.len;
+    e.normal = normal;
+    const f3 old_dir = ray.dir;
+    ray = refraction_ray(c, ray, e, k);
+    ray.tdepth--;
+    if (ray.voxel == medium) {
+      internal++;
+      if (internal > 10) {
+        ray.dir = old_dir;
+        ray.voxel = 0;
+      }
+    }
+    medium = ray.voxel;
+    w.t = initial_t(ray.dir, w.cur, ray.pos);
+    const f3 step = sign3(ray.dir);
+    const float q = ((comp(w.cur, axis) + comp(step, axis)) - comp(ray.pos, axis)) /
+                        comp(ray.dir, axis) - (w.len - ray.len);
+    set_comp(w.t, axis, q);
   }
-  return miss;
+  steps += w.it;
+  k.c[VRT_CNT_DDA_STEPS] += w.it;
+  k.c[VRT_CNT_TIE3] += w.ties;
+  if (w.ties) flags |= VRT_HIT_FLAG_TIE3;
+  if (r == WALK_CAP) {
+    k.c[VRT_CNT_STEP_CAP]++;
+    flags |= VRT_HIT_FLAG_STEP_CAP;
+  }
+  return h;
 }
 
 constexpr int kMaxStack = 17;
@@ -350,6 +495,7 @@ __global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __r
     Ctx c;
     c.vox = vox;
     c.n = a.n;
+    c.lg = 31 - __builtin_clz(uint32_t(a.n));
     c.fn = a.fn;
     c.max_len = a.max_len;
     c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);

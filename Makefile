@@ -18,6 +18,11 @@ $(LIBDIR)/libvrt.so: $(SRC) include/vrt.h
 oracle:
 	$(MAKE) -C oracle
 
+# experiment variants for scripts/ab.py: make variant NAME=w5 DEFS="-DVRT_MIN_WAVES=5"
+variant: $(SRC) include/vrt.h
+	mkdir -p build/variants
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/libvrt_$(NAME).so $(SRC) -Wl,-rpath,/opt/rocm/lib
+
 asm: $(SRC) include/vrt.h
 	mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) -c --cuda-device-only -S -o build/asm/vrt_render.s voxelraytracer_amd/csrc/vrt_render.hip
@@ -27,4 +32,4 @@ clean:
 	rm -rf $(LIBDIR) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean variant

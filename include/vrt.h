@@ -115,7 +115,12 @@ int vrt_abi_version(void);
  * ownership of `vol->voxels`. N must be a power of two in [2, 1024]. */
 int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol);
 
-/* Device pointer of the resident volume (N^3 bytes), e.g. for a broadcast. NULL if none. */
+/* Same from a DEVICE buffer of N^3 bytes on this context's GPU (e.g. after an RCCL broadcast of
+ * the volume to every GPU of the node), ordered on `hip_stream`; returns after the copy. */
+int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream);
+
+/* Device pointer of the resident volume (N^3 bytes, canonical layout), e.g. for a broadcast.
+ * NULL if none. */
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
 
 /* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats

@@ -136,6 +136,12 @@ class Renderer:
         self._check(self._lib.vrt_upload_volume(self._h, C.byref(vol)), "vrt_upload_volume")
         self.n = n
 
+    def upload_volume_device(self, d_voxels: int, n: int, stream: int = 0):
+        """Upload from a device buffer (e.g. a torch uint8 CUDA tensor's data_ptr())."""
+        self._check(self._lib.vrt_upload_volume_device(self._h, d_voxels, n, stream or None),
+                    "vrt_upload_volume_device")
+        self.n = n
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libvrt.so")
+LIB_PATH = os.environ.get("VRT_LIB") or os.path.join(_HERE, "_lib", "libvrt.so")
 
 VRT_OK = 0
 VRT_ERR_INVALID = -1
@@ -95,6 +95,7 @@ SIGNATURES = {
     "vrt_destroy": (None, [C.c_void_p]),
     "vrt_last_error": (C.c_char_p, [C.c_void_p]),
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),
+    "vrt_upload_volume_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "vrt_volume_device_ptr": (C.c_void_p, [C.c_void_p]),
     "vrt_render": (
         C.c_int,

@@ -5,8 +5,13 @@
 // 8x8 sub-tile, so the 64 rays of a wave start coherent. Every float operation of the DDA is
 // replayed in the reference's order with -ffp-contract=off and correctly rounded div/sqrt, which
 // makes hit records bit-exact against the CPU oracle (DESIGN.md "Numerics").
+//
+// Device volume layout: (N+1)^3 bytes, x fastest, where plane N repeats plane 0 on each axis.
+// GetVoxel's texel for a coordinate c in [0, N] is then simply floor(c) (GL_REPEAT folded into
+// the layout), and the hot loop addresses it with two 24-bit multiply-adds.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -66,6 +71,7 @@ __device__ __forceinline__ f3 refract3(f3 i, f3 n, float eta) {
   const float s = eta * d + __builtin_sqrtf(k);
   return eta * i - s * n;
 }
+__device__ __forceinline__ f3 sign3(f3 d) { return mk(gsign(d.x), gsign(d.y), gsign(d.z)); }
 
 // Jenkins one-at-a-time mix, voxel.glsl:98-125
 __device__ __forceinline__ uint32_t hash1(uint32_t x) {
@@ -93,18 +99,18 @@ __device__ __forceinline__ f3 randomize(f3 dir, f3 pos, float randomness, float 
 
 // ------------------------------------------------------- materials (_COLOR_ONLY, :71-91) ----
 
-__device__ __forceinline__ float mat_refr(uint32_t b) { return b == 2 ? 1.5f : 1.0f; }
-__device__ __forceinline__ bool mat_transparent(uint32_t b) { return b == 0 || b == 2; }
-__device__ __forceinline__ bool mat_reflective(uint32_t b) { return b == 2; }
-__device__ __forceinline__ float mat_kd(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 0.4f); }
-__device__ __forceinline__ float mat_ks(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 0.2f); }
-__device__ __forceinline__ float mat_exp(uint32_t b) { return b == 0 ? 0.0f : (b == 2 ? 1.0f : 10.0f); }
-__device__ __forceinline__ float4 mat_color(uint32_t b) {
-  if (b == 1) return make_float4(0.5f, 0.5f, 0.5f, 1.0f);
-  if (b >= 3) return make_float4(0.05f, 0.5f, 0.1f, 1.0f);
+__device__ __forceinline__ uint32_t mat_id(uint32_t b) { return b > 3 ? 3 : b; }
+__device__ __forceinline__ float mat_refr(uint32_t b) { return mat_id(b) == 2 ? 1.5f : 1.0f; }
+__device__ __forceinline__ bool mat_transparent(uint32_t m) { return m == 0 || m == 2; }
+__device__ __forceinline__ bool mat_reflective(uint32_t m) { return m == 2; }
+__device__ __forceinline__ float mat_kd(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 0.4f); }
+__device__ __forceinline__ float mat_ks(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 0.2f); }
+__device__ __forceinline__ float mat_exp(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 10.0f); }
+__device__ __forceinline__ float4 mat_color(uint32_t m) {
+  if (m == 1) return make_float4(0.5f, 0.5f, 0.5f, 1.0f);
+  if (m == 3) return make_float4(0.05f, 0.5f, 0.1f, 1.0f);
   return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
-__device__ __forceinline__ uint32_t mat_id(uint32_t b) { return b > 3 ? 3 : b; }
 
 constexpr float kAmbient = 0.3f;
 
@@ -121,7 +127,7 @@ struct Hit {
   f3 point, normal;
   float len;
   uint32_t voxel;
-  int32_t vidx;
+  int32_t vidx;  // canonical index x + y*N + z*N*N of the texel read
   bool found;
 };
 
@@ -130,29 +136,36 @@ struct Counters {
 };
 
 struct Ctx {
-  const uint8_t* __restrict__ vox;
-  int32_t n, lg;  // N and log2(N)
+  const uint8_t* __restrict__ vox;  // padded (N+1)^3 layout
+  int32_t n;
+  uint32_t p;  // N + 1
   float fn;
   float max_len;
   f3 sun, sun_n;
   float time, refl_noise, refr_noise;
 };
 
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+  return __umul24(a, b) + c;  // v_mad_u32_u24 (operands < 2^24: N <= 1024)
+}
+
+__device__ __forceinline__ int32_t canonical_index(const Ctx& c, uint32_t i, uint32_t j, uint32_t k) {
+  const uint32_t n = uint32_t(c.n);
+  i = i == n ? 0u : i;
+  j = j == n ? 0u : j;
+  k = k == n ? 0u : k;
+  return int32_t(i + (j + k * n) * n);
+}
+
 // GetVoxel (voxel.glsl:149-154): `>` bounds test, NEAREST + GL_REPEAT, NaN reads 0. Reference
 // form, used off the hot loop (refraction probes).
-__device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p, int32_t& vidx) {
-  if (!(p.x >= 0.0f && p.y >= 0.0f && p.z >= 0.0f && p.x <= c.fn && p.y <= c.fn && p.z <= c.fn)) {
-    vidx = -1;
+__device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p) {
+  if (!(p.x >= 0.0f && p.y >= 0.0f && p.z >= 0.0f && p.x <= c.fn && p.y <= c.fn && p.z <= c.fn))
     return 0u;
-  }
-  int32_t i = int32_t(__builtin_floorf(p.x));
-  int32_t j = int32_t(__builtin_floorf(p.y));
-  int32_t k = int32_t(__builtin_floorf(p.z));
-  i = i >= c.n ? i - c.n : i;
-  j = j >= c.n ? j - c.n : j;
-  k = k >= c.n ? k - c.n : k;
-  vidx = i + (j + k * c.n) * c.n;
-  return c.vox[vidx];
+  const uint32_t i = uint32_t(__builtin_floorf(p.x));
+  const uint32_t j = uint32_t(__builtin_floorf(p.y));
+  const uint32_t k = uint32_t(__builtin_floorf(p.z));
+  return c.vox[mad24(mad24(k, c.p, j), c.p, i)];
 }
 
 // TestCube (voxel.glsl:248-257) with centre N/2 and size N; bitwise ops, no short-circuit branches.
@@ -172,8 +185,6 @@ __device__ __forceinline__ f3 initial_t(f3 dir, f3 cur, f3 pos) {
             (next_plane(dir.z, cur.z) - pos.z) / dir.z);
 }
 
-__device__ __forceinline__ f3 sign3(f3 d) { return mk(gsign(d.x), gsign(d.y), gsign(d.z)); }
-
 __device__ __forceinline__ float sel3(int axis, float x, float y, float z) {
   return axis == 2 ? z : (axis == 1 ? y : x);
 }
@@ -191,8 +202,8 @@ __device__ __forceinline__ float div_rn(float a, float d, float y) {
 }
 
 // The fast walk needs every direction component normal and not tiny: then every t stays finite
-// and non-negative-zero (so v_min3 == GLSL min) and div_rn is exact. Otherwise (a +-0 component:
-// +-inf / NaN t values, where the GLSL would spin) the walk replays the reference literally.
+// and never -0 (so v_min3 == GLSL min) and div_rn is exact. Otherwise (a +-0 component: +-inf /
+// NaN t values, where the GLSL would spin) the walk replays the reference literally.
 __device__ __forceinline__ bool fast_path_ok(f3 d) {
   const float lo = 0x1p-64f;
   return __builtin_fabsf(d.x) >= lo && __builtin_fabsf(d.y) >= lo && __builtin_fabsf(d.z) >= lo &&
@@ -206,7 +217,7 @@ struct WalkState {
   float len;       // rayLength
   uint32_t it;     // iterations of this RayMarch/RayMarchShadow call (VRT_MAX_STEPS cap)
   uint32_t ties;   // index==3 events
-  bool check_cube; // TestCube can only fail after a sample outside [0,N]^3
+  bool check_cube; // TestCube must be evaluated at the loop top
 };
 
 enum : int { WALK_MISS = 0, WALK_EVENT = 1, WALK_CAP = 2 };
@@ -245,8 +256,6 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
                    dir.z > 0.0f ? hi : (dir.z < 0.0f ? -lo : __builtin_inff()));
   const f3 cs = mk(dir.x < 0.0f ? -1.0f : 1.0f, dir.y < 0.0f ? -1.0f : 1.0f,
                    dir.z < 0.0f ? -1.0f : 1.0f);
-  const uint32_t m = uint32_t(c.n - 1);
-  const uint32_t lg = uint32_t(c.lg);
   f3 t = w.t, cur = w.cur;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
@@ -256,9 +265,9 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     w.check_cube = cube_out;
     return (len < c.max_len && !cube_out) ? WALK_CAP : WALK_MISS;
   }
-  // live-out state kept in VGPRs (a bool live out of a divergent loop costs SALU mask merges
-  // every iteration): status = event | inb << 1 | cube_out << 2
-  uint32_t status, v, idx;
+  // live-outs kept in VGPRs (a bool live out of a divergent loop costs SALU mask merges every
+  // iteration): the sampled texel coordinates and v_sel = inb ? v : 0; pidx_sel = ~0 if outside
+  uint32_t vi, vj, vk, v_sel, pidx_sel;
   int axis;
   for (;;) {
     ++it;
@@ -277,14 +286,17 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     } else {  // same voxel: the +-0 added on an un-crossed axis only flips the sign of a zero
       smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f), cur.z + (ez ? hs.z : 0.0f));
     }
-    // branch-free fetch: clamp to [0,N] (med3; NaN -> in range), floor, wrap N -> 0 (GL_REPEAT,
-    // power-of-two N); the sample is inside iff clamping left it unchanged (NaN: outside)
+    // branch-free fetch: clamp to [0,N] (med3; NaN -> in range), floor; the sample is inside iff
+    // clamping left it unchanged (NaN: outside); GL_REPEAT's N -> 0 is in the padded layout
     const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
     const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
     const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
     const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
-    idx = (cvt_flr(qx) & m) | ((cvt_flr(qy) & m) << lg) | ((cvt_flr(qz) & m) << (2u * lg));
-    v = c.vox[idx];
+    vi = cvt_flr(qx);
+    vj = cvt_flr(qy);
+    vk = cvt_flr(qz);
+    const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
+    const uint32_t v = c.vox[pidx];
     ties += (ey & ez) ? 1u : 0u;
     axis = ez ? 2 : (ey ? 1 : 0);
     // t update for the crossed axis (voxel.glsl:296/381), computed while the load is in flight
@@ -300,16 +312,14 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     q = q - s;
     t = mk(axis == 0 ? q : t.x, axis == 1 ? q : t.y, axis == 2 ? q : t.z);
     // loop-top tests of the NEXT iteration; TestCube can only fail after an outside sample
-    bool cube_next;
-    if (EXACT) cube_next = !inb && !test_cube(cur, dir, c.fn);
-    else cube_next = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
-    const bool stop = !(len < c.max_len) | cube_next | (it >= VRT_MAX_STEPS);
+    if (EXACT) cube_out = !inb && !test_cube(cur, dir, c.fn);
+    else cube_out = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
+    const bool stop = !(len < c.max_len) | cube_out | (it >= VRT_MAX_STEPS);
     // outside samples read 0 (GetVoxel :151-152)
-    bool event;
-    if (SHADOW) event = inb & (v != 0u) & (v != 2u);
-    else event = inb ? (v != medium) : (medium != 0u);
-    status = (event ? 1u : 0u) | (inb ? 2u : 0u) | (cube_next ? 4u : 0u);
-    asm volatile("" : "+v"(status));
+    v_sel = inb ? v : 0u;
+    pidx_sel = inb ? pidx : ~0u;
+    asm volatile("" : "+v"(v_sel), "+v"(pidx_sel));  // materialise: no SALU live-out masks
+    const bool event = SHADOW ? (v_sel != 0u && v_sel != 2u) : (v_sel != medium);
     if (event | stop) break;
   }
   w.t = t;
@@ -317,17 +327,20 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
   w.len = len;
   w.it = it;
   w.ties = ties;
-  const bool inb = (status & 2u) != 0u;
-  if (status & 1u) {
+  const bool event = SHADOW ? (v_sel != 0u && v_sel != 2u) : (v_sel != medium);
+  const bool inb = pidx_sel != ~0u;
+  if (event) {
     axis_out = axis;
-    vidx_out = inb ? int32_t(idx) : -1;
-    v_out = inb ? v : 0u;
+    vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
+    v_out = v_sel;
     w.check_cube = !inb;  // on re-entry (new direction after a refraction): re-test iff outside
     return WALK_EVENT;
   }
-  cube_out = (status & 4u) != 0u;
+  // stopped: which loop-top test fired (length first, then TestCube, then the cap)?
+  if (!(len < c.max_len)) return WALK_MISS;
+  cube_out = !inb && !test_cube(cur, dir, c.fn);
   w.check_cube = cube_out;
-  return (len < c.max_len && !cube_out) ? WALK_CAP : WALK_MISS;
+  return cube_out ? WALK_MISS : WALK_CAP;
 }
 
 template <bool SHADOW>
@@ -354,9 +367,8 @@ __device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
 
 // GetRefractionRay (voxel.glsl:217-246)
 __device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counters& k) {
-  int32_t dummy;
-  const uint32_t outv = get_voxel(c, h.point + h.normal * 0.5f, dummy);
-  const uint32_t inv = get_voxel(c, h.point - h.normal * 0.5f, dummy);
+  const uint32_t outv = get_voxel(c, h.point + h.normal * 0.5f);
+  const uint32_t inv = get_voxel(c, h.point - h.normal * 0.5f);
   k.c[VRT_CNT_REFRACTION_PROBES]++;
   const float eta = mat_refr(outv) / mat_refr(inv);
   Ray r;
@@ -378,28 +390,37 @@ __device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counte
   return r;
 }
 
-// RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
-__device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
-                             uint32_t& flags) {
-  WalkState w;
+__device__ __forceinline__ void walk_init(WalkState& w, const Ray& ray) {
   w.len = ray.len;
   w.cur = ray.pos;
   w.t = initial_t(ray.dir, ray.pos, ray.pos);
   w.it = 0;
   w.ties = 0;
   w.check_cube = true;
-  int axis;
-  int32_t vidx;
-  uint32_t v;
-  const int r = walk<true>(c, ray.pos, ray.dir, ray.len, 0u, w, axis, vidx, v);
+}
+
+__device__ __forceinline__ void walk_account(const WalkState& w, int r, int steps_slot,
+                                             Counters& k, uint32_t& steps, uint32_t& flags) {
   steps += w.it;
-  k.c[VRT_CNT_SHADOW_STEPS] += w.it;
+  k.c[steps_slot] += w.it;
   k.c[VRT_CNT_TIE3] += w.ties;
   if (w.ties) flags |= VRT_HIT_FLAG_TIE3;
   if (r == WALK_CAP) {
     k.c[VRT_CNT_STEP_CAP]++;
     flags |= VRT_HIT_FLAG_STEP_CAP;
   }
+}
+
+// RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
+__device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
+                             uint32_t& flags) {
+  WalkState w;
+  walk_init(w, ray);
+  int axis;
+  int32_t vidx;
+  uint32_t v;
+  const int r = walk<true>(c, ray.pos, ray.dir, ray.len, 0u, w, axis, vidx, v);
+  walk_account(w, r, VRT_CNT_SHADOW_STEPS, k, steps, flags);
   return r == WALK_EVENT;
 }
 
@@ -413,12 +434,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
   h.point = mk(0.0f, 0.0f, 0.0f);
   h.normal = h.point;
   WalkState w;
-  w.len = ray.len;
-  w.cur = ray.pos;
-  w.t = initial_t(ray.dir, ray.pos, ray.pos);
-  w.it = 0;
-  w.ties = 0;
-  w.check_cube = true;
+  walk_init(w, ray);
   uint32_t medium = ray.voxel;
   int internal = 0;
   int r;
@@ -464,21 +480,64 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
                         comp(ray.dir, axis) - (w.len - ray.len);
     set_comp(w.t, axis, q);
   }
-  steps += w.it;
-  k.c[VRT_CNT_DDA_STEPS] += w.it;
-  k.c[VRT_CNT_TIE3] += w.ties;
-  if (w.ties) flags |= VRT_HIT_FLAG_TIE3;
-  if (r == WALK_CAP) {
-    k.c[VRT_CNT_STEP_CAP]++;
-    flags |= VRT_HIT_FLAG_STEP_CAP;
+  walk_account(w, r, VRT_CNT_DDA_STEPS, k, steps, flags);
+  return h;
+}
+
+// TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
+__device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
+                                                 uint32_t& steps, uint32_t& flags) {
+  const Hit h = march(c, ray, k, steps, flags);
+  if (h.found) {
+    Ray sr;  // GetShadowRay (:191-201)
+    sr.voxel = h.voxel;
+    sr.pos = h.point;
+    sr.dir = c.sun_n;
+    sr.len = h.len;
+    sr.energy = ray.energy;
+    sr.rdepth = 0;
+    sr.tdepth = 0;
+    k.c[VRT_CNT_SHADOW_RAYS]++;
+    const bool in_shadow = march_shadow(c, sr, k, steps, flags);
+    const uint32_t m = mat_id(h.voxel);
+    float brightness;
+    if (in_shadow) {
+      brightness = kAmbient;
+    } else {
+      const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sr.dir), 0.0f);
+      const float specular =
+          mat_ks(m) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m));
+      brightness = kAmbient + diffuse + specular;
+    }
+    const float4 col = mat_color(m);  // RayColor (:184-188)
+    const float e = ray.energy;
+    color.x = mixf(color.x, col.x * col.w * brightness, e);
+    color.y = mixf(color.y, col.y * col.w * brightness, e);
+    color.z = mixf(color.z, col.z * col.w * brightness, e);
+  } else {
+    // GetSkyboxColor (:386-393), then the second mix at :420
+    const f3 u = normalize3(ray.dir);
+    const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
+    const float grad = (u.y + 1.0f) * 0.5f;
+    const float sy = gmax(c.sun.y, 0.0f);
+    const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
+    const float a1 = 1.0f - ray.energy;
+    const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
+    color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
   }
   return h;
 }
 
 constexpr int kMaxStack = 17;
 
+#ifndef VRT_MIN_WAVES
+#define VRT_MIN_WAVES 1
+#endif
+
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
-__global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __restrict__ vox,
+// The primary ray (stack[0] of the reference) stays in registers; the scratch stack only ever
+// holds secondary rays, so pixels that spawn none never touch it.
+__global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, const uint8_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
@@ -495,7 +554,7 @@ __global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __r
     Ctx c;
     c.vox = vox;
     c.n = a.n;
-    c.lg = 31 - __builtin_clz(uint32_t(a.n));
+    c.p = uint32_t(a.n) + 1u;
     c.fn = a.fn;
     c.max_len = a.max_len;
     c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
@@ -518,81 +577,41 @@ __global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __r
     const f3 vdir = mk(f4[0] / f4[3], f4[1] / f4[3], f4[2] / f4[3]) - vnear;
 
     f3 color = mk(0.0f, 0.0f, 0.0f);
+    Ray ray;
+    ray.pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
+    ray.dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);
+    ray.len = 0.0f;
+    ray.energy = 1.0f;
+    ray.voxel = 0;
+    ray.rdepth = 0;
+    ray.tdepth = 0;
     Ray stack[kMaxStack];
     const int cap = a.max_refl + a.max_transp + 1;
-    stack[0].pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
-    stack[0].dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);
-    stack[0].len = 0.0f;
-    stack[0].energy = 1.0f;
-    stack[0].voxel = 0;
-    stack[0].rdepth = 0;
-    stack[0].tdepth = 0;
-    int sp = 1;
+    int sp = 0;
     uint32_t steps = 0, flags = 0;
-    int32_t hit_vidx = -1;
-    float hit_len = 0.0f;
-    bool first = true;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
-    while (sp > 0) {
-      Ray ray = stack[--sp];
-      if (!first) k.c[VRT_CNT_SECONDARY_RAYS]++;
-      // TraceWithShadow (voxel.glsl:395-423)
-      const Hit h = march(c, ray, k, steps, flags);
-      if (h.found) {
-        Ray sr;
-        sr.voxel = h.voxel;
-        sr.pos = h.point;
-        sr.dir = c.sun_n;
-        sr.len = h.len;
-        sr.energy = ray.energy;
-        sr.rdepth = 0;
-        sr.tdepth = 0;
-        k.c[VRT_CNT_SHADOW_RAYS]++;
-        const bool in_shadow = march_shadow(c, sr, k, steps, flags);
+    const Hit h0 = trace_with_shadow(c, ray, color, k, steps, flags);
+    const int32_t hit_vidx = h0.found ? h0.vidx : -1;
+    const float hit_len = h0.found ? h0.len : 0.0f;
+    if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
+      Hit h = h0;
+      for (;;) {
         const uint32_t m = mat_id(h.voxel);
-        float brightness;
-        if (in_shadow) {
-          brightness = kAmbient;
-        } else {
-          const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sr.dir), 0.0f);
-          const float specular =
-              mat_ks(m) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m));
-          brightness = kAmbient + diffuse + specular;
-        }
-        const float4 col = mat_color(m);
-        const float e = ray.energy;
-        color.x = mixf(color.x, col.x * col.w * brightness, e);
-        color.y = mixf(color.y, col.y * col.w * brightness, e);
-        color.z = mixf(color.z, col.z * col.w * brightness, e);
-      } else {
-        // GetSkyboxColor (:386-393), then the second mix at :420
-        const f3 u = normalize3(ray.dir);
-        const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
-        const float grad = (u.y + 1.0f) * 0.5f;
-        const float sy = gmax(c.sun.y, 0.0f);
-        const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
-        const float a1 = 1.0f - ray.energy;
-        const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
-        color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
-      }
-      if (first) {
         if (h.found) {
-          hit_vidx = h.vidx;
-          hit_len = h.len;
+          if (mat_reflective(m) && ray.rdepth < a.max_refl) {
+            if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
+            else flags |= VRT_HIT_FLAG_STACK_FULL;
+          }
+          if (mat_transparent(m) && ray.tdepth < a.max_transp && mat_color(m).w != 1.0f) {
+            if (sp < cap) stack[sp++] = refraction_ray(c, ray, h, k);
+            else flags |= VRT_HIT_FLAG_STACK_FULL;
+          }
         }
-        first = false;
-      }
-      if (h.found) {
-        const uint32_t m = mat_id(h.voxel);
-        if (mat_reflective(m) && ray.rdepth < a.max_refl) {
-          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
-          else flags |= VRT_HIT_FLAG_STACK_FULL;
-        }
-        if (mat_transparent(m) && ray.tdepth < a.max_transp && mat_color(m).w != 1.0f) {
-          if (sp < cap) stack[sp++] = refraction_ray(c, ray, h, k);
-          else flags |= VRT_HIT_FLAG_STACK_FULL;
-        }
+        if (sp == 0) break;
+        ray = stack[--sp];
+        k.c[VRT_CNT_SECONDARY_RAYS]++;
+        h = trace_with_shadow(c, ray, color, k, steps, flags);
       }
     }
     const size_t o = size_t(li) * size_t(a.width) + size_t(px);
@@ -618,13 +637,27 @@ __global__ void __launch_bounds__(256) render_kernel(KArgs a, const uint8_t* __r
   }
 }
 
+// Re-layout N^3 (x fastest) into the padded (N+1)^3 device format: plane N repeats plane 0.
+__global__ void __launch_bounds__(256) pad_volume_kernel(const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst, uint32_t n) {
+  const uint32_t p = n + 1u;
+  const uint64_t total = uint64_t(p) * p * p;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
+       q += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t i = uint32_t(q % p), j = uint32_t((q / p) % p), k = uint32_t(q / (uint64_t(p) * p));
+    const uint32_t si = i == n ? 0u : i, sj = j == n ? 0u : j, sk = k == n ? 0u : k;
+    dst[q] = src[si + (uint64_t(sj) + uint64_t(sk) * n) * n];
+  }
+}
+
 }  // namespace vrt
 
 // ---------------------------------------------------------------------------- C-ABI context --
 
 struct vrt_ctx {
   int device = 0;
-  uint8_t* d_vox = nullptr;
+  uint8_t* d_vox = nullptr;      // canonical N^3
+  uint8_t* d_vox_pad = nullptr;  // padded (N+1)^3, the kernel's format
   int32_t n = 0;
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
@@ -645,15 +678,15 @@ int hip_fail(vrt_ctx* c, hipError_t e, const char* what) {
   return fail(c, VRT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define VRT_HIP(ctx, call)                                      \
-  do {                                                          \
-    hipError_t e_ = (call);                                     \
-    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);    \
+#define VRT_HIP(ctx, call)                                   \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
   } while (0)
 
 int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) {
   if (!cam || !p) return fail(ctx, VRT_ERR_INVALID, "null camera or params");
-  if (!ctx->d_vox) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
+  if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
   if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
     return fail(ctx, VRT_ERR_INVALID, "bad image size");
   if (!p->color_only)
@@ -692,6 +725,43 @@ void launch(const vrt::KArgs& a, const uint8_t* vox, float4* out, vrt_hit* hit,
   hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(256), 0, s, a, vox, out, hit, cnt);
 }
 
+int volume_alloc(vrt_ctx* ctx, int32_t n) {
+  if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
+    return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->d_vox && ctx->n != n) {
+    (void)hipFree(ctx->d_vox);
+    (void)hipFree(ctx->d_vox_pad);
+    ctx->d_vox = ctx->d_vox_pad = nullptr;
+  }
+  if (!ctx->d_vox) {
+    const size_t bytes = size_t(n) * n * n, pbytes = size_t(n + 1) * (n + 1) * (n + 1);
+    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess) {
+      ctx->d_vox = nullptr;
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume");
+    }
+    if (hipMalloc(&ctx->d_vox_pad, pbytes) != hipSuccess) {
+      (void)hipFree(ctx->d_vox);
+      ctx->d_vox = ctx->d_vox_pad = nullptr;
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc padded volume");
+    }
+  }
+  ctx->n = n;
+  return VRT_OK;
+}
+
+int volume_finish(vrt_ctx* ctx, hipStream_t s) {
+  const uint64_t p = uint64_t(ctx->n) + 1;
+  const uint64_t total = p * p * p;
+  const unsigned blocks = unsigned(std::min<uint64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(vrt::pad_volume_kernel, dim3(blocks), dim3(256), 0, s, ctx->d_vox,
+                     ctx->d_vox_pad, uint32_t(ctx->n));
+  VRT_HIP(ctx, hipGetLastError());
+  VRT_HIP(ctx, hipStreamSynchronize(s));
+  ctx->err.clear();
+  return VRT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -718,6 +788,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->d_vox) (void)hipFree(c->d_vox);
+  if (c->d_vox_pad) (void)hipFree(c->d_vox_pad);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_hit) (void)hipFree(c->d_hit);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
@@ -731,25 +802,22 @@ const char* vrt_last_error(const vrt_ctx* c) { return c ? c->err.c_str() : "null
 int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
   if (!ctx) return VRT_ERR_INVALID;
   if (!vol || !vol->voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
-  const int32_t n = vol->n;
-  if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
-    return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t bytes = size_t(n) * n * n;
-  if (ctx->d_vox && ctx->n != n) {
-    (void)hipFree(ctx->d_vox);
-    ctx->d_vox = nullptr;
-  }
-  if (!ctx->d_vox) {
-    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess) {
-      ctx->d_vox = nullptr;
-      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume");
-    }
-  }
-  ctx->n = n;
+  const int st = volume_alloc(ctx, vol->n);
+  if (st != VRT_OK) return st;
+  const size_t bytes = size_t(vol->n) * vol->n * vol->n;
   VRT_HIP(ctx, hipMemcpy(ctx->d_vox, vol->voxels, bytes, hipMemcpyHostToDevice));
-  ctx->err.clear();
-  return VRT_OK;
+  return volume_finish(ctx, nullptr);
+}
+
+int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!d_voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
+  const int st = volume_alloc(ctx, n);
+  if (st != VRT_OK) return st;
+  const size_t bytes = size_t(n) * n * n;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  VRT_HIP(ctx, hipMemcpyAsync(ctx->d_vox, d_voxels, bytes, hipMemcpyDeviceToDevice, s));
+  return volume_finish(ctx, s);
 }
 
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->d_vox : nullptr; }
@@ -766,7 +834,7 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
     return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
   if (rows == 0) return VRT_OK;
   const vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
-  launch(a, ctx->d_vox, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
+  launch(a, ctx->d_vox_pad, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
          reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
@@ -795,7 +863,7 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* 
   VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
   const vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
   VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
-  launch(a, ctx->d_vox, ctx->d_out, out_hit ? ctx->d_hit : nullptr, ctx->d_cnt, nullptr);
+  launch(a, ctx->d_vox_pad, ctx->d_out, out_hit ? ctx->d_hit : nullptr, ctx->d_cnt, nullptr);
   VRT_HIP(ctx, hipGetLastError());
   VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
   VRT_HIP(ctx, hipMemcpy(out_rgba, ctx->d_out, pixels * sizeof(float4), hipMemcpyDeviceToHost));

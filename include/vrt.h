@@ -99,7 +99,7 @@ enum {
 
 typedef struct {
   uint64_t counters[VRT_CNT_COUNT];
-  float kernel_ms;            /* hipEvent time of the render kernel(s) */
+  float kernel_ms;            /* hipEvent time of the render (kernel + counter reduction) */
   float reserved[3];
 } vrt_stats;
 
@@ -132,8 +132,9 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
 /* Asynchronous band render into DEVICE buffers on `hip_stream` (hipStream_t, NULL = default).
  * Renders frame rows row0 + i*row_step for i in [0, rows) at full width; output row i of
  * d_out_rgba / d_out_hit holds frame row row0 + i*row_step. d_out_hit and d_counters
- * (VRT_CNT_COUNT uint64, accumulated with atomics, caller zeroes) may be NULL. No host sync,
- * no allocation: capturable in a hipGraph. */
+ * (VRT_CNT_COUNT uint64, ACCUMULATED into; the caller zeroes them) may be NULL. Counting uses a
+ * per-context replica buffer: at most one counted render per context in flight at a time.
+ * No host sync, no allocation: capturable in a hipGraph. */
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
                           int32_t row0, int32_t rows, int32_t row_step,
                           float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,

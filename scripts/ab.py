@@ -53,21 +53,27 @@ def main():
         vox = vrt.build_scene(scene, n)
         cam = vrt.make_camera(w, hgt)
         p = vrt.default_params(R, T)
-        vol = abi.Volume(vox.ctypes.data_as(C.POINTER(C.c_uint8)), n)
+        vol = abi.Volume(vox.ctypes.data_as(C.POINTER(C.c_uint8)), n)  # noqa
         for L, h in handles.values():
             assert L.vrt_upload_volume(h, C.byref(vol)) == 0
         imgs = {}
         times = {k: [] for k in handles}
-        for r in range(args.rounds + 1):
+        stream = torch.cuda.current_stream()
+        outs = {k: torch.empty((hgt, w, 4), dtype=torch.float32, device="cuda") for k in handles}
+        for r in range(args.rounds + 2):
             for name, (L, h) in handles.items():
-                rgba = np.empty((hgt, w, 4), np.float32)
-                st = abi.Stats()
-                assert L.vrt_render(h, C.byref(cam), C.byref(p), rgba.ctypes.data, None,
-                                    C.byref(st)) == 0
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                rc = L.vrt_render_rows_async(h, C.byref(cam), C.byref(p), 0, hgt, 1,
+                                             outs[name].data_ptr(), None, None, stream.cuda_stream)
+                assert rc == 0
+                e1.record(stream)
+                torch.cuda.synchronize()
                 if r == 0:
-                    imgs[name] = rgba
-                else:
-                    times[name].append(st.kernel_ms)
+                    imgs[name] = outs[name].cpu().numpy()
+                elif r >= 2:
+                    times[name].append(e0.elapsed_time(e1))
         base = imgs["base"]
         for name in handles:
             t = np.array(times[name])

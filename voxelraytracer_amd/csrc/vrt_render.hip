@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -26,6 +27,8 @@ namespace vrt {
 struct KArgs {
   float inv_pv[16];
   float sun[3];
+  float sun_n[3];    // normalize(u_SunDir), GLSL normalize semantics (host: same IEEE ops)
+  float sun_rcp[3];  // RN(1 / sun_n): the shadow walk's per-axis reciprocals (uniform)
   float time, ray_noise, refl_noise, refr_noise, max_len;
   float fn;
   int32_t n, width, height;
@@ -141,7 +144,7 @@ struct Ctx {
   uint32_t p;  // N + 1
   float fn;
   float max_len;
-  f3 sun, sun_n;
+  f3 sun, sun_n, sun_rcp;
   float time, refl_noise, refr_noise;
 };
 
@@ -241,14 +244,16 @@ __device__ __forceinline__ float opaque(float x) {
 // Every float op of a step is the reference's, in its order; only their scheduling differs: the
 // t update of a step (which does not depend on the voxel) is issued before the voxel test so it
 // overlaps the load, and is simply not used when the step ends in an event.
+#ifndef VRT_CUBE_BRANCH
+#define VRT_CUBE_BRANCH 0
+#endif
+
 template <bool SHADOW, bool EXACT>
-__device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir, float len0,
-                                        uint32_t medium, WalkState& w, int& axis_out,
+__device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
+                                        float len0, uint32_t medium, WalkState& w, int& axis_out,
                                         int32_t& vidx_out, uint32_t& v_out) {
   const f3 step = sign3(dir);
   const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
-  f3 rcp = mk(1.0f, 1.0f, 1.0f);
-  if (!EXACT) rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
   // TestCube per axis as one compare: sign(d)*p > bound (bound = +inf on a zero axis)
   const float hi = c.fn * 0.5f + c.fn / 2.0f, lo = c.fn * 0.5f - c.fn / 2.0f;
   const f3 cb = mk(dir.x > 0.0f ? hi : (dir.x < 0.0f ? -lo : __builtin_inff()),
@@ -304,7 +309,8 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     const float pa = sel3(axis, pos.x, pos.y, pos.z);
     const float da = sel3(axis, dir.x, dir.y, dir.z);
     const float ca = sel3(axis, cur.x, cur.y, cur.z);
-    const float sa = sel3(axis, step.x, step.y, step.z);
+    // sign(d) on the crossed axis; on the fast path d != 0, so it is copysign(1, d) (one v_bfi)
+    const float sa = EXACT ? sel3(axis, step.x, step.y, step.z) : __builtin_copysignf(1.0f, da);
     const float num = (ca + sa) - pa;
     float q;
     if (EXACT) q = num / da;
@@ -312,8 +318,14 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     q = q - s;
     t = mk(axis == 0 ? q : t.x, axis == 1 ? q : t.y, axis == 2 ? q : t.z);
     // loop-top tests of the NEXT iteration; TestCube can only fail after an outside sample
-    if (EXACT) cube_out = !inb && !test_cube(cur, dir, c.fn);
-    else cube_out = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
+    if (EXACT) {
+      cube_out = !inb && !test_cube(cur, dir, c.fn);
+    } else if (VRT_CUBE_BRANCH) {  // skipped when every lane of the wave sampled inside
+      cube_out = false;
+      if (!inb) cube_out = (cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z);
+    } else {
+      cube_out = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
+    }
     const bool stop = !(len < c.max_len) | cube_out | (it >= VRT_MAX_STEPS);
     // outside samples read 0 (GetVoxel :151-152)
     v_sel = inb ? v : 0u;
@@ -343,13 +355,25 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
   return cube_out ? WALK_MISS : WALK_CAP;
 }
 
-template <bool SHADOW>
-__device__ __forceinline__ int walk(const Ctx& c, const f3 pos, const f3 dir, float len0,
-                                    uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
-                                    uint32_t& v) {
-  if (__builtin_expect(fast_path_ok(dir), 1))
-    return dda_walk<SHADOW, false>(c, pos, dir, len0, medium, w, axis, vidx, v);
-  return dda_walk<SHADOW, true>(c, pos, dir, len0, medium, w, axis, vidx, v);
+// RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)
+__device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
+                                        uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
+                                        uint32_t& v) {
+  if (__builtin_expect(fast_path_ok(dir), 1)) {
+    const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
+    return dda_walk<false, false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+  }
+  return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
+}
+
+// RayMarchShadow walk: the direction is normalize(u_SunDir) for every ray (uniform constants)
+__device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len0, WalkState& w) {
+  int axis;
+  int32_t vidx;
+  uint32_t v;
+  if (__builtin_expect(fast_path_ok(c.sun_n), 1))
+    return dda_walk<true, false>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+  return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
 
 // GetReflectionRay (voxel.glsl:203-215)
@@ -416,10 +440,7 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
                              uint32_t& flags) {
   WalkState w;
   walk_init(w, ray);
-  int axis;
-  int32_t vidx;
-  uint32_t v;
-  const int r = walk<true>(c, ray.pos, ray.dir, ray.len, 0u, w, axis, vidx, v);
+  const int r = walk_shadow(c, ray.pos, ray.len, w);
   walk_account(w, r, VRT_CNT_SHADOW_STEPS, k, steps, flags);
   return r == WALK_EVENT;
 }
@@ -442,7 +463,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk<false>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    r = walk_ray(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -530,6 +551,10 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 
 constexpr int kMaxStack = 17;
 
+// Counter replicas: one 64-bit add per wave and counter into replica (block % kCntReplicas);
+// a single array would serialise ~300K same-address atomics per 1080p frame at the memory side.
+constexpr int kCntReplicas = 256;
+
 #ifndef VRT_MIN_WAVES
 #define VRT_MIN_WAVES 1
 #endif
@@ -558,7 +583,8 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
     c.fn = a.fn;
     c.max_len = a.max_len;
     c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
-    c.sun_n = normalize3(c.sun);
+    c.sun_n = mk(a.sun_n[0], a.sun_n[1], a.sun_n[2]);
+    c.sun_rcp = mk(a.sun_rcp[0], a.sun_rcp[1], a.sun_rcp[2]);
     c.time = a.time;
     c.refl_noise = a.refl_noise;
     c.refr_noise = a.refr_noise;
@@ -627,14 +653,29 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
   }
 
   if (counters) {
+    unsigned long long* slot =
+        counters + size_t((blockIdx.y * gridDim.x + blockIdx.x) % kCntReplicas) * VRT_CNT_COUNT;
 #pragma unroll
     for (int q = 0; q < VRT_CNT_COUNT; ++q) {
       unsigned long long v = k.c[q];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0 && v) atomicAdd(counters + q, v);
+      if (lane == 0 && v) atomicAdd(slot + q, v);
     }
   }
+}
+
+// Sum the counter replicas into `dst` (accumulating) and zero them for the next render.
+__global__ void __launch_bounds__(64) reduce_counters_kernel(unsigned long long* __restrict__ rep,
+                                                             unsigned long long* __restrict__ dst) {
+  const int q = threadIdx.x;
+  if (q >= VRT_CNT_COUNT) return;
+  unsigned long long s = 0;
+  for (int r = 0; r < kCntReplicas; ++r) {
+    s += rep[r * VRT_CNT_COUNT + q];
+    rep[r * VRT_CNT_COUNT + q] = 0;
+  }
+  dst[q] += s;
 }
 
 // Re-layout N^3 (x fastest) into the padded (N+1)^3 device format: plane N repeats plane 0.
@@ -661,7 +702,8 @@ struct vrt_ctx {
   int32_t n = 0;
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
-  unsigned long long* d_cnt = nullptr;
+  unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of vrt_render
+  unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
   size_t out_pixels = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
@@ -702,6 +744,13 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   vrt::KArgs a;
   std::memcpy(a.inv_pv, cam->inv_pv, sizeof(a.inv_pv));
   std::memcpy(a.sun, p->sun_dir, sizeof(a.sun));
+  // normalize(u_SunDir) exactly as the kernel's normalize3 (IEEE single ops, no contraction)
+  const float sx = p->sun_dir[0], sy = p->sun_dir[1], sz = p->sun_dir[2];
+  const float inv = 1.0f / std::sqrt(sx * sx + sy * sy + sz * sz);
+  a.sun_n[0] = sx * inv;
+  a.sun_n[1] = sy * inv;
+  a.sun_n[2] = sz * inv;
+  for (int i = 0; i < 3; ++i) a.sun_rcp[i] = 1.0f / a.sun_n[i];
   a.time = p->time;
   a.ray_noise = p->ray_noise;
   a.refl_noise = p->reflection_noise;
@@ -719,10 +768,13 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   return a;
 }
 
-void launch(const vrt::KArgs& a, const uint8_t* vox, float4* out, vrt_hit* hit,
+// Render kernel, then (when counting) fold the replicas into `cnt` (accumulate) and re-zero them.
+void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
   dim3 grid((a.width + 15) / 16, (a.rows + 15) / 16);
-  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(256), 0, s, a, vox, out, hit, cnt);
+  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(256), 0, s, a, ctx->d_vox_pad, out, hit,
+                     cnt ? ctx->d_cnt_rep : nullptr);
+  if (cnt) hipLaunchKernelGGL(vrt::reduce_counters_kernel, dim3(1), dim3(64), 0, s, ctx->d_cnt_rep, cnt);
 }
 
 int volume_alloc(vrt_ctx* ctx, int32_t n) {
@@ -775,9 +827,13 @@ int vrt_create(int device, vrt_ctx** out) {
   if (device < 0 || device >= count) return VRT_ERR_INVALID;
   vrt_ctx* c = new vrt_ctx();
   c->device = device;
+  const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
   if (hipSetDevice(device) != hipSuccess || hipEventCreate(&c->ev0) != hipSuccess ||
-      hipEventCreate(&c->ev1) != hipSuccess) {
-    delete c;
+      hipEventCreate(&c->ev1) != hipSuccess ||
+      hipMalloc(&c->d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT) != hipSuccess ||
+      hipMalloc(&c->d_cnt_rep, rep_bytes) != hipSuccess ||
+      hipMemset(c->d_cnt_rep, 0, rep_bytes) != hipSuccess) {
+    vrt_destroy(c);
     return VRT_ERR_DEVICE;
   }
   *out = c;
@@ -792,6 +848,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_hit) (void)hipFree(c->d_hit);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
+  if (c->d_cnt_rep) (void)hipFree(c->d_cnt_rep);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -834,7 +891,7 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
     return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
   if (rows == 0) return VRT_OK;
   const vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
-  launch(a, ctx->d_vox_pad, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
+  launch(ctx, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
          reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
@@ -859,11 +916,11 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* 
       return fail(ctx, VRT_ERR_OOM, "hipMalloc frame buffers");
     ctx->out_pixels = pixels;
   }
-  if (!ctx->d_cnt) VRT_HIP(ctx, hipMalloc(&ctx->d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT));
-  VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
+  if (stats)
+    VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
   const vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
   VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
-  launch(a, ctx->d_vox_pad, ctx->d_out, out_hit ? ctx->d_hit : nullptr, ctx->d_cnt, nullptr);
+  launch(ctx, a, ctx->d_out, out_hit ? ctx->d_hit : nullptr, stats ? ctx->d_cnt : nullptr, nullptr);
   VRT_HIP(ctx, hipGetLastError());
   VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
   VRT_HIP(ctx, hipMemcpy(out_rgba, ctx->d_out, pixels * sizeof(float4), hipMemcpyDeviceToHost));

@@ -63,6 +63,14 @@ CASES = [
     ("terrain", 128, 256, 144, 4, 2, {}),
     ("refraction", 128, 192, 108, 4, 4, dict(pos=(0.3, -0.2, 0.1), rot=(10.0, 170.0, 0.0))),
     ("glass_cube", 64, 96, 96, 8, 8, dict(pos=(1.0, 2.0, -3.0), rot=(-60.0, 20.0, 0.0))),
+    # degenerate geometry: +0 direction components (exact fallback walk), a -6e-17 component
+    # (Markstein division with ~1e16 reciprocals), zero-t ties incl. the index-3 (y+z) tie
+    ("glass_cube", 16, 9, 9, 4, 4, dict(pos=(0.0, 0.0, 0.0), rot=(0.0, 0.0, 0.0))),
+    ("glass_cube", 128, 65, 65, 4, 4, dict(pos=(0.0, 0.0, 0.0), rot=(0.0, 0.0, 0.0))),
+    ("refraction", 16, 9, 7, 4, 4, dict(pos=(0.0, 0.0, 0.0), rot=(0.0, 90.0, 0.0))),
+    ("glass_cube", 16, 15, 15, 4, 4, dict(pos=(0.25, 0.25, 0.25), rot=(-35.26439, 45.0, 0.0))),
+    ("terrain", 32, 121, 121, 4, 2, dict(pos=(0.0, 5.0, 0.0), rot=(-90.0, 0.0, 0.0))),
+    ("terrain", 512, 384, 216, 4, 2, {}),
 ]
 
 

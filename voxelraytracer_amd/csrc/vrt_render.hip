@@ -245,7 +245,7 @@ __device__ __forceinline__ float opaque(float x) {
 // t update of a step (which does not depend on the voxel) is issued before the voxel test so it
 // overlaps the load, and is simply not used when the step ends in an event.
 #ifndef VRT_CUBE_BRANCH
-#define VRT_CUBE_BRANCH 0
+#define VRT_CUBE_BRANCH 1
 #endif
 
 template <bool SHADOW, bool EXACT>
@@ -556,7 +556,7 @@ constexpr int kMaxStack = 17;
 constexpr int kCntReplicas = 256;
 
 #ifndef VRT_MIN_WAVES
-#define VRT_MIN_WAVES 1
+#define VRT_MIN_WAVES 5
 #endif
 
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.

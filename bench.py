@@ -5,9 +5,10 @@ Workload (BASELINE.json metric "1920x1080 @ 128^3 voxels, 4 bounces"): configs[3
 _REFRACTION scene at 128^3, 1920x1080, reflect+refract 4 bounces (MAX_REFLECTIONS =
 MAX_TRANSPARENCIES = 4), colour-only, noise 0, camera/sun of SURVEY.md §8d. A step = one frame.
 
-Multi-GPU (one process per GPU, torchrun): the frame is split into cyclic row bands (rank r owns
-rows r, r+N, ...); every rank renders its band into HBM and rank 0 gathers the RGBA bands over
-RCCL each frame (the only exchange of the path). The total work is the fixed frame: strong
+Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
+cyclic row bands (rank r owns rows r, r+N, ...); every rank renders its band into HBM and rank 0
+gathers the RGBA bands over RCCL each frame (the only exchange of the path), pipelined so the
+gather of frame k overlaps the render of frame k+1. The total work is the fixed frame: strong
 scaling.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
@@ -84,13 +85,13 @@ def main():
     import torch.distributed as dist
 
     import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -99,57 +100,56 @@ def main():
     scene, n, w, h, R, T, desc = CONFIGS[args.config]
     cam = vrt.make_camera(w, h)
     params = vrt.default_params(R, T)
-    # Volume: built once on rank 0 (main.cpp:218-288) and broadcast over RCCL to every GPU.
-    vox_host = vrt.build_scene(scene, n) if rank == 0 else np.empty(n ** 3, np.uint8)
-    if world > 1:
-        t = torch.from_numpy(vox_host).to(dev)
-        dist.broadcast(t, 0)
-        vox_host = t.cpu().numpy()
-    ren = vrt.Renderer(local)
-    ren.upload_volume(vox_host, n)
-
-    if h % world:
-        raise SystemExit(f"height {h} not divisible by {world} GPUs")
-    rows = h // world
-    band = torch.empty((rows, w, 4), dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(band) for _ in range(world)] if (rank == 0 and world > 1) else None
-    # on one GPU the band IS the frame; with N ranks rank 0 assembles the frame from the gather
-    frame = torch.empty((h, w, 4), dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    # One counted frame (outside the timed region) gives the rays and algorithmic bytes per frame.
+    # Volume: built once on rank 0 (main.cpp:218-288), broadcast over RCCL to every GPU, uploaded
+    # device-to-device into each rank's context (padded (N+1)^3 layout built on the GPU).
+    vox_host = vrt.build_scene(scene, n) if rank == 0 else np.zeros(n ** 3, np.uint8)
+    vox_dev = torch.from_numpy(vox_host).to(dev)
+    broadcast_volume(vox_dev)
+    ren = vrt.Renderer(local)
+    ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
+
+    evs = []
+
+    def render_band(row0, rows, step, out):
+        e = None
+        if timing["on"]:
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record(stream)
+        ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, 0, sptr)
+        if e is not None:
+            e[1].record(stream)
+            evs.append(e)
+
+    timing = {"on": False}
+    tiler = FrameTiler(w, h, render_band, dev)
+
+    # One counted band per rank (outside the timed region): rays and algorithmic bytes per frame.
     cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device=dev)
-    ren.render_rows_async(cam, params, rank, rows, world, band.data_ptr(), 0, cnt.data_ptr(), sptr)
+    ren.render_rows_async(cam, params, tiler.row0, tiler.rows, tiler.step,
+                          tiler.bands[0].data_ptr(), 0, cnt.data_ptr(), sptr)
     torch.cuda.synchronize(dev)
+    own = vrt.counters_dict(cnt.cpu().tolist())
     if world > 1:
         dist.all_reduce(cnt)
     counters = vrt.counters_dict(cnt.cpu().tolist())
     rays_per_frame = vrt.total_rays(counters)
     bytes_per_frame = vrt.algorithmic_bytes(counters)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        ren.render_rows_async(cam, params, rank, rows, world, band.data_ptr(), 0, 0, sptr)
-        if ev is not None:
-            ev[1].record(stream)
-        if world > 1:
-            dist.gather(band, gather, dst=0)
-            if rank == 0:   # re-interleave the cyclic bands into the frame (frame row = i*N + r)
-                torch.stack(gather, 1, out=frame.view(rows, world, w, 4))
-
     for _ in range(args.warmup):
-        step()
+        tiler.frame()
+    tiler.finish()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    timing["on"] = True
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
+    for _ in range(args.steps):
+        tiler.frame()
+    tiler.finish()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -163,8 +163,9 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel on this rank: algorithmic bytes of its band per launch
-        own_bytes = bytes_per_frame / world
+        # roofline of the dominant kernel: the algorithmic bytes of THIS rank's band per launch
+        # over its mean launch time (HIP events on the stream the kernel is launched on)
+        own_bytes = vrt.algorithmic_bytes(own)
         achieved = own_bytes / (float(np.mean(kernel_ms)) * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
@@ -195,7 +196,8 @@ def main():
                 "height": h,
                 "max_reflections": R,
                 "max_transparencies": T,
-                "parallelism": f"row-band x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": (f"cyclic row bands x{world} + RCCL gather to rank 0"
+                                if world > 1 else "single GPU, whole frame"),
                 "rays_per_frame": rays_per_frame,
                 "algorithmic_bytes_per_frame": bytes_per_frame,
             },
@@ -206,6 +208,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                "bytes_per_launch": own_bytes,
                 "kernel_ms": round(float(np.mean(kernel_ms)), 4),
                 "kernel_ms_max_over_ranks": round(kern_ms_max, 4),
             },

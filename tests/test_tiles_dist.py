@@ -1,0 +1,100 @@
+"""Multi-rank framebuffer tiling (voxelraytracer_amd/tiles.py) on CPU with the gloo backend.
+
+Each rank renders its cyclic row band with the CPU oracle standing in for the HIP kernel (the
+same render_band contract bench.py feeds with vrt_render_rows_async), rank 0 gathers and
+re-interleaves; the assembled frames of a pipelined sequence must equal single-process oracle
+frames bit for bit. Also checks the volume broadcast."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, n, w, h, frames, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume
+
+    vox = torch.from_numpy(vrt.build_scene("glass_cube", n)) if rank == 0 else \
+        torch.zeros(n ** 3, dtype=torch.uint8)
+    broadcast_volume(vox)
+    vox_np = vox.numpy()
+    cam = vrt.make_camera(w, h)
+    params = [vrt.default_params(1, 2, time=float(t + 1)) for t in range(frames)]
+    state = {"i": 0}
+
+    def render_band(row0, rows, step, out):
+        rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"]], row0=row0, rows=rows,
+                                   row_step=step, threads=1)
+        out.copy_(torch.from_numpy(rgba))
+        state["i"] += 1
+
+    tiler = FrameTiler(w, h, render_band, torch.device("cpu"))
+    got = []
+    for _ in range(frames):
+        f = tiler.frame()
+        if f is not None:
+            got.append(f.clone().numpy())
+    f = tiler.finish()
+    if f is not None:
+        got.append(f.clone().numpy())
+    if rank == 0:
+        q.put((got, bytes(vox_np)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tiled_frames_match_single_process(built, world):
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h, frames = 16, 24, 18, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, vox_bytes = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    assert vox_bytes == vox.tobytes()   # broadcast replicated the volume
+    cam = vrt.make_camera(w, h)
+    assert len(got) == frames
+    for t in range(frames):
+        ref, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1)))
+        assert np.array_equal(got[t].view(np.uint32), ref.view(np.uint32)), t
+
+
+def test_band_spec_and_assembly():
+    from voxelraytracer_amd.tiles import assemble_cyclic, band_spec
+
+    assert band_spec(1, 4, 1080) == (1, 270, 4)
+    with pytest.raises(ValueError):
+        band_spec(0, 7, 1080)
+    frame = torch.arange(12 * 2 * 1, dtype=torch.float32).reshape(12, 2, 1)
+    bands = torch.stack([frame[r::3] for r in range(3)])
+    assert torch.equal(assemble_cyclic(bands), frame)

@@ -241,118 +241,117 @@ __device__ __forceinline__ float opaque(float x) {
 // The DDA loop of RayMarch / RayMarchShadow (voxel.glsl:273-298, :317-382) up to the first event.
 // Event: SHADOW -> an opaque voxel (HasVoxel && !transparent); otherwise the sampled byte differs
 // from the ray's medium, which covers both the hit (:353) and the leave-transparent case (:357).
-// Every float op of a step is the reference's, in its order; only their scheduling differs: the
-// t update of a step (which does not depend on the voxel) is issued before the voxel test so it
-// overlaps the load, and is simply not used when the step ends in an event.
-#ifndef VRT_CUBE_BRANCH
-#define VRT_CUBE_BRANCH 1
-#endif
-
+// Every float op of a step is the reference's, in its order; only their scheduling differs:
+//  - the inner loop exits on a cheap superset of the stop conditions (a sample outside the
+//    volume, a byte != medium, the length, the cap); the outer loop then replays the reference's
+//    decisions exactly: the event of that iteration, else the next iteration's loop-top tests
+//    (length, TestCube — which can only fail after an outside sample — and the cap), and
+//    re-enters the inner loop when none fires;
+//  - the t update of a step (independent of the voxel) is issued before the voxel-load wait and
+//    is simply dead after an event.
 template <bool SHADOW, bool EXACT>
 __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
                                         int32_t& vidx_out, uint32_t& v_out) {
   const f3 step = sign3(dir);
   const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
-  // TestCube per axis as one compare: sign(d)*p > bound (bound = +inf on a zero axis)
-  const float hi = c.fn * 0.5f + c.fn / 2.0f, lo = c.fn * 0.5f - c.fn / 2.0f;
-  const f3 cb = mk(dir.x > 0.0f ? hi : (dir.x < 0.0f ? -lo : __builtin_inff()),
-                   dir.y > 0.0f ? hi : (dir.y < 0.0f ? -lo : __builtin_inff()),
-                   dir.z > 0.0f ? hi : (dir.z < 0.0f ? -lo : __builtin_inff()));
-  const f3 cs = mk(dir.x < 0.0f ? -1.0f : 1.0f, dir.y < 0.0f ? -1.0f : 1.0f,
-                   dir.z < 0.0f ? -1.0f : 1.0f);
   f3 t = w.t, cur = w.cur;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
-  // loop-top tests of the reference for the first iteration: length, TestCube, (step cap)
-  bool cube_out = w.check_cube && !test_cube(cur, dir, c.fn);
-  if (!(len < c.max_len) | cube_out | (it >= VRT_MAX_STEPS)) {
-    w.check_cube = cube_out;
-    return (len < c.max_len && !cube_out) ? WALK_CAP : WALK_MISS;
-  }
-  // live-outs kept in VGPRs (a bool live out of a divergent loop costs SALU mask merges every
-  // iteration): the sampled texel coordinates and v_sel = inb ? v : 0; pidx_sel = ~0 if outside
-  uint32_t vi, vj, vk, v_sel, pidx_sel;
-  int axis;
+  bool check = w.check_cube;
+  int result;
   for (;;) {
-    ++it;
-    float tmin;
-    if (EXACT) tmin = gmin(t.x, gmin(t.y, t.z));
-    else tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
-    t = mk(t.x - tmin, t.y - tmin, t.z - tmin);
-    len += tmin;
-    const float s = len - len0;
-    cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
-    const bool ex = t.x == 0.0f, ey = t.y == 0.0f, ez = t.z == 0.0f;
-    f3 smp;
-    if (EXACT) {
-      smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
-               cur.z + (0.5f * float(ez)) * step.z);
-    } else {  // same voxel: the +-0 added on an un-crossed axis only flips the sign of a zero
-      smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f), cur.z + (ez ? hs.z : 0.0f));
+    // loop-top tests of the reference, in its order: length, TestCube, then our step cap
+    if (!(len < c.max_len) || (check && !test_cube(cur, dir, c.fn))) {
+      result = WALK_MISS;
+      break;
     }
-    // branch-free fetch: clamp to [0,N] (med3; NaN -> in range), floor; the sample is inside iff
-    // clamping left it unchanged (NaN: outside); GL_REPEAT's N -> 0 is in the padded layout
-    const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
-    const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
-    const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
-    const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
-    vi = cvt_flr(qx);
-    vj = cvt_flr(qy);
-    vk = cvt_flr(qz);
-    const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-    const uint32_t v = c.vox[pidx];
-    ties += (ey & ez) ? 1u : 0u;
-    axis = ez ? 2 : (ey ? 1 : 0);
-    // t update for the crossed axis (voxel.glsl:296/381), computed while the load is in flight
-    // (unconditionally: after an event t is dead)
-    const float pa = sel3(axis, pos.x, pos.y, pos.z);
-    const float da = sel3(axis, dir.x, dir.y, dir.z);
-    const float ca = sel3(axis, cur.x, cur.y, cur.z);
-    // sign(d) on the crossed axis; on the fast path d != 0, so it is copysign(1, d) (one v_bfi)
-    const float sa = EXACT ? sel3(axis, step.x, step.y, step.z) : __builtin_copysignf(1.0f, da);
-    const float num = (ca + sa) - pa;
-    float q;
-    if (EXACT) q = num / da;
-    else q = div_rn(num, da, sel3(axis, rcp.x, rcp.y, rcp.z));
-    q = q - s;
-    t = mk(axis == 0 ? q : t.x, axis == 1 ? q : t.y, axis == 2 ? q : t.z);
-    // loop-top tests of the NEXT iteration; TestCube can only fail after an outside sample
-    if (EXACT) {
-      cube_out = !inb && !test_cube(cur, dir, c.fn);
-    } else if (VRT_CUBE_BRANCH) {  // skipped when every lane of the wave sampled inside
-      cube_out = false;
-      if (!inb) cube_out = (cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z);
-    } else {
-      cube_out = !inb & ((cs.x * cur.x > cb.x) | (cs.y * cur.y > cb.y) | (cs.z * cur.z > cb.z));
+    if (it >= VRT_MAX_STEPS) {
+      result = WALK_CAP;
+      break;
     }
-    const bool stop = !(len < c.max_len) | cube_out | (it >= VRT_MAX_STEPS);
+    // inner loop; live-outs kept in VGPRs (a bool live out of a divergent loop costs SALU mask
+    // merges every iteration): the pre-update t (-> crossed axis), the texel coordinates, the raw
+    // byte, and pidx_sel = the padded index, or ~0 for an outside sample
+    f3 tp;
+    uint32_t vi, vj, vk, v_raw, pidx_sel;
+    // step counter of this inner loop: wave-uniform (every active lane enters together), so it
+    // lives in an SGPR; its bound keeps every lane's total <= VRT_MAX_STEPS, the exact per-lane
+    // cap is the outer test above
+    uint32_t it_max = it;
+    for (int off = 32; off > 0; off >>= 1) it_max = max(it_max, uint32_t(__shfl_xor(int(it_max), off, 64)));
+    const uint32_t k_max = __builtin_amdgcn_readfirstlane(VRT_MAX_STEPS - it_max);
+    const uint32_t it0 = it;
+    uint32_t k = 0;
+    for (;;) {
+      ++k;
+      float tmin;
+      if (EXACT) tmin = gmin(t.x, gmin(t.y, t.z));
+      else tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
+      tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+      len += tmin;
+      const float s = len - len0;
+      cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+      const bool ex = tp.x == 0.0f, ey = tp.y == 0.0f, ez = tp.z == 0.0f;
+      f3 smp;
+      if (EXACT) {
+        smp = mk(cur.x + (0.5f * float(ex)) * step.x, cur.y + (0.5f * float(ey)) * step.y,
+                 cur.z + (0.5f * float(ez)) * step.z);
+      } else {  // same voxel: the +-0 added on an un-crossed axis only flips the sign of a zero
+        smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f), cur.z + (ez ? hs.z : 0.0f));
+      }
+      // branch-free fetch: clamp to [0,N] (med3; NaN -> in range), floor; the sample is inside
+      // iff clamping left it unchanged (NaN: outside); GL_REPEAT's N -> 0 is in the layout
+      const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+      const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+      const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+      const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
+      vi = cvt_flr(qx);
+      vj = cvt_flr(qy);
+      vk = cvt_flr(qz);
+      const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
+      v_raw = c.vox[pidx];
+      if (ey & ez) ties++;  // intersectionAxis[3]: rare, a skipped branch otherwise
+      // t update for the crossed axis (voxel.glsl:296/381), while the load is in flight
+      const bool az = ez, ay = ey & !ez, ax = !ey & !ez;  // axis = ez ? 2 : ey ? 1 : 0
+      const float pa = az ? pos.z : (ay ? pos.y : pos.x);
+      const float da = az ? dir.z : (ay ? dir.y : dir.x);
+      const float ca = az ? cur.z : (ay ? cur.y : cur.x);
+      // sign(d) on the crossed axis; on the fast path d != 0, so it is copysign(1, d) (one v_bfi)
+      const float sa = EXACT ? (az ? step.z : (ay ? step.y : step.x)) : __builtin_copysignf(1.0f, da);
+      const float num = (ca + sa) - pa;
+      float q;
+      if (EXACT) q = num / da;
+      else q = div_rn(num, da, az ? rcp.z : (ay ? rcp.y : rcp.x));
+      q = q - s;
+      t = mk(ax ? q : tp.x, ay ? q : tp.y, az ? q : tp.z);
+      pidx_sel = inb ? pidx : ~0u;
+      asm volatile("" : "+v"(pidx_sel));  // materialise: no SALU live-out mask for inb
+      const bool hit = SHADOW ? (v_raw != 0u && v_raw != 2u) : (v_raw != medium);
+      if (!inb | hit | !(len < c.max_len) | (k >= k_max)) break;
+    }
+    it = it0 + k;
+    const bool inb = pidx_sel != ~0u;
     // outside samples read 0 (GetVoxel :151-152)
-    v_sel = inb ? v : 0u;
-    pidx_sel = inb ? pidx : ~0u;
-    asm volatile("" : "+v"(v_sel), "+v"(pidx_sel));  // materialise: no SALU live-out masks
-    const bool event = SHADOW ? (v_sel != 0u && v_sel != 2u) : (v_sel != medium);
-    if (event | stop) break;
+    const uint32_t v = inb ? v_raw : 0u;
+    const bool event = SHADOW ? (v != 0u && v != 2u) : (v != medium);
+    if (event) {
+      axis_out = tp.z == 0.0f ? 2 : (tp.y == 0.0f ? 1 : 0);
+      vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
+      v_out = v;
+      check = !inb;  // on re-entry (new direction after a refraction): re-test iff outside
+      result = WALK_EVENT;
+      break;
+    }
+    check = !inb;  // not an event: evaluate the next iteration's loop-top tests
   }
   w.t = t;
   w.cur = cur;
   w.len = len;
   w.it = it;
   w.ties = ties;
-  const bool event = SHADOW ? (v_sel != 0u && v_sel != 2u) : (v_sel != medium);
-  const bool inb = pidx_sel != ~0u;
-  if (event) {
-    axis_out = axis;
-    vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
-    v_out = v_sel;
-    w.check_cube = !inb;  // on re-entry (new direction after a refraction): re-test iff outside
-    return WALK_EVENT;
-  }
-  // stopped: which loop-top test fired (length first, then TestCube, then the cap)?
-  if (!(len < c.max_len)) return WALK_MISS;
-  cube_out = !inb && !test_cube(cur, dir, c.fn);
-  w.check_cube = cube_out;
-  return cube_out ? WALK_MISS : WALK_CAP;
+  w.check_cube = check;
+  return result;
 }
 
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)

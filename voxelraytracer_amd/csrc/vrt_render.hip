@@ -437,6 +437,9 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 // RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
+#ifdef VRT_ABLATE_SHADOW  // timing-only ablation build (scripts/ab.py); wrong images
+  if (ray.len >= 0.0f) return false;
+#endif
   WalkState w;
   walk_init(w, ray);
   const int r = walk_shadow(c, ray.pos, ray.len, w);
@@ -555,7 +558,7 @@ constexpr int kMaxStack = 17;
 constexpr int kCntReplicas = 256;
 
 #ifndef VRT_MIN_WAVES
-#define VRT_MIN_WAVES 5
+#define VRT_MIN_WAVES 6
 #endif
 
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
@@ -619,7 +622,11 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
     const Hit h0 = trace_with_shadow(c, ray, color, k, steps, flags);
     const int32_t hit_vidx = h0.found ? h0.vidx : -1;
     const float hit_len = h0.found ? h0.len : 0.0f;
+#ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
+    if (false) {
+#else
     if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
+#endif
       Hit h = h0;
       for (;;) {
         const uint32_t m = mat_id(h.voxel);

@@ -123,6 +123,11 @@ int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, v
  * NULL if none. */
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
 
+/* Diagnostic: copy the kernel's device volume, (N+1)^3 u16 = voxel | D << 8 (x fastest; plane N
+ * repeats plane 0 with D = 0; D = Chebyshev distance to the nearest non-empty voxel or the volume
+ * outside, capped at 32), to `out` (count >= (N+1)^3). Synchronous. */
+int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count);
+
 /* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats
  * (alpha = 1, voxel.glsl:451) to the HOST buffer out_rgba. out_hit (W*H records) and stats may
  * be NULL. */

@@ -142,6 +142,14 @@ class Renderer:
                     "vrt_upload_volume_device")
         self.n = n
 
+    def debug_packed_volume(self) -> np.ndarray:
+        """The kernel's device volume ((N+1)^3 u16 voxel | D << 8), for tests."""
+        p = self.n + 1
+        out = np.empty(p ** 3, np.uint16)
+        self._check(self._lib.vrt_debug_packed_volume(self._h, out.ctypes.data, out.size),
+                    "vrt_debug_packed_volume")
+        return out.reshape(p, p, p)
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 

@@ -139,7 +139,7 @@ struct Counters {
 };
 
 struct Ctx {
-  const uint8_t* __restrict__ vox;  // padded (N+1)^3 layout
+  const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | D << 8 (see pack kernel)
   int32_t n;
   uint32_t p;  // N + 1
   float fn;
@@ -168,7 +168,7 @@ __device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p) {
   const uint32_t i = uint32_t(__builtin_floorf(p.x));
   const uint32_t j = uint32_t(__builtin_floorf(p.y));
   const uint32_t k = uint32_t(__builtin_floorf(p.z));
-  return c.vox[mad24(mad24(k, c.p, j), c.p, i)];
+  return c.vox[mad24(mad24(k, c.p, j), c.p, i)] & 0xFFu;
 }
 
 // TestCube (voxel.glsl:248-257) with centre N/2 and size N; bitwise ops, no short-circuit branches.
@@ -310,7 +310,7 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
       vj = cvt_flr(qy);
       vk = cvt_flr(qz);
       const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-      v_raw = c.vox[pidx];
+      v_raw = c.vox[pidx] & 0xFFu;
       if (ey & ez) ties++;  // intersectionAxis[3]: rare, a skipped branch otherwise
       // t update for the crossed axis (voxel.glsl:296/381), while the load is in flight
       const bool az = ez, ay = ey & !ez, ax = !ey & !ez;  // axis = ez ? 2 : ey ? 1 : 0
@@ -354,13 +354,132 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
   return result;
 }
 
+// ---------------------------------------------------------------- empty-space step skipping --
+//
+// The packed volume carries, per voxel v, D(v) = the Chebyshev distance (in voxels, capped at
+// kDistCap) to the nearest non-empty voxel or to the outside of the volume, so every voxel of the
+// box [v-D+1, v+D-1]^3 is empty and inside. After a sampled step whose texel is empty with D >= 2,
+// an air ray (or a shadow ray) computes s_lim, the ray parameter up to which its position provably
+// stays inside that box on every axis (box faces v+D and v+1-D pulled in by kSkipMargin, far above
+// the float error of cur = pos + s*dir). A step with s < s_lim therefore samples an empty voxel
+// inside the volume — no event, no TestCube — and needs only the exact DDA state update; the
+// sample, its address and the load are skipped. Every float op that defines the walk's state is
+// still executed, in the reference's order, so the walk is bit-identical.
+constexpr uint32_t kDistCap = 32;
+constexpr float kSkipMargin = 1.0f / 256.0f;
+
+template <bool SHADOW>
+__device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
+                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
+                                         int32_t& vidx_out, uint32_t& v_out) {
+  // fast path: every dir component is non-zero, so sign(d) = copysign(1, d)
+  const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
+                     __builtin_copysignf(1.0f, dir.z));
+  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
+  // skip-box face in travel direction: B = (v + c0) + sgn * (D - margin); c0 = 0 / 1 for d > 0 / < 0
+  const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
+  const bool skip_ok = SHADOW || medium == 0u;
+  f3 t = w.t, cur = w.cur;
+  float len = w.len;
+  uint32_t it = w.it, ties = w.ties;
+  bool check = w.check_cube;
+  int result;
+  for (;;) {
+    // loop-top tests of the reference, in its order: length, TestCube, then our step cap
+    if (!(len < c.max_len) || (check && !test_cube(cur, dir, c.fn))) {
+      result = WALK_MISS;
+      break;
+    }
+    if (it >= VRT_MAX_STEPS) {
+      result = WALK_CAP;
+      break;
+    }
+    f3 tp;
+    // v_raw / pidx_sel (the padded index, ~0 when outside) are written only by sampled steps: a
+    // skip window opens only after an in-volume empty sample, so during it they already hold the
+    // values of an empty in-volume texel, which is exactly what a skipped step would read.
+    uint32_t vi = 0, vj = 0, vk = 0, v_raw = 0u, pidx_sel = 0u;
+    uint32_t it_max = it;
+    for (int off = 32; off > 0; off >>= 1) it_max = max(it_max, uint32_t(__shfl_xor(int(it_max), off, 64)));
+    const uint32_t k_max = __builtin_amdgcn_readfirstlane(VRT_MAX_STEPS - it_max);
+    const uint32_t it0 = it;
+    uint32_t k = 0;
+    float s_lim = -1.0f;  // no skip window yet: the first step samples
+    for (;;) {
+      ++k;
+      const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
+      tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+      len += tmin;
+      const float s = len - len0;
+      const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
+      ties += (ey & ez) ? 1u : 0u;  // intersectionAxis[3]
+      // t update for the crossed axis (voxel.glsl:296/381)
+      const bool az = ez, ay = ey & !ez, ax = !ey & !ez;
+      const float pa = az ? pos.z : (ay ? pos.y : pos.x);
+      const float da = az ? dir.z : (ay ? dir.y : dir.x);
+      const float ra = az ? rcp.z : (ay ? rcp.y : rcp.x);
+      const float ca = pa + s * da;  // == cur on that axis: the same two ops
+      const float num = (ca + __builtin_copysignf(1.0f, da)) - pa;
+      const float q = div_rn(num, da, ra) - s;
+      t = mk(ax ? q : tp.x, ay ? q : tp.y, az ? q : tp.z);
+      asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
+      if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
+        cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+        const bool ex = tp.x == 0.0f;
+        const f3 smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f),
+                          cur.z + (ez ? hs.z : 0.0f));
+        const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+        const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+        const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+        const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
+        vi = cvt_flr(qx);
+        vj = cvt_flr(qy);
+        vk = cvt_flr(qz);
+        const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
+        const uint32_t packed = c.vox[pidx];
+        v_raw = packed & 0xFFu;
+        const uint32_t dist = packed >> 8;
+        pidx_sel = inb ? pidx : ~0u;
+        const float fd = float(dist) - kSkipMargin;
+        const float lx = ((float(vi) + c0.x) + step.x * fd - pos.x) * rcp.x;
+        const float ly = ((float(vj) + c0.y) + step.y * fd - pos.y) * rcp.y;
+        const float lz = ((float(vk) + c0.z) + step.z * fd - pos.z) * rcp.z;
+        const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
+        s_lim = open ? __builtin_fminf(lx, __builtin_fminf(ly, lz)) : -1.0f;
+      }
+      const bool hit = SHADOW ? (v_raw != 0u && v_raw != 2u) : (v_raw != medium);
+      if ((pidx_sel == ~0u) | hit | !(len < c.max_len) | (k >= k_max)) break;
+    }
+    it = it0 + k;
+    const bool inb = pidx_sel != ~0u;
+    const uint32_t v = inb ? v_raw : 0u;  // outside samples read 0 (GetVoxel :151-152)
+    const bool event = SHADOW ? (v != 0u && v != 2u) : (v != medium);
+    if (event) {  // events only come from sampled steps, whose cur and texel are fresh
+      axis_out = tp.z == 0.0f ? 2 : (tp.y == 0.0f ? 1 : 0);
+      vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
+      v_out = v;
+      check = !inb;
+      result = WALK_EVENT;
+      break;
+    }
+    check = !inb;  // not an event: evaluate the next iteration's loop-top tests
+  }
+  w.t = t;
+  w.cur = cur;
+  w.len = len;
+  w.it = it;
+  w.ties = ties;
+  w.check_cube = check;
+  return result;
+}
+
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    return dda_walk<false, false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -371,7 +490,7 @@ __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len
   int32_t vidx;
   uint32_t v;
   if (__builtin_expect(fast_path_ok(c.sun_n), 1))
-    return dda_walk<true, false>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    return skip_walk<true>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
 
@@ -564,7 +683,7 @@ constexpr int kCntReplicas = 256;
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
 // The primary ray (stack[0] of the reference) stays in registers; the scratch stack only ever
 // holds secondary rays, so pixels that spawn none never touch it.
-__global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, const uint8_t* __restrict__ vox,
+__global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
@@ -684,16 +803,49 @@ __global__ void __launch_bounds__(64) reduce_counters_kernel(unsigned long long*
   dst[q] += s;
 }
 
-// Re-layout N^3 (x fastest) into the padded (N+1)^3 device format: plane N repeats plane 0.
-__global__ void __launch_bounds__(256) pad_volume_kernel(const uint8_t* __restrict__ src,
-                                                         uint8_t* __restrict__ dst, uint32_t n) {
+// Chebyshev distance field, one separable pass per axis (x, then y, then z), capped at
+// kDistCap: out(v) = min(kDistCap, distance to the boundary pseudo-voxels -1 and N on this axis,
+// min over |o| < kDistCap of max(|o|, in(v + o e_axis))), where the x pass reads in = 0 for a
+// non-empty voxel and kDistCap otherwise. The composition is the exact L-inf distance transform
+// (capped), so D(v) >= 1 guarantees an empty box of half-width D-1 around v inside the volume.
+__global__ void __launch_bounds__(256) dist_pass_kernel(const uint8_t* __restrict__ in,
+                                                        uint8_t* __restrict__ out, uint32_t n,
+                                                        int axis, int first) {
+  const uint64_t total = uint64_t(n) * n * n;
+  const uint64_t stride = axis == 0 ? 1u : (axis == 1 ? uint64_t(n) : uint64_t(n) * n);
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
+       q += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t coord = uint32_t((q / stride) % n);
+    uint32_t d = min(min(coord + 1u, n - coord), kDistCap);
+    for (uint32_t o = 0; o < kDistCap && o < d; ++o) {
+      // neighbours at offset -o and +o along the axis
+      for (int sgn = -1; sgn <= 1; sgn += 2) {
+        if (o == 0 && sgn > 0) break;
+        const int64_t cc = int64_t(coord) + sgn * int64_t(o);
+        if (cc < 0 || cc >= int64_t(n)) continue;
+        const uint8_t v = in[uint64_t(int64_t(q) + (cc - int64_t(coord)) * int64_t(stride))];
+        const uint32_t val = first ? (v != 0 ? 0u : kDistCap) : uint32_t(v);
+        d = min(d, max(o, val));
+      }
+    }
+    out[q] = uint8_t(d);
+  }
+}
+
+// Pack into the kernel's padded (N+1)^3 format: voxel | D << 8, plane N repeats plane 0 (GL_REPEAT
+// folded into the layout) with D = 0 there (those texels are only read at c == N exactly).
+__global__ void __launch_bounds__(256) pack_volume_kernel(const uint8_t* __restrict__ src,
+                                                          const uint8_t* __restrict__ dist,
+                                                          uint16_t* __restrict__ dst, uint32_t n) {
   const uint32_t p = n + 1u;
   const uint64_t total = uint64_t(p) * p * p;
   for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
        q += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t i = uint32_t(q % p), j = uint32_t((q / p) % p), k = uint32_t(q / (uint64_t(p) * p));
+    const bool edge = i == n || j == n || k == n;
     const uint32_t si = i == n ? 0u : i, sj = j == n ? 0u : j, sk = k == n ? 0u : k;
-    dst[q] = src[si + (uint64_t(sj) + uint64_t(sk) * n) * n];
+    const uint64_t sq = si + (uint64_t(sj) + uint64_t(sk) * n) * n;
+    dst[q] = uint16_t(src[sq] | (edge ? 0u : uint32_t(dist[sq]) << 8));
   }
 }
 
@@ -703,8 +855,9 @@ __global__ void __launch_bounds__(256) pad_volume_kernel(const uint8_t* __restri
 
 struct vrt_ctx {
   int device = 0;
-  uint8_t* d_vox = nullptr;      // canonical N^3
-  uint8_t* d_vox_pad = nullptr;  // padded (N+1)^3, the kernel's format
+  uint8_t* d_vox = nullptr;       // canonical N^3
+  uint8_t* d_tmp = nullptr;       // 2 x N^3 distance-field scratch
+  uint16_t* d_vox_pad = nullptr;  // padded (N+1)^3 voxel | D << 8, the kernel's format
   int32_t n = 0;
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
@@ -789,31 +942,40 @@ int volume_alloc(vrt_ctx* ctx, int32_t n) {
   VRT_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->d_vox && ctx->n != n) {
     (void)hipFree(ctx->d_vox);
+    (void)hipFree(ctx->d_tmp);
     (void)hipFree(ctx->d_vox_pad);
-    ctx->d_vox = ctx->d_vox_pad = nullptr;
+    ctx->d_vox = ctx->d_tmp = nullptr;
+    ctx->d_vox_pad = nullptr;
   }
   if (!ctx->d_vox) {
-    const size_t bytes = size_t(n) * n * n, pbytes = size_t(n + 1) * (n + 1) * (n + 1);
-    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess) {
-      ctx->d_vox = nullptr;
-      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume");
-    }
-    if (hipMalloc(&ctx->d_vox_pad, pbytes) != hipSuccess) {
-      (void)hipFree(ctx->d_vox);
-      ctx->d_vox = ctx->d_vox_pad = nullptr;
-      return fail(ctx, VRT_ERR_OOM, "hipMalloc padded volume");
+    const size_t bytes = size_t(n) * n * n, pbytes = size_t(n + 1) * (n + 1) * (n + 1) * 2;
+    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess || hipMalloc(&ctx->d_tmp, 2 * bytes) != hipSuccess ||
+        hipMalloc(&ctx->d_vox_pad, pbytes) != hipSuccess) {
+      if (ctx->d_vox) (void)hipFree(ctx->d_vox);
+      if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
+      if (ctx->d_vox_pad) (void)hipFree(ctx->d_vox_pad);
+      ctx->d_vox = ctx->d_tmp = nullptr;
+      ctx->d_vox_pad = nullptr;
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume buffers");
     }
   }
   ctx->n = n;
   return VRT_OK;
 }
 
+// Distance field (3 passes) + padded packing on the GPU, then wait (upload is not a hot call).
 int volume_finish(vrt_ctx* ctx, hipStream_t s) {
-  const uint64_t p = uint64_t(ctx->n) + 1;
-  const uint64_t total = p * p * p;
-  const unsigned blocks = unsigned(std::min<uint64_t>((total + 255) / 256, 8192));
-  hipLaunchKernelGGL(vrt::pad_volume_kernel, dim3(blocks), dim3(256), 0, s, ctx->d_vox,
-                     ctx->d_vox_pad, uint32_t(ctx->n));
+  const uint32_t n = uint32_t(ctx->n);
+  const uint64_t vol = uint64_t(n) * n * n, pvol = uint64_t(n + 1) * (n + 1) * (n + 1);
+  const unsigned b1 = unsigned(std::min<uint64_t>((vol + 255) / 256, 16384));
+  const unsigned b2 = unsigned(std::min<uint64_t>((pvol + 255) / 256, 16384));
+  uint8_t* da = ctx->d_tmp;
+  uint8_t* db = ctx->d_tmp + vol;
+  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, 1);
+  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, 0);
+  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, db, da, n, 2, 0);
+  hipLaunchKernelGGL(vrt::pack_volume_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, da,
+                     ctx->d_vox_pad, n);
   VRT_HIP(ctx, hipGetLastError());
   VRT_HIP(ctx, hipStreamSynchronize(s));
   ctx->err.clear();
@@ -851,6 +1013,7 @@ void vrt_destroy(vrt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->d_vox) (void)hipFree(c->d_vox);
   if (c->d_vox_pad) (void)hipFree(c->d_vox_pad);
+  if (c->d_tmp) (void)hipFree(c->d_tmp);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_hit) (void)hipFree(c->d_hit);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
@@ -884,6 +1047,16 @@ int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, v
 }
 
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->d_vox : nullptr; }
+
+int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
+  const uint64_t p = uint64_t(ctx->n) + 1, total = p * p * p;
+  if (!out || count < total) return fail(ctx, VRT_ERR_INVALID, "output smaller than (N+1)^3");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  VRT_HIP(ctx, hipMemcpy(out, ctx->d_vox_pad, total * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  return VRT_OK;
+}
 
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
                           int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,

@@ -27,6 +27,8 @@ from bench import CONFIGS  # noqa: E402
 def load(path):
     lib = C.CDLL(path)
     for name, (res, args) in abi.SIGNATURES.items():
+        if not hasattr(lib, name):   # older variant builds may lack newer diagnostic symbols
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

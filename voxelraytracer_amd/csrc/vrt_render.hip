@@ -148,8 +148,17 @@ struct Ctx {
   float time, refl_noise, refr_noise;
 };
 
+// a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024)
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
-  return __umul24(a, b) + c;  // v_mad_u32_u24 (operands < 2^24: N <= 1024)
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// 16-bit load at a 32-bit byte offset from a wave-uniform base: global_load_ushort with an SGPR
+// base (no 64-bit address arithmetic per lane)
+__device__ __forceinline__ uint32_t load_u16(const uint16_t* __restrict__ base, uint32_t idx) {
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(base) + (idx << 1));
 }
 
 __device__ __forceinline__ int32_t canonical_index(const Ctx& c, uint32_t i, uint32_t j, uint32_t k) {
@@ -168,7 +177,7 @@ __device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p) {
   const uint32_t i = uint32_t(__builtin_floorf(p.x));
   const uint32_t j = uint32_t(__builtin_floorf(p.y));
   const uint32_t k = uint32_t(__builtin_floorf(p.z));
-  return c.vox[mad24(mad24(k, c.p, j), c.p, i)] & 0xFFu;
+  return load_u16(c.vox, mad24(mad24(k, c.p, j), c.p, i)) & 0xFFu;
 }
 
 // TestCube (voxel.glsl:248-257) with centre N/2 and size N; bitwise ops, no short-circuit branches.
@@ -310,7 +319,7 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
       vj = cvt_flr(qy);
       vk = cvt_flr(qz);
       const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-      v_raw = c.vox[pidx] & 0xFFu;
+      v_raw = load_u16(c.vox, pidx) & 0xFFu;
       if (ey & ez) ties++;  // intersectionAxis[3]: rare, a skipped branch otherwise
       // t update for the crossed axis (voxel.glsl:296/381), while the load is in flight
       const bool az = ez, ay = ey & !ez, ax = !ey & !ez;  // axis = ez ? 2 : ey ? 1 : 0
@@ -436,7 +445,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         vj = cvt_flr(qy);
         vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-        const uint32_t packed = c.vox[pidx];
+        const uint32_t packed = load_u16(c.vox, pidx);
         v_raw = packed & 0xFFu;
         const uint32_t dist = packed >> 8;
         pidx_sel = inb ? pidx : ~0u;
@@ -455,7 +464,9 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     const uint32_t v = inb ? v_raw : 0u;  // outside samples read 0 (GetVoxel :151-152)
     const bool event = SHADOW ? (v != 0u && v != 2u) : (v != medium);
     if (event) {  // events only come from sampled steps, whose cur and texel are fresh
-      axis_out = tp.z == 0.0f ? 2 : (tp.y == 0.0f ? 1 : 0);
+      float ty = tp.y, tz = tp.z;
+      asm volatile("" : "+v"(ty), "+v"(tz));  // recompute here: no per-step live-out masks
+      axis_out = tz == 0.0f ? 2 : (ty == 0.0f ? 1 : 0);
       vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
       v_out = v;
       check = !inb;

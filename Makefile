@@ -5,8 +5,9 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 LIBDIR := voxelraytracer_amd/_lib
+# -fno-slp-vectorize: packed-FP32 (v_pk_*) ops take two issue slots on gfx950, no gain here
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
-            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Wall
+            -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -Iinclude -Wall
 SRC := voxelraytracer_amd/csrc/vrt_render.hip voxelraytracer_amd/csrc/vrt_host.cpp
 
 all: $(LIBDIR)/libvrt.so oracle

@@ -404,10 +404,12 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       break;
     }
     f3 tp;
-    // v_raw / pidx_sel (the padded index, ~0 when outside) are written only by sampled steps: a
-    // skip window opens only after an in-volume empty sample, so during it they already hold the
-    // values of an empty in-volume texel, which is exactly what a skipped step would read.
-    uint32_t vi = 0, vj = 0, vk = 0, v_raw = 0u, pidx_sel = 0u;
+    // v_ev = the sampled byte, or kOutside for a sample outside the volume (which reads 0 but
+    // must stop the inner loop); pidx = its padded index. Both are written only by sampled
+    // steps: a skip window opens only after an in-volume empty sample, so during it they hold
+    // the values of an empty in-volume texel, exactly what a skipped step would read.
+    constexpr uint32_t kOutside = 0x100u;
+    uint32_t vi = 0, vj = 0, vk = 0, v_ev = 0u;
     uint32_t it_max = it;
     for (int off = 32; off > 0; off >>= 1) it_max = max(it_max, uint32_t(__shfl_xor(int(it_max), off, 64)));
     const uint32_t k_max = __builtin_amdgcn_readfirstlane(VRT_MAX_STEPS - it_max);
@@ -415,6 +417,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     uint32_t k = 0;
     float s_lim = -1.0f;  // no skip window yet: the first step samples
     for (;;) {
+      if (k >= k_max) break;  // wave-uniform step bound (scalar branch)
       ++k;
       const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
       tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
@@ -446,9 +449,9 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
         const uint32_t packed = load_u16(c.vox, pidx);
-        v_raw = packed & 0xFFu;
+        const uint32_t v_raw = packed & 0xFFu;
         const uint32_t dist = packed >> 8;
-        pidx_sel = inb ? pidx : ~0u;
+        v_ev = inb ? v_raw : kOutside;
         const float fd = float(dist) - kSkipMargin;
         const float lx = ((float(vi) + c0.x) + step.x * fd - pos.x) * rcp.x;
         const float ly = ((float(vj) + c0.y) + step.y * fd - pos.y) * rcp.y;
@@ -456,12 +459,14 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
         s_lim = open ? __builtin_fminf(lx, __builtin_fminf(ly, lz)) : -1.0f;
       }
-      const bool hit = SHADOW ? (v_raw != 0u && v_raw != 2u) : (v_raw != medium);
-      if ((pidx_sel == ~0u) | hit | !(len < c.max_len) | (k >= k_max)) break;
+      // stop the inner loop on: outside sample, a byte that is an event, the length
+      const bool stop = SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium);
+      if (stop | !(len < c.max_len)) break;
     }
     it = it0 + k;
-    const bool inb = pidx_sel != ~0u;
-    const uint32_t v = inb ? v_raw : 0u;  // outside samples read 0 (GetVoxel :151-152)
+    asm volatile("" : "+v"(v_ev));  // decide here, from the VGPR (no per-step live-out masks)
+    const bool inb = v_ev != kOutside;
+    const uint32_t v = inb ? v_ev : 0u;  // outside samples read 0 (GetVoxel :151-152)
     const bool event = SHADOW ? (v != 0u && v != 2u) : (v != medium);
     if (event) {  // events only come from sampled steps, whose cur and texel are fresh
       float ty = tp.y, tz = tp.z;

@@ -241,6 +241,19 @@ __device__ __forceinline__ uint32_t cvt_flr(float x) {
   return uint32_t(r);
 }
 
+// Max of x over the ACTIVE lanes only, as a wave-uniform value. (A __shfl reduction would also
+// read inactive lanes' stale registers, e.g. a step count of a lane that already stopped at the
+// cap, and stall the others.) Scalar loop: each round takes the value of an active lane holding a
+// larger x (ballot covers active lanes only), so it ends after <= 64 rounds, usually one.
+__device__ __forceinline__ uint32_t active_max(uint32_t x) {
+  uint32_t m = __builtin_amdgcn_readfirstlane(x);
+  for (;;) {
+    const unsigned long long bigger = __ballot(x > m);
+    if (bigger == 0ull) return m;
+    m = __builtin_amdgcn_readlane(x, int(__builtin_ctzll(bigger)));
+  }
+}
+
 // keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
@@ -287,9 +300,7 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
     // step counter of this inner loop: wave-uniform (every active lane enters together), so it
     // lives in an SGPR; its bound keeps every lane's total <= VRT_MAX_STEPS, the exact per-lane
     // cap is the outer test above
-    uint32_t it_max = it;
-    for (int off = 32; off > 0; off >>= 1) it_max = max(it_max, uint32_t(__shfl_xor(int(it_max), off, 64)));
-    const uint32_t k_max = __builtin_amdgcn_readfirstlane(VRT_MAX_STEPS - it_max);
+    const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
     const uint32_t it0 = it;
     uint32_t k = 0;
     for (;;) {
@@ -410,9 +421,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     // the values of an empty in-volume texel, exactly what a skipped step would read.
     constexpr uint32_t kOutside = 0x100u;
     uint32_t vi = 0, vj = 0, vk = 0, v_ev = 0u;
-    uint32_t it_max = it;
-    for (int off = 32; off > 0; off >>= 1) it_max = max(it_max, uint32_t(__shfl_xor(int(it_max), off, 64)));
-    const uint32_t k_max = __builtin_amdgcn_readfirstlane(VRT_MAX_STEPS - it_max);
+    const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
     const uint32_t it0 = it;
     uint32_t k = 0;
     float s_lim = -1.0f;  // no skip window yet: the first step samples

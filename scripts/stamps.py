@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Wave timeline of one render from the diagnostic build (make variant NAME=stamps
+DEFS=-DVRT_STAMPS; run with VRT_LIB=build/variants/libvrt_stamps.so).
+
+Each wave of render_kernel records s_memrealtime (100 MHz) at entry and exit plus its HW_ID /
+XCC_ID. Prints, per config: the kernel span, wave-duration quantiles, the busy fraction of the
+wave slots (sum of wave durations / (span x slots)), how the span splits into ramp (until every
+slot has started a wave), steady state and tail (after the last wave started), and the per-XCD
+finish times. Optional --save writes the raw stamps (npz) for plotting.
+Usage: VRT_LIB=build/variants/libvrt_stamps.so python scripts/stamps.py [--configs C3] [--save d]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import voxelraytracer_amd as vrt  # noqa: E402
+from voxelraytracer_amd import abi  # noqa: E402
+from bench import CONFIGS  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C3")
+    ap.add_argument("--wg-waves", type=int, default=4)
+    ap.add_argument("--slots", type=int, default=256 * 4 * 6, help="wave slots (CUs*SIMDs*occupancy)")
+    ap.add_argument("--save", default="")
+    args = ap.parse_args()
+    lib = abi.load_library()
+    if not hasattr(lib, "vrt_debug_stamps"):
+        sys.exit("VRT_LIB must point at the VRT_STAMPS diagnostic build")
+    lib.vrt_debug_stamps.restype = C.c_int
+    lib.vrt_debug_stamps.argtypes = [C.c_void_p, C.c_uint64]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    report = {}
+    for cfg in args.configs.split(","):
+        scene, n, w, h, R, T, _ = CONFIGS[cfg]
+        cam = vrt.make_camera(w, h)
+        params = vrt.default_params(R, T)
+        vox = torch.from_numpy(vrt.build_scene(scene, n)).to(dev)
+        out = torch.empty((h, w, 4), dtype=torch.float32, device=dev)
+        with vrt.Renderer(0) as ren:
+            ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
+            for _ in range(5):   # warm; the stamps of the last launch are kept
+                ren.render_rows_async(cam, params, 0, h, 1, out.data_ptr(), 0, 0, stream.cuda_stream)
+            torch.cuda.synchronize()
+        tw, th = (16, 16) if args.wg_waves == 4 else ((16, 8) if args.wg_waves == 2 else (8, 8))
+        waves = ((w + tw - 1) // tw) * ((h + th - 1) // th) * args.wg_waves
+        st = np.zeros((waves, 3), dtype=np.uint64)
+        assert lib.vrt_debug_stamps(st.ctypes.data, st.size) == 0
+        t0 = st[:, 0].min()
+        start = (st[:, 0] - t0).astype(np.float64) * 10.0   # ns (100 MHz)
+        end = (st[:, 1] - t0).astype(np.float64) * 10.0
+        dur = end - start
+        span = end.max()
+        xcc = (st[:, 2] >> np.uint64(32)).astype(np.int64) & 0xF
+        order = np.sort(start)
+        ramp = order[min(args.slots, waves) - 1]          # all slots have started a wave
+        last_start = order[-1]
+        q = np.quantile(dur, [0.0, 0.1, 0.5, 0.9, 0.99, 1.0])
+        r = dict(
+            waves=int(waves), span_us=span / 1e3,
+            wave_us_quantiles=dict(zip(["min", "p10", "p50", "p90", "p99", "max"],
+                                       [round(x / 1e3, 2) for x in q])),
+            slot_busy_frac=float(dur.sum() / (span * args.slots)),
+            ramp_us=ramp / 1e3, last_start_us=last_start / 1e3,
+            tail_us=(span - last_start) / 1e3,
+            xcd_finish_us={int(x): round(float(end[xcc == x].max()) / 1e3, 1)
+                           for x in np.unique(xcc)},
+            xcd_wave_ms_sum={int(x): round(float(dur[xcc == x].sum()) / 1e6, 2)
+                             for x in np.unique(xcc)},
+        )
+        # busy slots over time (10 bins): how many waves are resident
+        edges = np.linspace(0, span, 11)
+        mids = (edges[:-1] + edges[1:]) / 2
+        r["resident_waves_over_time"] = [int(((start <= m) & (end > m)).sum()) for m in mids]
+        report[cfg] = r
+        print(cfg, json.dumps(r))
+        if args.save:
+            os.makedirs(args.save, exist_ok=True)
+            np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st)
+    return report
+
+
+if __name__ == "__main__":
+    main()

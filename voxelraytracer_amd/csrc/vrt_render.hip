@@ -254,6 +254,16 @@ __device__ __forceinline__ uint32_t active_max(uint32_t x) {
   }
 }
 
+// x + (a && b ? 1 : 0) as one v_addc with the lane mask as carry-in (active lanes only). The
+// masks of a and b are taken separately (each a plain v_cmp result) and ANDed in SALU; a ballot
+// of the combined bool would be materialised in a VGPR first.
+__device__ __forceinline__ uint32_t add_if_both(uint32_t x, bool a, bool b) {
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b);
+  unsigned long long co;
+  asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(x), "=s"(co) : "s"(m));
+  return x;
+}
+
 // keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
@@ -399,6 +409,9 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   // skip-box face in travel direction: B = (v + c0) + sgn * (D - margin); c0 = 0 / 1 for d > 0 / < 0
   const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
   const bool skip_ok = SHADOW || medium == 0u;
+  // Skip windows also end where the length test could first fail: s = fl(len - len0) is
+  // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
+  const float s_len = c.max_len - len0;
   f3 t = w.t, cur = w.cur;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
@@ -433,7 +446,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       len += tmin;
       const float s = len - len0;
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
-      ties += (ey & ez) ? 1u : 0u;  // intersectionAxis[3]
+      ties = add_if_both(ties, ey, ez);  // intersectionAxis[3]
       // t update for the crossed axis (voxel.glsl:296/381)
       const bool az = ez, ay = ey & !ez, ax = !ey & !ez;
       const float pa = az ? pos.z : (ay ? pos.y : pos.x);
@@ -466,11 +479,13 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const float ly = ((float(vj) + c0.y) + step.y * fd - pos.y) * rcp.y;
         const float lz = ((float(vk) + c0.z) + step.z * fd - pos.z) * rcp.z;
         const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
-        s_lim = open ? __builtin_fminf(lx, __builtin_fminf(ly, lz)) : -1.0f;
+        s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
+        // stop the inner loop on: outside sample, a byte that is an event, the length. Only a
+        // sampled step can stop it: a skipped one reads an empty in-volume texel and has
+        // s < s_len, hence len < max_len (see s_len).
+        const bool stop = SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium);
+        if (stop | !(len < c.max_len)) break;
       }
-      // stop the inner loop on: outside sample, a byte that is an event, the length
-      const bool stop = SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium);
-      if (stop | !(len < c.max_len)) break;
     }
     it = it0 + k;
     asm volatile("" : "+v"(v_ev));  // decide here, from the VGPR (no per-step live-out masks)
@@ -697,6 +712,46 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 
 constexpr int kMaxStack = 17;
 
+// Lane id as a fresh (volatile) value each call, so the compiler cannot keep one copy alive
+// across the whole trace.
+__device__ __forceinline__ uint32_t lane_id() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+// Waves per workgroup (1, 2 or 4): each wave renders an 8x8 pixel tile; a workgroup covers
+// 8x8, 16x8 or 16x16 pixels (wave = threadIdx.x >> 6, uniform).
+#ifndef VRT_WG_WAVES
+#define VRT_WG_WAVES 4
+#endif
+static_assert(VRT_WG_WAVES == 1 || VRT_WG_WAVES == 2 || VRT_WG_WAVES == 4, "1, 2 or 4 waves");
+constexpr int kWgThreads = 64 * VRT_WG_WAVES;
+constexpr int kTileW = VRT_WG_WAVES >= 2 ? 16 : 8;
+constexpr int kTileH = VRT_WG_WAVES == 4 ? 16 : 8;
+__device__ __forceinline__ int pixel_x(int wave, uint32_t lane) {
+  return int(blockIdx.x) * kTileW + (wave & 1) * 8 + int(lane & 7u);
+}
+__device__ __forceinline__ int pixel_row(int wave, uint32_t lane) {
+  return int(blockIdx.y) * kTileH + (wave >> 1) * 8 + int(lane >> 3);
+}
+
+#ifdef VRT_STAMPS
+// Diagnostic build only (scripts/stamps.py): per wave {start, end} s_memrealtime (100 MHz) and
+// {HW_ID, XCC_ID}, indexed by the linear wave id. Never part of the product library.
+constexpr int kMaxStampWaves = 1 << 18;
+__device__ unsigned long long g_stamps[kMaxStampWaves][3];
+__device__ __forceinline__ uint32_t hw_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v;
+}
+#endif
+
 // Counter replicas: one 64-bit add per wave and counter into replica (block % kCntReplicas);
 // a single array would serialise ~300K same-address atomics per 1080p frame at the memory side.
 constexpr int kCntReplicas = 256;
@@ -708,13 +763,20 @@ constexpr int kCntReplicas = 256;
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
 // The primary ray (stack[0] of the reference) stays in registers; the scratch stack only ever
 // holds secondary rays, so pixels that spawn none never touch it.
-__global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
+__global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  // The pixel is re-derived after the trace from wave-uniform SGPRs and a fresh lane id instead
+  // of being kept alive across it: at 80 VGPRs the long-lived copies were spilled to scratch by
+  // every wave (~1.8 KB/wave of scratch writes, most of the excess WRITE_SIZE over the frame).
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+#ifdef VRT_STAMPS
+  const uint32_t wave_lin = (blockIdx.y * gridDim.x + blockIdx.x) * VRT_WG_WAVES + wave;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int px = pixel_x(wave, lane_id());
+  const int li = pixel_row(wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
 
   Counters k;
@@ -790,7 +852,8 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
         h = trace_with_shadow(c, ray, color, k, steps, flags);
       }
     }
-    const size_t o = size_t(li) * size_t(a.width) + size_t(px);
+    const uint32_t l2 = lane_id();
+    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.width) + size_t(pixel_x(wave, l2));
     out[o] = make_float4(color.x, color.y, color.z, 1.0f);
     if (hits) {
       vrt_hit hr;
@@ -802,6 +865,16 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
     }
   }
 
+#ifdef VRT_STAMPS
+  {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    if (lane_id() == 0 && wave_lin < kMaxStampWaves) {
+      g_stamps[wave_lin][0] = t_start;
+      g_stamps[wave_lin][1] = t_end;
+      g_stamps[wave_lin][2] = (unsigned long long)xcc_id() << 32 | hw_id();
+    }
+  }
+#endif
   if (counters) {
     unsigned long long* slot =
         counters + size_t((blockIdx.y * gridDim.x + blockIdx.x) % kCntReplicas) * VRT_CNT_COUNT;
@@ -810,7 +883,7 @@ __global__ void __launch_bounds__(256, VRT_MIN_WAVES) render_kernel(KArgs a, con
       unsigned long long v = k.c[q];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0 && v) atomicAdd(slot + q, v);
+      if (lane_id() == 0 && v) atomicAdd(slot + q, v);
     }
   }
 }
@@ -955,8 +1028,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
 // Render kernel, then (when counting) fold the replicas into `cnt` (accumulate) and re-zero them.
 void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
-  dim3 grid((a.width + 15) / 16, (a.rows + 15) / 16);
-  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(256), 0, s, a, ctx->d_vox_pad, out, hit,
+  dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
+  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
                      cnt ? ctx->d_cnt_rep : nullptr);
   if (cnt) hipLaunchKernelGGL(vrt::reduce_counters_kernel, dim3(1), dim3(64), 0, s, ctx->d_cnt_rep, cnt);
 }
@@ -1082,6 +1155,15 @@ int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count) {
   VRT_HIP(ctx, hipMemcpy(out, ctx->d_vox_pad, total * sizeof(uint16_t), hipMemcpyDeviceToHost));
   return VRT_OK;
 }
+
+#ifdef VRT_STAMPS
+// diagnostic build only: copy the per-wave stamps of the last render (count = 3 x waves)
+int vrt_debug_stamps(uint64_t* out, uint64_t count) {
+  if (!out || count > 3ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps), count * 8) == hipSuccess ? VRT_OK
+                                                                                     : VRT_ERR_DEVICE;
+}
+#endif
 
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
                           int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,

@@ -4,7 +4,9 @@
 Each library is loaded as its own ctypes handle (RTLD_LOCAL); every round renders each config
 once per variant in turn, so clock/thermal drift hits all variants alike. Prints the median and
 min kernel ms per (variant, config) and checks that all variants agree bit-exactly on the image.
-Usage: python scripts/ab.py [--rounds 10] [--configs C1,C2,C3]
+Each timed sample is --batch back-to-back launches (per-launch mean), which averages out the
+launch-to-launch jitter of single-event timings.
+Usage: python scripts/ab.py [--rounds 10] [--batch 8] [--configs C1,C2,C3]
 """
 import argparse
 import ctypes as C
@@ -39,6 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--configs", default="C1,C2,C3")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="back-to-back launches per timed sample (ms reported per launch)")
     args = ap.parse_args()
     libs = {"base": abi.LIB_PATH}
     for p in sorted(glob.glob(os.path.join(ROOT, "build", "variants", "libvrt_*.so"))):
@@ -66,16 +70,19 @@ def main():
             for name, (L, h) in handles.items():
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
+                nb = 1 if r == 0 else args.batch
                 e0.record(stream)
-                rc = L.vrt_render_rows_async(h, C.byref(cam), C.byref(p), 0, hgt, 1,
-                                             outs[name].data_ptr(), None, None, stream.cuda_stream)
-                assert rc == 0
+                for _ in range(nb):
+                    rc = L.vrt_render_rows_async(h, C.byref(cam), C.byref(p), 0, hgt, 1,
+                                                 outs[name].data_ptr(), None, None,
+                                                 stream.cuda_stream)
+                    assert rc == 0
                 e1.record(stream)
                 torch.cuda.synchronize()
                 if r == 0:
                     imgs[name] = outs[name].cpu().numpy()
                 elif r >= 2:
-                    times[name].append(e0.elapsed_time(e1))
+                    times[name].append(e0.elapsed_time(e1) / nb)
         base = imgs["base"]
         for name in handles:
             t = np.array(times[name])

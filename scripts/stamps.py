@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--wg-waves", type=int, default=4)
     ap.add_argument("--slots", type=int, default=256 * 4 * 6, help="wave slots (CUs*SIMDs*occupancy)")
     ap.add_argument("--save", default="")
+    ap.add_argument("--band", default="", help="ROW0,ROWS: also time that band alone (few waves, "
+                    "each alone on its SIMD) against the same tiles inside the full frame")
     args = ap.parse_args()
     lib = abi.load_library()
     if not hasattr(lib, "vrt_debug_stamps"):
@@ -82,6 +84,26 @@ def main():
         edges = np.linspace(0, span, 11)
         mids = (edges[:-1] + edges[1:]) / 2
         r["resident_waves_over_time"] = [int(((start <= m) & (end > m)).sum()) for m in mids]
+        if args.band:
+            b0, brows = (int(x) for x in args.band.split(","))
+            tile_row = lambda wl: (wl // args.wg_waves // ((w + tw - 1) // tw)) * (th // 8) + \
+                ((wl % args.wg_waves) >> 1)
+            full_rows = tile_row(np.arange(waves))
+            sel = (full_rows >= b0 // 8) & (full_rows < (b0 + brows) // 8)
+            with vrt.Renderer(0) as ren:
+                ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
+                for _ in range(3):
+                    ren.render_rows_async(cam, params, b0, brows, 1, out.data_ptr(), 0, 0,
+                                          stream.cuda_stream)
+                torch.cuda.synchronize()
+            bw = ((w + tw - 1) // tw) * ((brows + th - 1) // th) * args.wg_waves
+            sb = np.zeros((bw, 3), dtype=np.uint64)
+            assert lib.vrt_debug_stamps(sb.ctypes.data, sb.size) == 0
+            db = (sb[:, 1] - sb[:, 0]).astype(np.float64) * 10.0
+            r["band"] = dict(rows=[b0, brows], waves_alone=int(bw),
+                             mean_wave_us_alone=float(db.mean() / 1e3),
+                             mean_wave_us_in_full_frame=float(dur[sel].mean() / 1e3),
+                             span_us_alone=float((sb[:, 1].max() - sb[:, 0].min()) * 10.0 / 1e3))
         report[cfg] = r
         print(cfg, json.dumps(r))
         if args.save:

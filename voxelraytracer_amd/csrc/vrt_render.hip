@@ -264,6 +264,13 @@ __device__ __forceinline__ uint32_t add_if_both(uint32_t x, bool a, bool b) {
   return x;
 }
 
+// m's lane bit ? if_set : if_clear, as one v_cndmask on an SGPR lane mask
+__device__ __forceinline__ float sel_mask(unsigned long long m, float if_set, float if_clear) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+}
+
 // keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
@@ -408,6 +415,14 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
   // skip-box face in travel direction: B = (v + c0) + sgn * (D - margin); c0 = 0 / 1 for d > 0 / < 0
   const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
+  const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
+  // the selects read dir/rcp as VGPRs (the lane mask takes the one scalar operand a VOP3 may
+  // read): materialise shadow rays' uniform sun constants once, not per step
+  f3 dv = dir, rv = rcp;
+  if (SHADOW) {
+    asm volatile("" : "+v"(dv.x), "+v"(dv.y), "+v"(dv.z));
+    asm volatile("" : "+v"(rv.x), "+v"(rv.y), "+v"(rv.z));
+  }
   const bool skip_ok = SHADOW || medium == 0u;
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
@@ -437,6 +452,9 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
     const uint32_t it0 = it;
     uint32_t k = 0;
+    // this lane's step count at its exit: set by the stopping (sampled) step; lanes that run
+    // into the uniform bound leave with k == k_max. Keeps k from being copied to a VGPR per step.
+    uint32_t k_exit = k_max;
     float s_lim = -1.0f;  // no skip window yet: the first step samples
     for (;;) {
       if (k >= k_max) break;  // wave-uniform step bound (scalar branch)
@@ -446,18 +464,26 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       len += tmin;
       const float s = len - len0;
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
+#ifndef VRT_DIAG_SAMPLED
       ties = add_if_both(ties, ey, ez);  // intersectionAxis[3]
+#endif
       // t update for the crossed axis (voxel.glsl:296/381)
-      const bool az = ez, ay = ey & !ez, ax = !ey & !ez;
-      const float pa = az ? pos.z : (ay ? pos.y : pos.x);
-      const float da = az ? dir.z : (ay ? dir.y : dir.x);
-      const float ra = az ? rcp.z : (ay ? rcp.y : rcp.x);
+      // crossed axis: z if ez (index 2, and 3 clamped), else y if ey, else x. Selected with the
+      // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
+      const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
+      const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
+      const float pa = sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x));
+      const float da = sel_mask(mez, dv.z, sel_mask(mey, dv.y, dv.x));
+      const float ra = sel_mask(mez, rv.z, sel_mask(mey, rv.y, rv.x));
       const float ca = pa + s * da;  // == cur on that axis: the same two ops
       const float num = (ca + __builtin_copysignf(1.0f, da)) - pa;
       const float q = div_rn(num, da, ra) - s;
-      t = mk(ax ? q : tp.x, ay ? q : tp.y, az ? q : tp.z);
+      t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
       asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
       if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
+#ifdef VRT_DIAG_SAMPLED  // diagnostic build: the TIE3 counter counts sampled fast-path steps
+        ++ties;
+#endif
         cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
         const bool ex = tp.x == 0.0f;
         const f3 smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f),
@@ -474,20 +500,27 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const uint32_t v_raw = packed & 0xFFu;
         const uint32_t dist = packed >> 8;
         v_ev = inb ? v_raw : kOutside;
+        // exit parameter of the pulled-in box face per axis, ((v + c0) + sgn*fd - pos) * rcp,
+        // as v*rcp + (fd*|rcp| + boff): only has to be conservative (error <~ 4e-4 |rcp| for
+        // N <= 1024, against the 1/256 * |rcp| face margin), so it may contract
         const float fd = float(dist) - kSkipMargin;
-        const float lx = ((float(vi) + c0.x) + step.x * fd - pos.x) * rcp.x;
-        const float ly = ((float(vj) + c0.y) + step.y * fd - pos.y) * rcp.y;
-        const float lz = ((float(vk) + c0.z) + step.z * fd - pos.z) * rcp.z;
+        const float lx = __builtin_fmaf(float(vi), rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
+        const float ly = __builtin_fmaf(float(vj), rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
+        const float lz = __builtin_fmaf(float(vk), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
         const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
         s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
         // stop the inner loop on: outside sample, a byte that is an event, the length. Only a
         // sampled step can stop it: a skipped one reads an empty in-volume texel and has
         // s < s_len, hence len < max_len (see s_len).
         const bool stop = SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium);
-        if (stop | !(len < c.max_len)) break;
+        if (stop | !(len < c.max_len)) {
+          k_exit = k;
+          asm volatile("" : "+v"(k_exit));
+          break;
+        }
       }
     }
-    it = it0 + k;
+    it = it0 + k_exit;
     asm volatile("" : "+v"(v_ev));  // decide here, from the VGPR (no per-step live-out masks)
     const bool inb = v_ev != kOutside;
     const uint32_t v = inb ? v_ev : 0u;  // outside samples read 0 (GetVoxel :151-152)

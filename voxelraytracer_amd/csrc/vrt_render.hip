@@ -138,6 +138,12 @@ struct Counters {
   uint32_t c[VRT_CNT_COUNT];
 };
 
+// Crossed-axis operands of a skip step from a per-lane LDS table (one ds_read_b128) instead of
+// three 3-way register selects.
+#ifndef VRT_LDS_AXIS
+#define VRT_LDS_AXIS 1
+#endif
+
 struct Ctx {
   const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | D << 8 (see pack kernel)
   int32_t n;
@@ -146,6 +152,9 @@ struct Ctx {
   float max_len;
   f3 sun, sun_n, sun_rcp;
   float time, refl_noise, refr_noise;
+#if VRT_LDS_AXIS
+  float4* ax;  // this lane's 3-entry axis table in LDS: {pos, dir, rcp, sign} per axis
+#endif
 };
 
 // a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024)
@@ -262,6 +271,13 @@ __device__ __forceinline__ uint32_t add_if_both(uint32_t x, bool a, bool b) {
   unsigned long long co;
   asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(x), "=s"(co) : "s"(m));
   return x;
+}
+
+// crossed-axis index from the compare masks: mez ? 2 : (mey ? 1 : 0), two v_cndmask
+__device__ __forceinline__ uint32_t axis_index(unsigned long long mey, unsigned long long mez) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, 0, 1, %1\n\tv_cndmask_b32_e64 %0, %0, 2, %2" : "=&v"(r) : "s"(mey), "s"(mez));
+  return r;
 }
 
 // m's lane bit ? if_set : if_clear, as one v_cndmask on an SGPR lane mask
@@ -418,11 +434,17 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
   // the selects read dir/rcp as VGPRs (the lane mask takes the one scalar operand a VOP3 may
   // read): materialise shadow rays' uniform sun constants once, not per step
+#if VRT_LDS_AXIS
+  c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
+  c.ax[1] = make_float4(pos.y, dir.y, rcp.y, step.y);
+  c.ax[2] = make_float4(pos.z, dir.z, rcp.z, step.z);
+#else
   f3 dv = dir, rv = rcp;
   if (SHADOW) {
     asm volatile("" : "+v"(dv.x), "+v"(dv.y), "+v"(dv.z));
     asm volatile("" : "+v"(rv.x), "+v"(rv.y), "+v"(rv.z));
   }
+#endif
   const bool skip_ok = SHADOW || medium == 0u;
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
@@ -472,11 +494,18 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
       const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
       const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
+#if VRT_LDS_AXIS
+      const uint32_t ai = axis_index(mey, mez);
+      const float4 ae = c.ax[ai];
+      const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
+#else
       const float pa = sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x));
       const float da = sel_mask(mez, dv.z, sel_mask(mey, dv.y, dv.x));
       const float ra = sel_mask(mez, rv.z, sel_mask(mey, rv.y, rv.x));
+      const float sa = __builtin_copysignf(1.0f, da);
+#endif
       const float ca = pa + s * da;  // == cur on that axis: the same two ops
-      const float num = (ca + __builtin_copysignf(1.0f, da)) - pa;
+      const float num = (ca + sa) - pa;
       const float q = div_rn(num, da, ra) - s;
       t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
       asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
@@ -829,6 +858,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     c.time = a.time;
     c.refl_noise = a.refl_noise;
     c.refr_noise = a.refr_noise;
+#if VRT_LDS_AXIS
+    __shared__ float4 ax_tab[kWgThreads * 3];
+    c.ax = &ax_tab[threadIdx.x * 3];
+#endif
 
     const int py = a.row0 + li * a.row_step;
     const float ndx = (2.0f * (float(px) + 0.5f)) / float(a.width) - 1.0f;

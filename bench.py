@@ -5,13 +5,20 @@ Workload (BASELINE.json metric "1920x1080 @ 128^3 voxels, 4 bounces"): configs[3
 _REFRACTION scene at 128^3, 1920x1080, reflect+refract 4 bounces (MAX_REFLECTIONS =
 MAX_TRANSPARENCIES = 4), colour-only, noise 0, camera/sun of SURVEY.md §8d. A step = one frame.
 
+Output (default --output rgba8): the reference's stored frame, i.e. the colour written to the RGB8
+ray-trace FBO and the temporal filter into the RGB8 history (main.cpp:363-393), fused into the
+kernel epilogue (4 B history read + 4 B write per pixel); --output f32 writes vrt_render's float
+RGBA frame (16 B per pixel).
+
 Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
 cyclic row bands (rank r owns rows r, r+N, ...); every rank renders its band into HBM and rank 0
-gathers the RGBA bands over RCCL each frame (the only exchange of the path), pipelined so the
-gather of frame k overlaps the render of frame k+1. The total work is the fixed frame: strong
-scaling.
+gathers the bands over RCCL each frame (the only exchange of the path), pipelined so the gather
+of frame k overlaps the render of frame k+1. Default --scaling weak: with N ranks the frame is
+N*H rows of the same view (N-fold vertical sample density), so each rank renders exactly the
+config's W x H pixels; --scaling strong splits the config's frame N ways.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
+                       [--output rgba8|f32] [--alpha A] [--scaling weak|strong]
 """
 import argparse
 import json
@@ -43,6 +50,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the oracle CPU baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--output", default="rgba8", choices=["rgba8", "f32"],
+                    help="rgba8: the reference's stored frame (RGB8 store + temporal filter fused "
+                         "into the kernel); f32: the float RGBA frame of vrt_render")
+    ap.add_argument("--alpha", type=float, default=1.0,
+                    help="temporal filter u_Alpha (slider default 1.0, res/guis/header.xml:20)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: N ranks render an N-fold taller frame (each a config-sized band); "
+                         "strong: the config's frame is split N ways")
     return ap.parse_args()
 
 
@@ -98,10 +113,15 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     scene, n, w, h, R, T, desc = CONFIGS[args.config]
-    cam = vrt.make_camera(w, h)
+    # weak: the framebuffer is H*N rows of the same view (N-fold vertical sample density), so every
+    # rank renders an H-row cyclic band of the config's size; strong: the config's frame is split
+    frame_h = h * world if args.scaling == "weak" else h
+    cam = vrt.make_camera(w, h)   # the config's projection (aspect W/H) at any sample density
+    cam.height = frame_h
     params = vrt.default_params(R, T)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    rgba8 = args.output == "rgba8"
 
     # Volume: built once on rank 0 (main.cpp:218-288), broadcast over RCCL to every GPU, uploaded
     # device-to-device into each rank's context (padded (N+1)^3 layout built on the GPU).
@@ -112,31 +132,39 @@ def main():
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
 
     evs = []
+    timing = {"on": False}
 
-    def render_band(row0, rows, step, out):
+    def launch(row0, rows, step, out, prev, cnt_ptr=0):
+        if rgba8:
+            ren.render_temporal_rows_async(cam, params, args.alpha, row0, rows, step,
+                                           prev.data_ptr(), out.data_ptr(), 0, 0, cnt_ptr, sptr)
+        else:
+            ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sptr)
+
+    def render_band(row0, rows, step, out, prev):
         e = None
         if timing["on"] and world > 1:   # N=1: one event pair brackets the whole timed region
             e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             e[0].record(stream)
-        ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, 0, sptr)
+        launch(row0, rows, step, out, prev)
         if e is not None:
             e[1].record(stream)
             evs.append(e)
 
-    timing = {"on": False}
-    tiler = FrameTiler(w, h, render_band, dev)
+    tiler = FrameTiler(w, frame_h, render_band, dev,
+                       dtype=torch.uint8 if rgba8 else torch.float32)
 
     # One counted band per rank (outside the timed region): rays and algorithmic bytes per frame.
     cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device=dev)
-    ren.render_rows_async(cam, params, tiler.row0, tiler.rows, tiler.step,
-                          tiler.bands[0].data_ptr(), 0, cnt.data_ptr(), sptr)
+    launch(tiler.row0, tiler.rows, tiler.step, tiler.bands[0], tiler.bands[-1], cnt.data_ptr())
     torch.cuda.synchronize(dev)
     own = vrt.counters_dict(cnt.cpu().tolist())
     if world > 1:
         dist.all_reduce(cnt)
     counters = vrt.counters_dict(cnt.cpu().tolist())
+    pixel_bytes = 8 if rgba8 else 16
     rays_per_frame = vrt.total_rays(counters)
-    bytes_per_frame = vrt.algorithmic_bytes(counters)
+    bytes_per_frame = vrt.algorithmic_bytes(counters, pixel_bytes)
 
     for _ in range(args.warmup):
         tiler.frame()
@@ -171,16 +199,17 @@ def main():
         value = rays_per_frame * args.steps / elapsed / 1e6
         # roofline of the dominant kernel: the algorithmic bytes of THIS rank's band per launch
         # over its mean launch time (HIP events on the stream the kernel is launched on)
-        own_bytes = vrt.algorithmic_bytes(own)
+        own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
         achieved = own_bytes / (float(np.mean(kernel_ms)) * 1e-3) / 1e9
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{args.output}.json")
         if os.path.exists(pmc) and world == 1:
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(cam, vox_host, n, params, args.cpu_seconds, args.cpu_threads)
+            cam1 = vrt.make_camera(w, h)
+            cpu = cpu_baseline(cam1, vox_host, n, params, args.cpu_seconds, args.cpu_threads)
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
             "value": round(value, 3),
@@ -190,7 +219,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -200,8 +229,12 @@ def main():
                 "volume_n": n,
                 "width": w,
                 "height": h,
+                "frame": f"{w}x{frame_h}" + (f" ({world}x vertical sample density)"
+                                             if frame_h != h else ""),
                 "max_reflections": R,
                 "max_transparencies": T,
+                "output": ("RGB8 ray-trace store + temporal filter (alpha %g) fused, RGBA8 words"
+                           % args.alpha) if rgba8 else "float RGBA",
                 "parallelism": (f"cyclic row bands x{world} + RCCL gather to rank 0"
                                 if world > 1 else "single GPU, whole frame"),
                 "rays_per_frame": rays_per_frame,
@@ -221,6 +254,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    ren.close()
     if world > 1:
         dist.destroy_process_group()
 

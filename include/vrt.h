@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 1
+#define VRT_ABI_VERSION 2
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -144,6 +144,35 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
                           int32_t row0, int32_t rows, int32_t row_step,
                           float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
                           void* hip_stream);
+
+/* ---- temporal filter + RGB8 framebuffer ------------------------------ */
+/* The reference stores the ray-traced colour into an RGB8 FBO (FrameBuffer.cpp:8), blends it with
+ * the previous filtered frame, color = u_Alpha * new + (1 - u_Alpha) * old (temporal.glsl:18,
+ * main.cpp:363-377), into a second RGB8 FBO and swaps the two (main.cpp:391). These entry points
+ * run that post-pass fused into the render kernel's epilogue. Pixels are RGBA8 words (R in the
+ * low byte, A = 255: the FBOs have no alpha), W x rows, row 0 = bottom. Float -> UNORM8 store:
+ * clamp [0,1], x255, round half to even, NaN -> 0 (GL leaves ties/NaN implementation-defined).
+ * u_Alpha defaults to 1.0 (res/guis/header.xml:20), which makes the output the quantised frame. */
+
+/* Asynchronous band form on DEVICE buffers, same band/counter/stream rules as
+ * vrt_render_rows_async. d_prev_rgba8 holds the band's previous filtered frame and may alias
+ * d_cur_rgba8 (each pixel is read before it is written, by the same work-item). d_raw_rgba8
+ * (optional) receives the quantised ray-trace frame. */
+int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
+                                   float alpha, int32_t row0, int32_t rows, int32_t row_step,
+                                   const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                   uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                   void* hip_stream);
+
+/* Synchronous frame loop of main.cpp:323-393 with the two history FBOs and the ray-trace FBO kept
+ * in the context: render, filter against the last filtered frame, copy the new filtered frame to
+ * the HOST buffer out_rgba8 (W*H*4 bytes), then swap (PostRender). The history starts black and
+ * restarts black when the image size changes. stats may be NULL. */
+int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params, float alpha,
+                     uint8_t* out_rgba8, vrt_stats* stats);
+
+/* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history. */
+int vrt_history_reset(vrt_ctx* ctx);
 
 /* ---- host-side scene harness (mirrors src/main.cpp; no GPU needed) ----------------------- */
 

@@ -65,6 +65,12 @@ def lib():
         L.oracle_terrain_noise.argtypes = [C.c_int, C.c_uint32, C.c_void_p]
         L.oracle_build_scene.restype = C.c_int
         L.oracle_build_scene.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_void_p]
+        L.oracle_temporal.restype = None
+        L.oracle_temporal.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p,
+                                      C.c_uint64]
+        L.oracle_temporal_from_raw.restype = None
+        L.oracle_temporal_from_raw.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
+                                               C.c_uint64]
         _lib = L
     return _lib
 
@@ -142,3 +148,27 @@ def render(cam: Camera, vox: np.ndarray, n: int, params: Params, row0: int = 0, 
     if rc != 0:
         raise ValueError(f"oracle_render rc={rc}")
     return rgba, hits, {name: int(cnt[i]) for i, name in enumerate(COUNTER_NAMES)}
+
+
+def temporal(rgba: np.ndarray, prev_rgba8: np.ndarray, alpha: float):
+    """RGB8 store + temporal blend of a float frame (oracle_temporal): returns (raw, cur) RGBA8
+    arrays shaped like rgba[..., 4]."""
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    prev = np.ascontiguousarray(prev_rgba8, np.uint8)
+    assert rgba.shape == prev.shape and rgba.shape[-1] == 4
+    raw = np.empty(rgba.shape, np.uint8)
+    cur = np.empty(rgba.shape, np.uint8)
+    lib().oracle_temporal(rgba.ctypes.data, prev.ctypes.data, alpha, raw.ctypes.data,
+                          cur.ctypes.data, rgba.size // 4)
+    return raw, cur
+
+
+def temporal_from_raw(raw_rgba8: np.ndarray, prev_rgba8: np.ndarray, alpha: float) -> np.ndarray:
+    """Temporal blend of already-quantised new pixels (oracle_temporal_from_raw)."""
+    raw = np.ascontiguousarray(raw_rgba8, np.uint8)
+    prev = np.ascontiguousarray(prev_rgba8, np.uint8)
+    assert raw.shape == prev.shape and raw.shape[-1] == 4
+    cur = np.empty(raw.shape, np.uint8)
+    lib().oracle_temporal_from_raw(raw.ctypes.data, prev.ctypes.data, alpha, cur.ctypes.data,
+                                   raw.size // 4)
+    return cur

@@ -377,3 +377,28 @@ def render(inv_pv, w, h, vox, n, params, rows=None):
             rgba[i, px] = (color[0], color[1], color[2], 1.0)
             hits[i, px] = (rec[0], rec[1], st["steps"], st["flags"])
     return rgba, hits, tr.cnt
+
+
+# ---- temporal filter + RGB8 store (independent restatement of oracle_temporal) ----
+def unorm8(f):
+    """GL float -> UNORM8 store as pinned in DESIGN.md: clamp [0,1] (NaN -> 0), *255, round half
+    to even."""
+    f = np.asarray(f, np.float32)
+    c = np.fmin(np.fmax(f, np.float32(0.0)), np.float32(1.0))
+    return np.rint(c * np.float32(255.0)).astype(np.uint8)
+
+
+def temporal(rgba, prev_rgba8, alpha):
+    """temporal.glsl:18 on RGB8 textures; returns (raw, cur) RGBA8 (A = 255)."""
+    rgba = np.asarray(rgba, np.float32)
+    prev = np.asarray(prev_rgba8, np.uint8)
+    a = np.float32(alpha)
+    raw = np.empty(rgba.shape, np.uint8)
+    raw[..., :3] = unorm8(rgba[..., :3])
+    raw[..., 3] = 255
+    nw = raw[..., :3].astype(np.float32) / np.float32(255.0)
+    old = prev[..., :3].astype(np.float32) / np.float32(255.0)
+    cur = np.empty(rgba.shape, np.uint8)
+    cur[..., :3] = unorm8(a * nw + (np.float32(1.0) - a) * old)
+    cur[..., 3] = 255
+    return raw, cur

@@ -644,3 +644,50 @@ EXPORT int oracle_build_scene(int scene, int n, uint32_t seed, uint8_t* data) {
   }
   return VRT_OK;
 }
+
+/* ---- Temporal filter and RGB8 framebuffer store ----
+ * The ray-trace FBO and the two temporal FBOs are RGB8 textures (FrameBuffer.cpp:8, internal
+ * format RGB). Writing the shader's vec4 colour stores each of R, G, B as a normalized 8-bit value;
+ * GL's float -> UNORM conversion clamps to [0,1], scales by 255 and rounds to nearest. The tie
+ * rule (x.5) and NaN handling are implementation-defined in GL; this restatement pins ties to
+ * even (rintf) and NaN to 0 (fmaxf drops it). Sampling an RGB8 texel returns b / 255.
+ * temporal.glsl:18: color = u_Alpha * newColor + (1 - u_Alpha) * averageColor, stored to the
+ * current RGB8 FBO (main.cpp:363-377), then current and last swap (main.cpp:391). Pixels are
+ * RGBA8 words here, R in the low byte, A = 255 (the FBOs have no alpha channel).
+ */
+static inline uint8_t unorm8(float f) {
+  const float c = fminf(fmaxf(f, 0.0f), 1.0f);
+  return (uint8_t)rintf(c * 255.0f);
+}
+static inline float unorm8_read(uint8_t b) { return (float)b / 255.0f; }
+
+EXPORT void oracle_temporal(const float* rgba, const uint8_t* prev_rgba8, float alpha,
+                            uint8_t* raw_rgba8, uint8_t* cur_rgba8, uint64_t npix) {
+  const float one_minus = 1.0f - alpha;
+  for (uint64_t i = 0; i < npix; i++) {
+    for (int ch = 0; ch < 3; ch++) {
+      const uint8_t raw = unorm8(rgba[i * 4 + ch]);
+      if (raw_rgba8) raw_rgba8[i * 4 + ch] = raw;
+      const float nw = unorm8_read(raw);
+      const float old = unorm8_read(prev_rgba8[i * 4 + ch]);
+      cur_rgba8[i * 4 + ch] = unorm8(alpha * nw + one_minus * old);
+    }
+    if (raw_rgba8) raw_rgba8[i * 4 + 3] = 255;
+    cur_rgba8[i * 4 + 3] = 255;
+  }
+}
+
+/* the same blend from already-quantised new pixels (raw RGBA8), for checking the device's
+ * epilogue bit-exactly on its own raw output */
+EXPORT void oracle_temporal_from_raw(const uint8_t* raw_rgba8, const uint8_t* prev_rgba8, float alpha,
+                                     uint8_t* cur_rgba8, uint64_t npix) {
+  const float one_minus = 1.0f - alpha;
+  for (uint64_t i = 0; i < npix; i++) {
+    for (int ch = 0; ch < 3; ch++) {
+      const float nw = unorm8_read(raw_rgba8[i * 4 + ch]);
+      const float old = unorm8_read(prev_rgba8[i * 4 + ch]);
+      cur_rgba8[i * 4 + ch] = unorm8(alpha * nw + one_minus * old);
+    }
+    cur_rgba8[i * 4 + 3] = 255;
+  }
+}

@@ -24,7 +24,7 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, n, w, h, frames, q):
+def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -39,16 +39,21 @@ def worker(rank, world, port, n, w, h, frames, q):
     broadcast_volume(vox)
     vox_np = vox.numpy()
     cam = vrt.make_camera(w, h)
-    params = [vrt.default_params(1, 2, time=float(t + 1)) for t in range(frames)]
+    params = [vrt.default_params(1, 2, time=float(t + 1), ray_noise=0.05) for t in range(frames)]
     state = {"i": 0}
 
-    def render_band(row0, rows, step, out):
+    def render_band(row0, rows, step, out, prev):
         rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"]], row0=row0, rows=rows,
                                    row_step=step, threads=1)
-        out.copy_(torch.from_numpy(rgba))
+        if mode == "rgba8":   # the fused temporal filter + RGB8 store, band-local history
+            _, cur = oracle.temporal(rgba, prev.numpy().copy(), alpha)
+            out.copy_(torch.from_numpy(cur))
+        else:
+            out.copy_(torch.from_numpy(rgba))
         state["i"] += 1
 
-    tiler = FrameTiler(w, h, render_band, torch.device("cpu"))
+    tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
+                       dtype=torch.uint8 if mode == "rgba8" else torch.float32)
     got = []
     for _ in range(frames):
         f = tiler.frame()
@@ -85,7 +90,8 @@ def test_tiled_frames_match_single_process(built, world):
     cam = vrt.make_camera(w, h)
     assert len(got) == frames
     for t in range(frames):
-        ref, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1)))
+        ref, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                  ray_noise=0.05))
         assert np.array_equal(got[t].view(np.uint32), ref.view(np.uint32)), t
 
 
@@ -98,3 +104,32 @@ def test_band_spec_and_assembly():
     frame = torch.arange(12 * 2 * 1, dtype=torch.float32).reshape(12, 2, 1)
     bands = torch.stack([frame[r::3] for r in range(3)])
     assert torch.equal(assemble_cyclic(bands), frame)
+
+
+def test_tiled_temporal_rgba8_frames(built):
+    """RGBA8 bands with the temporal filter: each rank's history is its own band of the previous
+    frame, so the assembled sequence equals the single-process filtered sequence bit for bit."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h, frames, world, alpha = 16, 20, 12, 4, 2, 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, _ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    hist = np.zeros((h, w, 4), np.uint8)
+    assert len(got) == frames
+    for t in range(frames):
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert np.array_equal(got[t], hist), t

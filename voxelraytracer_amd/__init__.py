@@ -88,9 +88,12 @@ def counters_dict(values) -> dict:
     return {name: int(values[i]) for i, name in enumerate(COUNTER_NAMES)}
 
 
-def algorithmic_bytes(c: dict) -> int:
-    """1 B per DDA step (both marches) + 2 B per refraction probe + 16 B per RGBA pixel."""
-    return c["dda_steps"] + c["shadow_steps"] + 2 * c["refraction_probes"] + 16 * c["pixels"]
+def algorithmic_bytes(c: dict, pixel_bytes: int = 16) -> int:
+    """1 B per DDA step (both marches) + 2 B per refraction probe + the per-pixel output bytes:
+    16 for the float RGBA frame, 8 for the fused temporal RGB8 path (4 B history
+    read + 4 B filtered write)."""
+    return (c["dda_steps"] + c["shadow_steps"] + 2 * c["refraction_probes"]
+            + pixel_bytes * c["pixels"])
 
 
 def total_rays(c: dict) -> int:
@@ -177,3 +180,31 @@ class Renderer:
                                             stream or None),
             "vrt_render_rows_async",
         )
+
+    def render_temporal_rows_async(self, cam: Camera, params: Params, alpha: float, row0: int,
+                                   rows: int, row_step: int, d_prev: int, d_cur: int,
+                                   d_raw: int = 0, d_hit: int = 0, d_counters: int = 0,
+                                   stream: int = 0):
+        """Band render with the fused temporal filter + RGB8 store (vrt_render_temporal_rows_async)
+        into device RGBA8 buffers (e.g. torch uint8 [rows, W, 4] tensors' data_ptr())."""
+        self._check(
+            self._lib.vrt_render_temporal_rows_async(
+                self._h, C.byref(cam), C.byref(params), alpha, row0, rows, row_step, d_prev, d_cur,
+                d_raw or None, d_hit or None, d_counters or None, stream or None),
+            "vrt_render_temporal_rows_async",
+        )
+
+    def render_frame(self, cam: Camera, params: Params, alpha: float = 1.0):
+        """main.cpp's frame loop with the history in the context (vrt_render_frame): returns the
+        new filtered frame as rgba8[H,W,4] uint8 and the stats."""
+        out = np.empty((cam.height, cam.width, 4), dtype=np.uint8)
+        st = abi.Stats()
+        self._check(self._lib.vrt_render_frame(self._h, C.byref(cam), C.byref(params), alpha,
+                                               out.ctypes.data, C.byref(st)), "vrt_render_frame")
+        stats = counters_dict(st.counters)
+        stats["kernel_ms"] = float(st.kernel_ms)
+        return out, stats
+
+    def history_reset(self):
+        """Key F (main.cpp:417-421): the last ray-traced frame becomes the temporal history."""
+        self._check(self._lib.vrt_history_reset(self._h), "vrt_history_reset")

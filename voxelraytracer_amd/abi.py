@@ -117,6 +117,16 @@ SIGNATURES = {
             C.c_void_p,
         ],
     ),
+    "vrt_render_temporal_rows_async": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_int32, C.c_int32,
+         C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    ),
+    "vrt_render_frame": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p, C.POINTER(Stats)],
+    ),
+    "vrt_history_reset": (C.c_int, [C.c_void_p]),
     "vrt_terrain_noise": (C.c_int, [C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_build_scene": (C.c_int, [C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_camera_make": (

@@ -34,6 +34,11 @@ struct KArgs {
   int32_t n, width, height;
   int32_t row0, rows, row_step;
   int32_t max_refl, max_transp;
+  // temporal epilogue (cur != nullptr): RGB8 store + temporal.glsl blend instead of float RGBA
+  float alpha;
+  const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
+  uint32_t* cur;         // filtered frame written here
+  uint32_t* raw;         // optional: the quantised ray-trace frame (the reference's rayTrace FBO)
 };
 
 // ------------------------------------------------------------------ GLSL vector semantics --
@@ -421,7 +426,7 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 constexpr uint32_t kDistCap = 32;
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
-template <bool SHADOW>
+template <bool SHADOW, bool STATS>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
@@ -487,7 +492,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float s = len - len0;
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
 #ifndef VRT_DIAG_SAMPLED
-      ties = add_if_both(ties, ey, ez);  // intersectionAxis[3]
+      if (STATS) ties = add_if_both(ties, ey, ez);  // intersectionAxis[3] (counter/flag only)
 #endif
       // t update for the crossed axis (voxel.glsl:296/381)
       // crossed axis: z if ez (index 2, and 3 clamped), else y if ey, else x. Selected with the
@@ -576,23 +581,25 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
 }
 
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)
+template <bool STATS>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    return skip_walk<false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
 
 // RayMarchShadow walk: the direction is normalize(u_SunDir) for every ray (uniform constants)
+template <bool STATS>
 __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len0, WalkState& w) {
   int axis;
   int32_t vidx;
   uint32_t v;
   if (__builtin_expect(fast_path_ok(c.sun_n), 1))
-    return skip_walk<true>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    return skip_walk<true, STATS>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
 
@@ -656,6 +663,7 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 }
 
 // RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
+template <bool STATS>
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
 #ifdef VRT_ABLATE_SHADOW  // timing-only ablation build (scripts/ab.py); wrong images
@@ -663,12 +671,13 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
 #endif
   WalkState w;
   walk_init(w, ray);
-  const int r = walk_shadow(c, ray.pos, ray.len, w);
+  const int r = walk_shadow<STATS>(c, ray.pos, ray.len, w);
   walk_account(w, r, VRT_CNT_SHADOW_STEPS, k, steps, flags);
   return r == WALK_EVENT;
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
+template <bool STATS>
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -686,7 +695,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk_ray(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    r = walk_ray<STATS>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -729,9 +738,10 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
 }
 
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
+template <bool STATS>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
-  const Hit h = march(c, ray, k, steps, flags);
+  const Hit h = march<STATS>(c, ray, k, steps, flags);
   if (h.found) {
     Ray sr;  // GetShadowRay (:191-201)
     sr.voxel = h.voxel;
@@ -742,7 +752,7 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
     sr.rdepth = 0;
     sr.tdepth = 0;
     k.c[VRT_CNT_SHADOW_RAYS]++;
-    const bool in_shadow = march_shadow(c, sr, k, steps, flags);
+    const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
     const uint32_t m = mat_id(h.voxel);
     float brightness;
     if (in_shadow) {
@@ -773,6 +783,29 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 }
 
 constexpr int kMaxStack = 17;
+
+// ---- RGB8 framebuffer store + temporal filter (oracle/vrt_oracle.c oracle_temporal) ----------
+// GL float -> UNORM8 store into the RGB8 FBO attachments (FrameBuffer.cpp:8): clamp to [0,1]
+// (NaN -> 0), scale by 255, round half to even (pinned in DESIGN.md); a texel reads back b / 255.
+__device__ __forceinline__ uint32_t unorm8(float f) {
+  const float c = __builtin_fminf(__builtin_fmaxf(f, 0.0f), 1.0f);
+  return uint32_t(__builtin_rintf(c * 255.0f));
+}
+__device__ __forceinline__ float unorm8_read(uint32_t b) { return float(b) / 255.0f; }
+__device__ __forceinline__ uint32_t pack_rgb8(float r, float g, float b) {
+  return unorm8(r) | (unorm8(g) << 8) | (unorm8(b) << 16) | 0xFF000000u;
+}
+// temporal.glsl:18  color = u_Alpha * newColor + (1 - u_Alpha) * averageColor, on RGB8 texels
+__device__ __forceinline__ uint32_t temporal_blend(uint32_t nw, uint32_t old, float alpha) {
+  const float om = 1.0f - alpha;
+  uint32_t r = 0xFF000000u;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float v = alpha * unorm8_read((nw >> (8 * ch)) & 0xFFu) + om * unorm8_read((old >> (8 * ch)) & 0xFFu);
+    r |= unorm8(v) << (8 * ch);
+  }
+  return r;
+}
 
 // Lane id as a fresh (volatile) value each call, so the compiler cannot keep one copy alive
 // across the whole trace.
@@ -825,6 +858,10 @@ constexpr int kCntReplicas = 256;
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
 // The primary ray (stack[0] of the reference) stays in registers; the scratch stack only ever
 // holds secondary rays, so pixels that spawn none never touch it.
+// STATS: this instance writes hit records and/or counters. Without it the per-lane counters,
+// step/flag/tie tracking are dead code (~20 VGPRs and a VALU per DDA step freed); the rendering
+// arithmetic is the same source in both instances.
+template <bool STATS>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -891,7 +928,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     uint32_t steps = 0, flags = 0;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
-    const Hit h0 = trace_with_shadow(c, ray, color, k, steps, flags);
+    const Hit h0 = trace_with_shadow<STATS>(c, ray, color, k, steps, flags);
     const int32_t hit_vidx = h0.found ? h0.vidx : -1;
     const float hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
@@ -915,13 +952,19 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
         if (sp == 0) break;
         ray = stack[--sp];
         k.c[VRT_CNT_SECONDARY_RAYS]++;
-        h = trace_with_shadow(c, ray, color, k, steps, flags);
+        h = trace_with_shadow<STATS>(c, ray, color, k, steps, flags);
       }
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.width) + size_t(pixel_x(wave, l2));
-    out[o] = make_float4(color.x, color.y, color.z, 1.0f);
-    if (hits) {
+    if (a.cur) {  // fused reference post-pass: RGB8 ray-trace store, temporal blend, RGB8 store
+      const uint32_t rw = pack_rgb8(color.x, color.y, color.z);
+      if (a.raw) a.raw[o] = rw;
+      a.cur[o] = temporal_blend(rw, a.prev[o], a.alpha);
+    } else {
+      out[o] = make_float4(color.x, color.y, color.z, 1.0f);
+    }
+    if (STATS && hits) {
       vrt_hit hr;
       hr.voxel_index = hit_vidx;
       hr.ray_length = hit_len;
@@ -941,7 +984,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     }
   }
 #endif
-  if (counters) {
+  if (STATS && counters) {
     unsigned long long* slot =
         counters + size_t((blockIdx.y * gridDim.x + blockIdx.x) % kCntReplicas) * VRT_CNT_COUNT;
 #pragma unroll
@@ -1028,6 +1071,11 @@ struct vrt_ctx {
   unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of vrt_render
   unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
   size_t out_pixels = 0;
+  // vrt_render_frame's ping-pong history (main.cpp:140-142, 363-393): RGBA8 words
+  uint32_t* d_hist[2] = {nullptr, nullptr};
+  uint32_t* d_raw = nullptr;
+  int hist_last = 0;  // index of lastFrameBuffer in d_hist
+  int32_t hist_w = 0, hist_h = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
 };
@@ -1088,14 +1136,27 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.row_step = row_step;
   a.max_refl = p->max_reflections;
   a.max_transp = p->max_transparencies;
+  a.alpha = 1.0f;
+  a.prev = nullptr;
+  a.cur = nullptr;
+  a.raw = nullptr;
   return a;
 }
 
 // Render kernel, then (when counting) fold the replicas into `cnt` (accumulate) and re-zero them.
+void free_history(vrt_ctx* ctx) {
+  for (uint32_t** b : {&ctx->d_hist[0], &ctx->d_hist[1], &ctx->d_raw}) {
+    if (*b) (void)hipFree(*b);
+    *b = nullptr;
+  }
+  ctx->hist_w = ctx->hist_h = 0;
+}
+
 void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
   dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
-  hipLaunchKernelGGL(vrt::render_kernel, grid, dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
+  hipLaunchKernelGGL((hit || cnt) ? vrt::render_kernel<true> : vrt::render_kernel<false>, grid,
+                     dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
                      cnt ? ctx->d_cnt_rep : nullptr);
   if (cnt) hipLaunchKernelGGL(vrt::reduce_counters_kernel, dim3(1), dim3(64), 0, s, ctx->d_cnt_rep, cnt);
 }
@@ -1182,6 +1243,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (c->d_hit) (void)hipFree(c->d_hit);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
   if (c->d_cnt_rep) (void)hipFree(c->d_cnt_rep);
+  free_history(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1246,6 +1308,86 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
   launch(ctx, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
          reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
   VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
+                                   float alpha, int32_t row0, int32_t rows, int32_t row_step,
+                                   const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                   uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                   void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
+  if (rows < 0 || row_step < 1 || row0 < 0 ||
+      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
+    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
+  if (rows == 0) return VRT_OK;
+  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
+  a.alpha = alpha;
+  a.prev = d_prev_rgba8;
+  a.cur = d_cur_rgba8;
+  a.raw = d_raw_rgba8;
+  launch(ctx, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
+         static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,
+                     uint8_t* out_rgba8, vrt_stats* stats) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t pixels = size_t(cam->width) * cam->height;
+  if (cam->width != ctx->hist_w || cam->height != ctx->hist_h) {  // (re)create: black history
+    free_history(ctx);
+    for (uint32_t** b : {&ctx->d_hist[0], &ctx->d_hist[1], &ctx->d_raw}) {
+      if (hipMalloc(b, pixels * 4) != hipSuccess) {
+        free_history(ctx);
+        return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
+      }
+      VRT_HIP(ctx, hipMemset(*b, 0, pixels * 4));
+    }
+    ctx->hist_w = cam->width;
+    ctx->hist_h = cam->height;
+    ctx->hist_last = 0;
+  }
+  if (stats)
+    VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
+  uint32_t* last = ctx->d_hist[ctx->hist_last];
+  uint32_t* cur = ctx->d_hist[1 - ctx->hist_last];
+  vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
+  a.alpha = alpha;
+  a.prev = last;
+  a.cur = cur;
+  a.raw = ctx->d_raw;
+  VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
+  launch(ctx, a, nullptr, nullptr, stats ? ctx->d_cnt : nullptr, nullptr);
+  VRT_HIP(ctx, hipGetLastError());
+  VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
+  VRT_HIP(ctx, hipMemcpy(out_rgba8, cur, pixels * 4, hipMemcpyDeviceToHost));
+  ctx->hist_last = 1 - ctx->hist_last;  // PostRender: std::swap(last, current) (main.cpp:391)
+  if (stats) {
+    unsigned long long h[VRT_CNT_COUNT];
+    VRT_HIP(ctx, hipMemcpy(h, ctx->d_cnt, sizeof(h), hipMemcpyDeviceToHost));
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) stats->counters[q] = h[q];
+    float ms = 0.0f;
+    VRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    stats->kernel_ms = ms;
+  }
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_history_reset(vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer)
+  std::swap(ctx->d_hist[ctx->hist_last], ctx->d_raw);
+  ctx->err.clear();
   return VRT_OK;
 }
 

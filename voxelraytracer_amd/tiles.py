@@ -8,7 +8,10 @@ xGMI with the "nccl" backend; gloo on CPU for tests), after which rank 0 re-inte
 into the frame. The volume is replicated once per GPU (broadcast_volume).
 
 FrameTiler double-buffers the band so that, over a sequence of frames, the gather of frame k
-overlaps the render of frame k+1 on the compute stream.
+overlaps the render of frame k+1 on the compute stream. Bands are RGBA8 words when the renderer
+runs the fused temporal filter + RGB8 store (the reference's stored frame format, main.cpp:363-393):
+4 B per pixel on the wire instead of 16. The temporal history is band-local (each rank blends its
+own rows), so it adds no exchange; the previous frame's band buffer IS the history.
 """
 from __future__ import annotations
 
@@ -45,12 +48,15 @@ def broadcast_volume(vox: torch.Tensor, src: int = 0, group=None) -> torch.Tenso
 class FrameTiler:
     """Renders a sequence of frames across `world` ranks.
 
-    render_band(row0, rows, row_step, out) must enqueue the band render into `out` ([rows, W, 4]
-    float32 on `device`) on the current stream (the HIP kernel through the C-ABI, or the oracle
-    in CPU tests). frame() renders the next frame and issues its gather asynchronously; on rank 0
-    it returns the PREVIOUS frame, assembled (None on the first call and on other ranks), so the
-    gather of frame k overlaps the render of frame k+1 on every rank. finish() drains the pipeline
-    and returns the last frame on rank 0.
+    render_band(row0, rows, row_step, out, prev) must enqueue the band render into `out`
+    ([rows, W, channels] of `dtype` on `device`) on the current stream (the HIP kernel through the
+    C-ABI, or the oracle in CPU tests); `prev` holds this rank's band of the previous frame (the
+    temporal history; zeros before the first frame; it is `out` itself with one buffer).
+    frame() renders the next frame and issues its gather asynchronously; on rank 0 it returns the
+    PREVIOUS frame, assembled (None on the first call and on other ranks), so the gather of frame
+    k overlaps the render of frame k+1 on every rank. Rank 0 re-interleaves on a side stream
+    (returned frames are ordered on `self.assembly_stream`). finish() drains the pipeline and
+    returns the last frame on rank 0.
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
@@ -63,7 +69,10 @@ class FrameTiler:
         self.render_band = render_band
         shape = (self.rows, width, channels)
         nbuf = 2 if self.world > 1 else 1
-        self.bands = [torch.empty(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.assembly_stream = None
+        if self.rank == 0 and self.world > 1 and torch.device(device).type == "cuda":
+            self.assembly_stream = torch.cuda.Stream(device=device)
         self.gathered = None
         self.frame_buf = None
         if self.rank == 0 and self.world > 1:
@@ -71,6 +80,7 @@ class FrameTiler:
                              for _ in range(nbuf)]
             self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
         self.pending = [None] * nbuf   # gather that still reads bands[b]
+        self.assembled = [None] * nbuf  # rank 0: assembly that still reads gathered[b]
         self.prev = None               # rank 0: buffer index of the frame awaiting assembly
         self.k = 0
 
@@ -79,21 +89,32 @@ class FrameTiler:
             return None
         b = self.prev
         self.prev = None
+        if self.assembly_stream is not None:
+            with torch.cuda.stream(self.assembly_stream):
+                self.pending[b].wait()          # the side stream waits for the gather
+                self.pending[b] = None
+                out = assemble_cyclic(self.gathered[b], self.frame_buf)
+            self.assembled[b] = self.assembly_stream.record_event()
+            return out
         self.pending[b].wait()
         self.pending[b] = None
         return assemble_cyclic(self.gathered[b], self.frame_buf)
 
     def frame(self) -> Optional[torch.Tensor]:
         if self.world == 1:
-            self.render_band(self.row0, self.rows, self.step, self.bands[0])
+            self.render_band(self.row0, self.rows, self.step, self.bands[0], self.bands[0])
             return self.bands[0]
         b = self.k % len(self.bands)
+        prev = self.bands[(self.k - 1) % len(self.bands)]
         self.k += 1
         if self.pending[b] is not None:   # the gather that last read this buffer must be done
             self.pending[b].wait()
             self.pending[b] = None
         band = self.bands[b]
-        self.render_band(self.row0, self.rows, self.step, band)
+        self.render_band(self.row0, self.rows, self.step, band, prev)
+        if self.assembled[b] is not None:   # rank 0: the assembly that read gathered[b]
+            torch.cuda.current_stream().wait_event(self.assembled[b])
+            self.assembled[b] = None
         glist = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
         work = dist.gather(band, glist, dst=0, group=self.group, async_op=True)
         out = self._assemble_prev() if self.rank == 0 else None

@@ -44,8 +44,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the oracle CPU baseline sample (0 disables)")

@@ -16,7 +16,7 @@ if [ -z "$SKIP_TESTS" ]; then
   step pytest_gpu 600 python -m pytest tests -m gpu -x -q
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
-step bench 300 python bench.py --config "$CFG" --steps 20 --warmup 3
+step bench 300 python bench.py --config "$CFG"
 export TMPDIR=/tmp
 step prof_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 3 --cpu-seconds 0
 [ -n "$NO_PMC" ] && exit 0

@@ -55,6 +55,9 @@ def parse():
                          "into the kernel); f32: the float RGBA frame of vrt_render")
     ap.add_argument("--alpha", type=float, default=1.0,
                     help="temporal filter u_Alpha (slider default 1.0, res/guis/header.xml:20)")
+    ap.add_argument("--shading", default="color", choices=["color", "textured"],
+                    help="color: _COLOR_ONLY materials (SURVEY §8d configs); textured: the "
+                         "reference's default build, atlas shading (synthetic 256/128 atlas)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: N ranks render an N-fold taller frame (each a config-sized band); "
                          "strong: the config's frame is split N ways")
@@ -119,6 +122,8 @@ def main():
     cam = vrt.make_camera(w, h)   # the config's projection (aspect W/H) at any sample density
     cam.height = frame_h
     params = vrt.default_params(R, T)
+    if args.shading == "textured":
+        params = vrt.textured_params(params, vrt.make_atlas())
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     rgba8 = args.output == "rgba8"
@@ -233,6 +238,8 @@ def main():
                                              if frame_h != h else ""),
                 "max_reflections": R,
                 "max_transparencies": T,
+                "shading": ("textured (synthetic 256x256 atlas, 128 px tiles)"
+                            if args.shading == "textured" else "colour-only"),
                 "output": ("RGB8 ray-trace store + temporal filter (alpha %g) fused, RGBA8 words"
                            % args.alpha) if rgba8 else "float RGBA",
                 "parallelism": (f"cyclic row bands x{world} + RCCL gather to rank 0"

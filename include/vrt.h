@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 2
+#define VRT_ABI_VERSION 3
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -60,9 +60,9 @@ typedef struct {
   float max_ray_length;       /* u_MaxRayLength, default 100 (voxel.glsl:17) */
   int32_t max_reflections;    /* MAX_REFLECTIONS   (voxel.glsl:4), 0..8 */
   int32_t max_transparencies; /* MAX_TRANSPARENCIES (voxel.glsl:5), 0..8 */
-  int32_t color_only;         /* _COLOR_ONLY (voxel.glsl:6): must be 1 in ABI v1 */
+  int32_t color_only;         /* _COLOR_ONLY (voxel.glsl:6): 1 colour-only, 0 textured */
   int32_t reserved0;
-  const uint8_t* atlas_rgba;  /* textured mode (not in ABI v1): u_TextureUnit atlas */
+  const uint8_t* atlas_rgba;  /* textured mode: u_TextureUnit atlas (see vrt_upload_atlas) */
   int32_t atlas_size;         /* u_AtlasSize */
   int32_t atlas_texture_size; /* u_AtlasTextureSize */
 } vrt_params;
@@ -144,6 +144,18 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
                           int32_t row0, int32_t rows, int32_t row_step,
                           float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
                           void* hip_stream);
+
+/* ---- textured mode (voxel.glsl without _COLOR_ONLY) --------------------- */
+/* With vrt_params.color_only = 0 the kernel shades with the textured material table
+ * (voxel.glsl:51-68) and GetColor reads the atlas (:174-182) at GetTextureCoordinate (:167-172)
+ * of the hit's face plane, with atlas_size = u_AtlasSize and atlas_texture_size =
+ * u_AtlasTextureSize (main.cpp:336-337). Atlas: atlas_size^2 RGBA8 texels, row 0 = bottom (GL
+ * t = 0), NEAREST + REPEAT; material slot (texX, texY) covers columns [texX*ts, (texX+1)*ts) and
+ * rows [size-(texY+1)*ts, size-texY*ts). atlas_size must be a power of two. The context keeps
+ * the atlas: it is uploaded by vrt_upload_atlas, or by any render call whose
+ * vrt_params.atlas_rgba is non-NULL and differs (pointer or size) from the last upload
+ * (a synchronous copy). Replaces the Atlas texture of main.cpp:187-193. */
+int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size);
 
 /* ---- temporal filter + RGB8 framebuffer ------------------------------ */
 /* The reference stores the ray-traced colour into an RGB8 FBO (FrameBuffer.cpp:8), blends it with

@@ -65,6 +65,9 @@ def lib():
         L.oracle_terrain_noise.argtypes = [C.c_int, C.c_uint32, C.c_void_p]
         L.oracle_build_scene.restype = C.c_int
         L.oracle_build_scene.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_void_p]
+        L.oracle_get_color.restype = None
+        L.oracle_get_color.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint8,
+                                       C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_temporal.restype = None
         L.oracle_temporal.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p,
                                       C.c_uint64]
@@ -172,3 +175,14 @@ def temporal_from_raw(raw_rgba8: np.ndarray, prev_rgba8: np.ndarray, alpha: floa
     lib().oracle_temporal_from_raw(raw.ctypes.data, prev.ctypes.data, alpha, cur.ctypes.data,
                                    raw.size // 4)
     return cur
+
+
+def get_color(atlas, atlas_size: int, tex_size: int, voxel: int, point, index: int,
+              textured: bool = True) -> np.ndarray:
+    """GetColor of one hit (oracle_get_color)."""
+    a = np.ascontiguousarray(atlas, np.uint8)
+    pt = np.asarray(point, np.float32)
+    out = np.zeros(4, np.float32)
+    lib().oracle_get_color(a.ctypes.data, atlas_size, tex_size, int(textured), voxel,
+                           pt.ctypes.data, index, out.ctypes.data)
+    return out

@@ -26,6 +26,13 @@ MATERIALS = [
     (F(1.5), True, True, F(1.0), F(1.0), F(1.0), (F(0), F(0), F(0), F(0))),
     (F(1.0), False, False, F(0.4), F(0.2), F(10.0), (F(0.05), F(0.5), F(0.1), F(1.0))),
 ]
+# voxel.glsl:51-68 (textured): refractivity, transparent, reflective, kd, ks, exp, (texX, texY)
+MATERIALS_TEX = [
+    (F(1.0), True, False, F(0.0), F(0.0), F(0.0), (0, 0)),
+    (F(1.0), False, False, F(0.4), F(0.6), F(60.0), (0, 0)),
+    (F(1.5), True, True, F(1.0), F(1.0), F(0.3), (0, 1)),
+    (F(1.0), False, False, F(0.4), F(0.4), F(20.0), (1, 1)),
+]
 AMBIENT = F(0.3)
 AXIS = ((0, 2, 1), (1, 0, 2), (2, 0, 1))   # intersectionAxis (:93)
 
@@ -125,8 +132,33 @@ class Tracer:
         self.max_len = F(params["max_ray_length"])
         self.R = params["max_reflections"]
         self.T = params["max_transparencies"]
+        self.textured = not params.get("color_only", 1)
+        if self.textured:
+            self.atlas = np.asarray(params["atlas"], np.uint8)   # [S, S, 4], row 0 = bottom
+            self.atlas_size = int(params["atlas_size"])
+            self.atlas_tex = int(params["atlas_texture_size"])
+        self.mats = MATERIALS_TEX if self.textured else MATERIALS
         self.cnt = dict(pixels=0, primary_rays=0, secondary_rays=0, shadow_rays=0, dda_steps=0,
                         shadow_steps=0, refraction_probes=0, tie3=0, step_cap=0)
+
+    def color(self, hit):
+        """GetColor (:174-182): the material colour, or the atlas texel at GetTextureCoordinate
+        (:167-172) of the hit's face plane (NEAREST, REPEAT, b / 255)."""
+        if not self.textured:
+            return MATERIALS[min(hit["voxel"], 3)][6]
+        tx, ty = MATERIALS_TEX[min(hit["voxel"], 3)][6]
+        ax = AXIS[hit["index"]]
+        px, py = hit["point"][ax[1]], hit["point"][ax[2]]
+        fx = px - F(np.floor(px))
+        fy = py - F(np.floor(py))
+        ts, size = F(self.atlas_tex), F(self.atlas_size)
+        u = ((fx + F(tx)) * ts) / size
+        v = ONE - ((((ONE - fy) + F(ty)) * ts) / size)
+        S = self.atlas_size
+        su, sv = u * size, v * size
+        i = int(np.floor(su)) % S if su == su else 0
+        j = int(np.floor(sv)) % S if sv == sv else 0
+        return tuple(F(b) / F(255.0) for b in self.atlas[j, i])
 
     # RandomizeDirection :132-140
     def randomize(self, d, p, randomness, seed):
@@ -171,7 +203,7 @@ class Tracer:
         outv, _ = self.get_voxel(v_add(hit["point"], v_scale(hit["normal"], HALF)))
         inv, _ = self.get_voxel(v_sub(hit["point"], v_scale(hit["normal"], HALF)))
         self.cnt["refraction_probes"] += 1
-        eta = MATERIALS[min(outv, 3)][0] / MATERIALS[min(inv, 3)][0]
+        eta = self.mats[min(outv, 3)][0] / self.mats[min(inv, 3)][0]
         d = v_refract(v_normalize(ray["dir"]), hit["normal"], eta)
         if d[0] == Z and d[1] == Z and d[2] == Z:
             out = self.reflection_ray(ray, hit)
@@ -180,7 +212,7 @@ class Tracer:
         else:
             e = ray["energy"]
             if ray["voxel"] == 0:
-                e = e * (ONE - MATERIALS[min(hit["voxel"], 3)][6][3])
+                e = e * (ONE - self.color(hit)[3])
             out = dict(pos=hit["point"], dir=self.randomize(d, hit["point"], self.refr_noise,
                                                             self.time),
                        energy=e, voxel=hit["voxel"])
@@ -231,7 +263,7 @@ class Tracer:
             self.cnt["shadow_steps"] += 1
             with np.errstate(all="ignore"):
                 t, length, cur, voxel, _, index, step = self._step(ray, t, length, stats)
-                if voxel != 0 and not MATERIALS[min(voxel, 3)][1]:
+                if voxel != 0 and not self.mats[min(voxel, 3)][1]:
                     return True
                 t = self._t_update(ray, t, cur, step, index, length)
         return False
@@ -262,7 +294,7 @@ class Tracer:
             normal = [Z, Z, Z]
             normal[a] = -g_sign(ray["dir"][a])
             hit = dict(found=True, voxel=voxel, point=cur, len=length, normal=tuple(normal),
-                       vidx=vidx)
+                       vidx=vidx, index=index)
             if voxel != 0 and voxel != ray_voxel:
                 return hit
             if ray_voxel != 0 and voxel == 0:
@@ -300,7 +332,7 @@ class Tracer:
             sr = self.shadow_ray(ray, hit)
             self.cnt["shadow_rays"] += 1
             in_shadow = self.march_shadow(sr, stats)
-            mat = MATERIALS[min(hit["voxel"], 3)]
+            mat = self.mats[min(hit["voxel"], 3)]
             if in_shadow:
                 b = AMBIENT
             else:
@@ -308,7 +340,7 @@ class Tracer:
                 spec = mat[4] * g_pow(g_max(v_dot(v_reflect(sr["dir"], hit["normal"]), ray["dir"]),
                                             Z), mat[5])
                 b = AMBIENT + diffuse + spec
-            rgba = mat[6]
+            rgba = self.color(hit)
             e = ray["energy"]
             color = tuple(g_mix(color[i], rgba[i] * rgba[3] * b, e) for i in range(3))
         else:
@@ -350,13 +382,13 @@ class Tracer:
                     rec = (hit["vidx"], hit["len"])
                 first = False
             if hit["found"]:
-                mat = MATERIALS[min(hit["voxel"], 3)]
+                mat = self.mats[min(hit["voxel"], 3)]
                 if mat[2] and ray["r"] < self.R:
                     if len(stack) < cap:
                         stack.append(self.reflection_ray(ray, hit))
                     else:
                         stats["flags"] |= 4
-                if mat[1] and ray["t"] < self.T and mat[6][3] != ONE:
+                if mat[1] and ray["t"] < self.T and self.color(hit)[3] != ONE:
                     if len(stack) < cap:
                         stack.append(self.refraction_ray(ray, hit))
                     else:

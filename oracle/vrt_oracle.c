@@ -111,25 +111,29 @@ EXPORT void oracle_randomize_direction(const float dir[3], const float pos[3], f
   out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
 
-/* ------------------------------------------------ materials, voxel.glsl:71-93 (_COLOR_ONLY) */
+/* ---------------------------------------------------------- materials, voxel.glsl:50-93 */
 
 typedef struct {
   float refractivity;
   int transparent, reflective;
   float diffuse, specularity, exponent;
-  float color[4];
+  float color[4];      /* _COLOR_ONLY */
+  int tex_x, tex_y;    /* textured: atlas slot */
 } material_t;
 
-static const material_t k_materials[4] = {
-  {1.0f, 1, 0, 0.0f, 0.0f, 0.0f, {0.0f, 0.0f, 0.0f, 0.0f}},    /* Air   :83 */
-  {1.0f, 0, 0, 0.4f, 0.2f, 10.0f, {0.5f, 0.5f, 0.5f, 1.0f}},   /* Stone :84 */
-  {1.5f, 1, 1, 1.0f, 1.0f, 1.0f, {0.0f, 0.0f, 0.0f, 0.0f}},    /* Glass :85 */
-  {1.0f, 0, 0, 0.4f, 0.2f, 10.0f, {0.05f, 0.5f, 0.1f, 1.0f}},  /* Grass :86 */
+static const material_t k_materials[4] = {   /* _COLOR_ONLY table :71-87 */
+  {1.0f, 1, 0, 0.0f, 0.0f, 0.0f, {0.0f, 0.0f, 0.0f, 0.0f}, 0, 0},    /* Air   :83 */
+  {1.0f, 0, 0, 0.4f, 0.2f, 10.0f, {0.5f, 0.5f, 0.5f, 1.0f}, 0, 0},   /* Stone :84 */
+  {1.5f, 1, 1, 1.0f, 1.0f, 1.0f, {0.0f, 0.0f, 0.0f, 0.0f}, 0, 0},    /* Glass :85 */
+  {1.0f, 0, 0, 0.4f, 0.2f, 10.0f, {0.05f, 0.5f, 0.1f, 1.0f}, 0, 0},  /* Grass :86 */
+};
+static const material_t k_materials_tex[4] = {   /* textured table :51-68 */
+  {1.0f, 1, 0, 0.0f, 0.0f, 0.0f, {0}, 0, 0},      /* Air   :64 */
+  {1.0f, 0, 0, 0.4f, 0.6f, 60.0f, {0}, 0, 0},     /* Stone :65 */
+  {1.5f, 1, 1, 1.0f, 1.0f, 0.3f, {0}, 0, 1},      /* Glass :66 */
+  {1.0f, 0, 0, 0.4f, 0.4f, 20.0f, {0}, 1, 1},     /* Grass :67 */
 };
 static const float k_ambient = 0.3f;                            /* :91 */
-
-/* GetMaterial (:156-160): clamp(int(b/255*256), 0, 3) == min(b, 3) for bytes */
-static inline const material_t* material(uint8_t b) { return &k_materials[b > 3 ? 3 : b]; }
 
 /* ------------------------------------------------------------------------- context ---- */
 
@@ -137,6 +141,9 @@ typedef struct {
   const uint8_t* vox;
   int n;
   float fn;             /* (float)u_Size */
+  int textured;         /* !_COLOR_ONLY */
+  const uint8_t* atlas; /* RGBA8, atlas_size^2 texels, row 0 = bottom (GL t = 0) */
+  int atlas_size, atlas_tex_size;   /* u_AtlasSize, u_AtlasTextureSize */
   v3 sun;               /* u_SunDir as given */
   float time, ray_noise, refl_noise, refr_noise, max_len;
   int max_refl, max_transp;
@@ -162,7 +169,38 @@ typedef struct {
   v3 normal;
   int found;
   int32_t vidx;
+  int index;            /* intersectionAxis row of the step (tie 3 clamped to 2) */
 } isect_t;
+
+/* GetMaterial (:156-160): clamp(int(b/255*256), 0, 3) == min(b, 3) for bytes */
+static inline const material_t* material(const ctx_t* c, uint8_t b) {
+  return &(c->textured ? k_materials_tex : k_materials)[b > 3 ? 3 : b];
+}
+
+/* GetTextureCoordinate (:167-172) on the hit's face plane, intersectionAxis[index][1..2] (:93),
+ * then texture(u_TextureUnit, uv) (:178): NEAREST + default REPEAT, i = floor(u * S) mod S
+ * (GL 4.5 §8.14.2), a NaN coordinate reads texel 0; RGBA8 texels read as b / 255. */
+static void get_color(const ctx_t* c, const isect_t* is, float out[4]) {
+  const material_t* m = material(c, is->voxel);
+  if (!c->textured) {
+    for (int q = 0; q < 4; q++) out[q] = m->color[q];
+    return;
+  }
+  static const int ia[3][3] = {{0, 2, 1}, {1, 0, 2}, {2, 0, 1}};
+  const float px = get(is->point, ia[is->index][1]), py = get(is->point, ia[is->index][2]);
+  const float fx = px - floorf(px), fy = py - floorf(py);
+  const float ts = (float)c->atlas_tex_size, as = (float)c->atlas_size;
+  const float tx = ((fx + (float)m->tex_x) * ts) / as;
+  const float ty = (((1.0f - fy) + (float)m->tex_y) * ts) / as;
+  const float u = tx, v = 1.0f - ty;
+  const float su = u * as, sv = v * as;
+  const int S = c->atlas_size;
+  int i = su == su ? (int)floorf(su) : 0, j = sv == sv ? (int)floorf(sv) : 0;
+  i = ((i % S) + S) % S;
+  j = ((j % S) + S) % S;
+  const uint8_t* t = c->atlas + ((size_t)j * S + i) * 4;
+  for (int q = 0; q < 4; q++) out[q] = (float)t[q] / 255.0f;
+}
 
 /* GetVoxel (:149-154): bounds test with `>` (not `>=`), then NEAREST/REPEAT texel fetch. */
 static inline uint8_t get_voxel(const ctx_t* c, v3 p, int32_t* vidx) {
@@ -211,7 +249,7 @@ static ray_t refraction_ray(const ctx_t* c, const ray_t* ray, const isect_t* is,
   uint8_t outv = get_voxel(c, add(is->point, scl(is->normal, 0.5f)), &dummy);
   uint8_t inv = get_voxel(c, sub(is->point, scl(is->normal, 0.5f)), &dummy);
   k->c[VRT_CNT_REFRACTION_PROBES]++;
-  float eta = material(outv)->refractivity / material(inv)->refractivity;
+  float eta = material(c, outv)->refractivity / material(c, inv)->refractivity;
   ray_t r;
   r.voxel = is->voxel;
   r.pos = is->point;
@@ -223,7 +261,11 @@ static ray_t refraction_ray(const ctx_t* c, const ray_t* ray, const isect_t* is,
   } else {
     r.dir = randomize_direction(r.dir, r.pos, c->refr_noise, c->time);
     r.energy = ray->energy;
-    if (ray->voxel == 0) r.energy *= 1.0f - material(is->voxel)->color[3];  /* :239-240 */
+    if (ray->voxel == 0) {   /* :239-240 */
+      float col[4];
+      get_color(c, is, col);
+      r.energy *= 1.0f - col[3];
+    }
   }
   r.len = is->len;
   r.rdepth = ray->rdepth;
@@ -255,7 +297,7 @@ static int march_shadow(const ctx_t* c, const ray_t* ray, cnt_t* k, uint32_t* st
     k->c[VRT_CNT_SHADOW_STEPS]++;
     int index = ey + 2 * ez;
     if (index > 2) { index = 2; k->c[VRT_CNT_TIE3]++; *flags |= VRT_HIT_FLAG_TIE3; }
-    if (voxel != 0 && !material(voxel)->transparent) return 1;
+    if (voxel != 0 && !material(c, voxel)->transparent) return 1;
     float q = ((get(cur, index) + get(stepDir, index)) - get(ray->pos, index)) /
                   get(ray->dir, index) - (rayLength - ray->len);
     set(&t, index, q);
@@ -296,11 +338,13 @@ static isect_t march(const ctx_t* c, ray_t* ray, cnt_t* k, uint32_t* steps, uint
     if (voxel != 0 && voxel != rayVoxel) {
       isect_t h;
       h.voxel = voxel; h.point = cur; h.len = rayLength; h.normal = normal; h.found = 1;
+      h.index = index;
       h.vidx = vidx;
       return h;
     } else if (rayVoxel != 0 && voxel == 0) {   /* leaving a transparent voxel :357-380 */
       isect_t is;
       is.voxel = voxel; is.point = cur; is.len = rayLength; is.normal = normal; is.found = 1;
+      is.index = index;
       is.vidx = vidx;
       v3 oldDir = ray->dir;
       *ray = refraction_ray(c, ray, &is, k);
@@ -347,7 +391,7 @@ static isect_t trace_with_shadow(const ctx_t* c, ray_t* ray, v3* color, cnt_t* k
     k->c[VRT_CNT_SHADOW_RAYS]++;
     int in_shadow = march_shadow(c, &sr, k, steps, flags);
     float brightness;
-    const material_t* m = material(is.voxel);
+    const material_t* m = material(c, is.voxel);
     if (in_shadow) {
       brightness = k_ambient;
     } else {
@@ -358,10 +402,12 @@ static isect_t trace_with_shadow(const ctx_t* c, ray_t* ray, v3* color, cnt_t* k
     }
     /* RayColor :184-188 */
     float e = ray->energy;
-    float a = m->color[3];
-    color->x = mixf(color->x, m->color[0] * a * brightness, e);
-    color->y = mixf(color->y, m->color[1] * a * brightness, e);
-    color->z = mixf(color->z, m->color[2] * a * brightness, e);
+    float col[4];
+    get_color(c, &is, col);
+    float a = col[3];
+    color->x = mixf(color->x, col[0] * a * brightness, e);
+    color->y = mixf(color->y, col[1] * a * brightness, e);
+    color->z = mixf(color->z, col[2] * a * brightness, e);
   } else {
     v3 sk = skybox(c, ray, *color);
     float a = 1.0f - ray->energy;
@@ -411,12 +457,13 @@ static void shade_pixel(const ctx_t* c, int px, int py, float* rgba, vrt_hit* hi
       first = 0;
     }
     if (is.found) {
-      const material_t* mt = material(is.voxel);
+      const material_t* mt = material(c, is.voxel);
       if (mt->reflective && ray.rdepth < c->max_refl) {
         if (sp < cap) stack[sp++] = reflection_ray(c, &ray, &is);
         else flags |= VRT_HIT_FLAG_STACK_FULL;
       }
-      if (mt->transparent && ray.tdepth < c->max_transp && mt->color[3] != 1.0f) {
+      float col[4];
+      if (mt->transparent && ray.tdepth < c->max_transp && (get_color(c, &is, col), col[3] != 1.0f)) {
         if (sp < cap) stack[sp++] = refraction_ray(c, &ray, &is, k);
         else flags |= VRT_HIT_FLAG_STACK_FULL;
       }
@@ -469,7 +516,8 @@ EXPORT int oracle_render(const vrt_camera* cam, const uint8_t* vox, int n, const
                          int row0, int rows, int row_step, float* out_rgba, vrt_hit* out_hit,
                          uint64_t* counters, int nthreads) {
   if (!cam || !vox || !p || !out_rgba || n <= 0 || rows < 0) return VRT_ERR_INVALID;
-  if (!p->color_only) return VRT_ERR_UNSUPPORTED;
+  if (!p->color_only && (!p->atlas_rgba || p->atlas_size <= 0 || p->atlas_texture_size <= 0))
+    return VRT_ERR_INVALID;
   if (p->max_reflections < 0 || p->max_transparencies < 0 ||
       p->max_reflections + p->max_transparencies + 1 > MAX_STACK)
     return VRT_ERR_UNSUPPORTED;
@@ -486,6 +534,10 @@ EXPORT int oracle_render(const vrt_camera* cam, const uint8_t* vox, int n, const
   c.max_refl = p->max_reflections;
   c.max_transp = p->max_transparencies;
   c.inv_pv = cam->inv_pv;
+  c.textured = !p->color_only;
+  c.atlas = p->atlas_rgba;
+  c.atlas_size = p->atlas_size;
+  c.atlas_tex_size = p->atlas_texture_size;
   c.width = cam->width;
   c.height = cam->height;
   job_t j;
@@ -690,4 +742,21 @@ EXPORT void oracle_temporal_from_raw(const uint8_t* raw_rgba8, const uint8_t* pr
     }
     cur_rgba8[i * 4 + 3] = 255;
   }
+}
+
+/* GetColor for one hit (known-answer tests of the textured path) */
+EXPORT void oracle_get_color(const uint8_t* atlas, int atlas_size, int atlas_tex_size, int textured,
+                             uint8_t voxel, const float point[3], int index, float out[4]) {
+  ctx_t c;
+  memset(&c, 0, sizeof c);
+  c.textured = textured;
+  c.atlas = atlas;
+  c.atlas_size = atlas_size;
+  c.atlas_tex_size = atlas_tex_size;
+  isect_t is;
+  memset(&is, 0, sizeof is);
+  is.voxel = voxel;
+  is.point = mk(point[0], point[1], point[2]);
+  is.index = index;
+  get_color(&c, &is, out);
 }

@@ -114,12 +114,78 @@ def test_row_bands_compose_to_full_frame(renderer):
         assert np.array_equal(out.reshape(h, w, 4).cpu().numpy(), full)
 
 
+TEXTURED = [
+    # textured mode (voxel.glsl without _COLOR_ONLY): (scene, N, W, H, R, T, atlas, tile, extra)
+    ("terrain", 16, 128, 96, 4, 2, 256, 128, {}),
+    ("terrain", 64, 160, 90, 4, 4, 32, 16, dict(ray_noise=0.02, time=3.0)),
+    ("glass_cube", 32, 128, 96, 4, 4, 256, 128, dict(reflection_noise=0.05, time=2.0)),
+    ("refraction", 128, 192, 108, 4, 4, 256, 128, {}),
+    ("glass_cube", 16, 15, 15, 4, 4, 256, 128, dict(pos=(0.25, 0.25, 0.25),
+                                                    rot=(-35.26439, 45.0, 0.0))),
+]
+
+
+@pytest.mark.parametrize("case", TEXTURED, ids=[f"tex_{c[0]}{c[1]}_{c[6]}_{i}"
+                                                for i, c in enumerate(TEXTURED)])
+def test_parity_textured(renderer, case):
+    scene, n, w, h, R, T, size, ts, extra = case
+    extra = dict(extra)
+    vox = vrt.build_scene(scene, n)
+    renderer.upload_volume(vox, n)
+    cam = vrt.make_camera(w, h, **{k: extra.pop(k) for k in ("pos", "rot") if k in extra})
+    p = vrt.textured_params(vrt.default_params(R, T, **extra), vrt.make_atlas(size, ts), ts)
+    rgba_g, hits_g, st = renderer.render(cam, p)
+    rgba_o, hits_o, cnt_o = oracle.render(cam, vox, n, p, threads=THREADS)
+    compare(rgba_g, hits_g, st, rgba_o, hits_o, cnt_o)
+
+
+def test_parity_textured_full_size_refraction(renderer):
+    """C3's frame (1920x1080, 128^3, (4,4)) in textured mode, the reference's default build."""
+    vox = vrt.build_scene("refraction", 128)
+    renderer.upload_volume(vox, 128)
+    cam = vrt.make_camera(1920, 1080)
+    p = vrt.textured_params(vrt.default_params(4, 4), vrt.make_atlas())
+    rgba_g, hits_g, st = renderer.render(cam, p)
+    rgba_o, hits_o, cnt_o = oracle.render(cam, vox, 128, p, threads=THREADS)
+    compare(rgba_g, hits_g, st, rgba_o, hits_o, cnt_o)
+
+
+def test_atlas_upload_and_switching(renderer):
+    """The context keeps the atlas: an explicit upload serves a params block without a pointer;
+    a different pointer re-uploads; colour-only renders are unaffected."""
+    vox = vrt.build_scene("terrain", 16)
+    renderer.upload_volume(vox, 16)
+    cam = vrt.make_camera(64, 48)
+    a1, a2 = vrt.make_atlas(seed=1), vrt.make_atlas(seed=2)
+    p1 = vrt.textured_params(vrt.default_params(4, 2), a1)
+    ref1, _, _ = oracle.render(cam, vox, 16, p1, threads=THREADS)
+    renderer.upload_atlas(a1)
+    p_noptr = vrt.default_params(4, 2)
+    p_noptr.color_only, p_noptr.atlas_size, p_noptr.atlas_texture_size = 0, 256, 128
+    g1, _, _ = renderer.render(cam, p_noptr)
+    assert np.abs(np.clip(g1, 0, 1) - np.clip(ref1, 0, 1)).max() <= COLOR_TOL
+    p2 = vrt.textured_params(vrt.default_params(4, 2), a2)
+    g2, _, _ = renderer.render(cam, p2)
+    ref2, _, _ = oracle.render(cam, vox, 16, p2, threads=THREADS)
+    assert np.abs(np.clip(g2, 0, 1) - np.clip(ref2, 0, 1)).max() <= COLOR_TOL
+    assert np.abs(ref1 - ref2).max() > 1e-3
+    g0, _, _ = renderer.render(cam, vrt.default_params(4, 2))
+    r0, _, _ = oracle.render(cam, vox, 16, vrt.default_params(4, 2), threads=THREADS)
+    assert np.abs(np.clip(g0, 0, 1) - np.clip(r0, 0, 1)).max() <= COLOR_TOL
+
+
 def test_errors_are_reported(renderer):
     cam = vrt.make_camera(8, 8)
     p = vrt.default_params()
-    p.color_only = 0
+    p.color_only = 0          # textured, but no atlas uploaded and none given
+    p.atlas_size, p.atlas_texture_size = 64, 32
+    fresh = vrt.Renderer(0)
+    fresh.upload_volume(vrt.build_scene("glass_cube", 16), 16)
     with pytest.raises(vrt.VrtError) as e:
-        renderer.render(cam, p)
-    assert e.value.code == -5
+        fresh.render(cam, p)
+    assert e.value.code == -1
+    fresh.close()
+    with pytest.raises(vrt.VrtError):
+        renderer.upload_atlas(np.zeros((48, 48, 4), np.uint8))   # not a power of two
     with pytest.raises(vrt.VrtError):
         renderer.upload_volume(np.zeros(27, np.uint8), 3)   # N must be a power of two

@@ -88,6 +88,65 @@ def counters_dict(values) -> dict:
     return {name: int(values[i]) for i, name in enumerate(COUNTER_NAMES)}
 
 
+# ---- textured mode (voxel.glsl without _COLOR_ONLY) ---------------------
+# Atlas layout (ABI): RGBA8 texels, atlas_size x atlas_size, row r at GL t = (r + 0.5) / size
+# (row 0 = bottom, as glTexImage2D consumes rows). Slot (texX, texY) of a material
+# (voxel.glsl:64-67) covers columns [texX*ts, (texX+1)*ts) and rows
+# [size - (texY+1)*ts, size - texY*ts), which is where GetTextureCoordinate (:167-172) lands.
+ATLAS_SLOTS = {"stone": (0, 0), "dirt": (1, 0), "glass": (0, 1), "grass": (1, 1)}
+
+
+def atlas_slot_rows(size: int, ts: int, tex_x: int, tex_y: int):
+    return slice(size - (tex_y + 1) * ts, size - tex_y * ts), slice(tex_x * ts, (tex_x + 1) * ts)
+
+
+def make_atlas(atlas_size: int = 256, texture_size: int = 128, seed: int = 0) -> np.ndarray:
+    """Deterministic synthetic atlas [size, size, 4] uint8 (the reference's PNG textures are not
+    shipped): per-slot base colour x value noise; the glass slot has alpha 40..255 with a band of
+    fully opaque texels (so both sides of GetColor(hit).a != 1, voxel.glsl:445, occur)."""
+    rng = np.random.default_rng(seed)
+    a = np.zeros((atlas_size, atlas_size, 4), np.uint8)
+    base = {"stone": (128, 128, 128), "dirt": (120, 80, 40), "glass": (170, 220, 255),
+            "grass": (30, 160, 40)}
+    for name, (tx, ty) in ATLAS_SLOTS.items():
+        rs, cs = atlas_slot_rows(atlas_size, texture_size, tx, ty)
+        noise = rng.uniform(0.6, 1.0, (texture_size, texture_size, 1))
+        rgb = np.clip(np.array(base[name], np.float64) * noise, 0, 255)
+        a[rs, cs, :3] = rgb.astype(np.uint8)
+        if name == "glass":
+            alpha = rng.integers(40, 256, (texture_size, texture_size))
+            alpha[:, : texture_size // 8] = 255
+            a[rs, cs, 3] = alpha
+        else:
+            a[rs, cs, 3] = 255
+    return a
+
+
+def load_atlas(texture_dir: str, suffix: str = "128", atlas_size: int = 256) -> np.ndarray:
+    """Atlas from the reference's res/textures/{stone,dirt,glass,grass}<suffix>.png (main.cpp:187-
+    193), for demos on a host that has them (needs PIL); tests use make_atlas()."""
+    from PIL import Image
+
+    a = np.zeros((atlas_size, atlas_size, 4), np.uint8)
+    for name, (tx, ty) in ATLAS_SLOTS.items():
+        im = np.asarray(Image.open(f"{texture_dir}/{name}{suffix}.png").convert("RGBA"))
+        ts = im.shape[0]
+        rs, cs = atlas_slot_rows(atlas_size, ts, tx, ty)
+        a[rs, cs] = im[::-1]   # image rows are top-down; atlas rows bottom-up
+    return a
+
+
+def textured_params(p: Params, atlas: np.ndarray, texture_size: int = 128) -> Params:
+    """Switch params to textured mode with this atlas (kept alive on the Params object)."""
+    atlas = np.ascontiguousarray(atlas, np.uint8)
+    p.color_only = 0
+    p.atlas_rgba = atlas.ctypes.data_as(C.POINTER(C.c_uint8))
+    p.atlas_size = atlas.shape[0]
+    p.atlas_texture_size = texture_size
+    p._atlas_ref = atlas
+    return p
+
+
 def algorithmic_bytes(c: dict, pixel_bytes: int = 16) -> int:
     """1 B per DDA step (both marches) + 2 B per refraction probe + the per-pixel output bytes:
     16 for the float RGBA frame, 8 for the fused temporal RGB8 path (4 B history
@@ -208,3 +267,10 @@ class Renderer:
     def history_reset(self):
         """Key F (main.cpp:417-421): the last ray-traced frame becomes the temporal history."""
         self._check(self._lib.vrt_history_reset(self._h), "vrt_history_reset")
+
+
+    def upload_atlas(self, atlas: np.ndarray):
+        """Textured mode's atlas ([S, S, 4] uint8, row 0 = bottom) into the context."""
+        a = np.ascontiguousarray(atlas, np.uint8)
+        self._check(self._lib.vrt_upload_atlas(self._h, a.ctypes.data, a.shape[0]),
+                    "vrt_upload_atlas")

@@ -127,6 +127,7 @@ SIGNATURES = {
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p, C.POINTER(Stats)],
     ),
     "vrt_history_reset": (C.c_int, [C.c_void_p]),
+    "vrt_upload_atlas": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
     "vrt_terrain_noise": (C.c_int, [C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_build_scene": (C.c_int, [C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_camera_make": (

@@ -34,6 +34,9 @@ struct KArgs {
   int32_t n, width, height;
   int32_t row0, rows, row_step;
   int32_t max_refl, max_transp;
+  // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom
+  int32_t textured, atlas_size, atlas_tex_size;
+  const uint32_t* atlas;
   // temporal epilogue (cur != nullptr): RGB8 store + temporal.glsl blend instead of float RGBA
   float alpha;
   const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
@@ -112,8 +115,16 @@ __device__ __forceinline__ float mat_refr(uint32_t b) { return mat_id(b) == 2 ? 
 __device__ __forceinline__ bool mat_transparent(uint32_t m) { return m == 0 || m == 2; }
 __device__ __forceinline__ bool mat_reflective(uint32_t m) { return m == 2; }
 __device__ __forceinline__ float mat_kd(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 0.4f); }
-__device__ __forceinline__ float mat_ks(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 0.2f); }
-__device__ __forceinline__ float mat_exp(uint32_t m) { return m == 0 ? 0.0f : (m == 2 ? 1.0f : 10.0f); }
+// specular factor / exponent: _COLOR_ONLY table (:83-86) or the textured table (:64-67)
+__device__ __forceinline__ float mat_ks(uint32_t m, bool tex) {
+  return m == 0 ? 0.0f : (m == 2 ? 1.0f : (tex ? (m == 1 ? 0.6f : 0.4f) : 0.2f));
+}
+__device__ __forceinline__ float mat_exp(uint32_t m, bool tex) {
+  return m == 0 ? 0.0f : (m == 2 ? (tex ? 0.3f : 1.0f) : (tex ? (m == 1 ? 60.0f : 20.0f) : 10.0f));
+}
+// atlas slot (texX, texY) of the textured table (:64-67)
+__device__ __forceinline__ uint32_t mat_tex_x(uint32_t m) { return m == 3 ? 1u : 0u; }
+__device__ __forceinline__ uint32_t mat_tex_y(uint32_t m) { return m >= 2 ? 1u : 0u; }
 __device__ __forceinline__ float4 mat_color(uint32_t m) {
   if (m == 1) return make_float4(0.5f, 0.5f, 0.5f, 1.0f);
   if (m == 3) return make_float4(0.05f, 0.5f, 0.1f, 1.0f);
@@ -136,6 +147,7 @@ struct Hit {
   float len;
   uint32_t voxel;
   int32_t vidx;  // canonical index x + y*N + z*N*N of the texel read
+  int32_t axis;  // intersectionAxis row of the step (tie 3 clamped to 2)
   bool found;
 };
 
@@ -160,6 +172,9 @@ struct Ctx {
 #if VRT_LDS_AXIS
   float4* ax;  // this lane's 3-entry axis table in LDS: {pos, dir, rcp, sign} per axis
 #endif
+  const uint32_t* atlas;  // textured instances only (TEX)
+  uint32_t atlas_mask;   // atlas_size - 1 (power of two)
+  float atlas_fs, atlas_fts;  // (float)u_AtlasSize, (float)u_AtlasTextureSize
 };
 
 // a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024)
@@ -604,6 +619,26 @@ __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len
 }
 
 // GetReflectionRay (voxel.glsl:203-215)
+// GetColor (:174-182). Textured: GetTextureCoordinate (:167-172) on the hit's face plane
+// intersectionAxis[axis][1..2] (:93), then texture(u_TextureUnit, uv): NEAREST + REPEAT,
+// i = floor(u * S) mod S (GL 4.5 §8.14.2; NaN -> 0 via v_cvt_flr), texels b / 255.
+template <bool TEX>
+__device__ __forceinline__ float4 get_color(const Ctx& c, const Hit& h) {
+  const uint32_t m = mat_id(h.voxel);
+  if (!TEX) return mat_color(m);
+  const float px = h.axis == 0 ? h.point.z : h.point.x;   // intersectionAxis[a][1]
+  const float py = h.axis == 2 ? h.point.y : (h.axis == 1 ? h.point.z : h.point.y);  // [a][2]
+  const float fx = px - floorf(px), fy = py - floorf(py);
+  const float tx = ((fx + float(mat_tex_x(m))) * c.atlas_fts) / c.atlas_fs;
+  const float ty = (((1.0f - fy) + float(mat_tex_y(m))) * c.atlas_fts) / c.atlas_fs;
+  const float u = tx, v = 1.0f - ty;
+  const uint32_t i = cvt_flr(u * c.atlas_fs) & c.atlas_mask;
+  const uint32_t j = cvt_flr(v * c.atlas_fs) & c.atlas_mask;
+  const uint32_t t = c.atlas[j * (c.atlas_mask + 1u) + i];
+  return make_float4(float(t & 0xFFu) / 255.0f, float((t >> 8) & 0xFFu) / 255.0f,
+                     float((t >> 16) & 0xFFu) / 255.0f, float(t >> 24) / 255.0f);
+}
+
 __device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
   Ray r;
   r.voxel = 0;
@@ -617,6 +652,7 @@ __device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
 }
 
 // GetRefractionRay (voxel.glsl:217-246)
+template <bool TEX>
 __device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counters& k) {
   const uint32_t outv = get_voxel(c, h.point + h.normal * 0.5f);
   const uint32_t inv = get_voxel(c, h.point - h.normal * 0.5f);
@@ -633,7 +669,7 @@ __device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counte
   } else {
     r.dir = randomize(r.dir, r.pos, c.refr_noise, c.time);
     r.energy = ray.energy;
-    if (ray.voxel == 0) r.energy *= 1.0f - mat_color(mat_id(h.voxel)).w;
+    if (ray.voxel == 0) r.energy *= 1.0f - get_color<TEX>(c, h).w;  // :239-240
   }
   r.len = h.len;
   r.rdepth = ray.rdepth;
@@ -677,7 +713,7 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -686,6 +722,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
   h.voxel = 0;
   h.point = mk(0.0f, 0.0f, 0.0f);
   h.normal = h.point;
+  h.axis = 0;
   WalkState w;
   walk_init(w, ray);
   uint32_t medium = ray.voxel;
@@ -706,6 +743,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
       h.point = w.cur;
       h.len = w.len;
       h.normal = normal;
+      h.axis = axis;
       break;
     }
     // rayVoxel != 0 && voxel == 0: leaving a transparent voxel, refract in place (:357-380)
@@ -716,8 +754,9 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     e.point = w.cur;
     e.len = w.len;
     e.normal = normal;
+    e.axis = axis;
     const f3 old_dir = ray.dir;
-    ray = refraction_ray(c, ray, e, k);
+    ray = refraction_ray<TEX>(c, ray, e, k);
     ray.tdepth--;
     if (ray.voxel == medium) {
       internal++;
@@ -738,10 +777,10 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
 }
 
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
-template <bool STATS>
+template <bool STATS, bool TEX>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS>(c, ray, k, steps, flags);
+  const Hit h = march<STATS, TEX>(c, ray, k, steps, flags);
   if (h.found) {
     Ray sr;  // GetShadowRay (:191-201)
     sr.voxel = h.voxel;
@@ -760,10 +799,10 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
     } else {
       const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sr.dir), 0.0f);
       const float specular =
-          mat_ks(m) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m));
+          mat_ks(m, TEX) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m, TEX));
       brightness = kAmbient + diffuse + specular;
     }
-    const float4 col = mat_color(m);  // RayColor (:184-188)
+    const float4 col = get_color<TEX>(c, h);  // RayColor (:184-188)
     const float e = ray.energy;
     color.x = mixf(color.x, col.x * col.w * brightness, e);
     color.y = mixf(color.y, col.y * col.w * brightness, e);
@@ -860,8 +899,8 @@ constexpr int kCntReplicas = 256;
 // holds secondary rays, so pixels that spawn none never touch it.
 // STATS: this instance writes hit records and/or counters. Without it the per-lane counters,
 // step/flag/tie tracking are dead code (~20 VGPRs and a VALU per DDA step freed); the rendering
-// arithmetic is the same source in both instances.
-template <bool STATS>
+// arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
+template <bool STATS, bool TEX>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -895,6 +934,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     c.time = a.time;
     c.refl_noise = a.refl_noise;
     c.refr_noise = a.refr_noise;
+    c.atlas = a.atlas;
+    c.atlas_mask = uint32_t(a.atlas_size) - 1u;
+    c.atlas_fs = float(a.atlas_size);
+    c.atlas_fts = float(a.atlas_tex_size);
 #if VRT_LDS_AXIS
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * 3];
@@ -928,7 +971,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     uint32_t steps = 0, flags = 0;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
-    const Hit h0 = trace_with_shadow<STATS>(c, ray, color, k, steps, flags);
+    const Hit h0 = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
     const int32_t hit_vidx = h0.found ? h0.vidx : -1;
     const float hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
@@ -944,15 +987,15 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
             if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
             else flags |= VRT_HIT_FLAG_STACK_FULL;
           }
-          if (mat_transparent(m) && ray.tdepth < a.max_transp && mat_color(m).w != 1.0f) {
-            if (sp < cap) stack[sp++] = refraction_ray(c, ray, h, k);
+          if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
+            if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
             else flags |= VRT_HIT_FLAG_STACK_FULL;
           }
         }
         if (sp == 0) break;
         ray = stack[--sp];
         k.c[VRT_CNT_SECONDARY_RAYS]++;
-        h = trace_with_shadow<STATS>(c, ray, color, k, steps, flags);
+        h = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
       }
     }
     const uint32_t l2 = lane_id();
@@ -1076,6 +1119,10 @@ struct vrt_ctx {
   uint32_t* d_raw = nullptr;
   int hist_last = 0;  // index of lastFrameBuffer in d_hist
   int32_t hist_w = 0, hist_h = 0;
+  // textured mode: the atlas (RGBA8 words), and which host buffer it came from
+  uint32_t* d_atlas = nullptr;
+  int32_t atlas_size = 0;
+  const uint8_t* atlas_src = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
 };
@@ -1097,13 +1144,37 @@ int hip_fail(vrt_ctx* c, hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
   } while (0)
 
+int upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t size) {
+  if (!rgba || size < 1 || size > 8192 || (size & (size - 1)) != 0)
+    return fail(ctx, VRT_ERR_INVALID, "atlas edge must be a power of two in [1, 8192]");
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t bytes = size_t(size) * size * 4;
+  if (ctx->atlas_size != size) {
+    if (ctx->d_atlas) (void)hipFree(ctx->d_atlas);
+    ctx->d_atlas = nullptr;
+    ctx->atlas_size = 0;
+    if (hipMalloc(&ctx->d_atlas, bytes) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc atlas");
+  }
+  VRT_HIP(ctx, hipMemcpy(ctx->d_atlas, rgba, bytes, hipMemcpyHostToDevice));
+  ctx->atlas_size = size;
+  ctx->atlas_src = rgba;
+  return VRT_OK;
+}
+
 int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) {
   if (!cam || !p) return fail(ctx, VRT_ERR_INVALID, "null camera or params");
   if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
   if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
     return fail(ctx, VRT_ERR_INVALID, "bad image size");
-  if (!p->color_only)
-    return fail(ctx, VRT_ERR_UNSUPPORTED, "textured mode is not in ABI v1 (color_only must be 1)");
+  if (!p->color_only) {  // textured mode: the context's atlas (uploaded here when it changes)
+    if (p->atlas_rgba && (p->atlas_rgba != ctx->atlas_src || p->atlas_size != ctx->atlas_size)) {
+      const int st = upload_atlas(ctx, p->atlas_rgba, p->atlas_size);
+      if (st != VRT_OK) return st;
+    }
+    if (!ctx->d_atlas || p->atlas_size != ctx->atlas_size)
+      return fail(ctx, VRT_ERR_INVALID, "textured mode needs an atlas of atlas_size (vrt_upload_atlas)");
+    if (p->atlas_texture_size <= 0) return fail(ctx, VRT_ERR_INVALID, "atlas_texture_size must be > 0");
+  }
   if (p->max_reflections < 0 || p->max_transparencies < 0 ||
       p->max_reflections + p->max_transparencies + 1 > vrt::kMaxStack)
     return fail(ctx, VRT_ERR_UNSUPPORTED, "max_reflections + max_transparencies must be <= 16");
@@ -1136,6 +1207,10 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.row_step = row_step;
   a.max_refl = p->max_reflections;
   a.max_transp = p->max_transparencies;
+  a.textured = p->color_only ? 0 : 1;
+  a.atlas_size = p->color_only ? 1 : p->atlas_size;
+  a.atlas_tex_size = p->atlas_texture_size;
+  a.atlas = ctx->d_atlas;
   a.alpha = 1.0f;
   a.prev = nullptr;
   a.cur = nullptr;
@@ -1155,7 +1230,10 @@ void free_history(vrt_ctx* ctx) {
 void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
   dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
-  hipLaunchKernelGGL((hit || cnt) ? vrt::render_kernel<true> : vrt::render_kernel<false>, grid,
+  const bool stats = hit || cnt;
+  hipLaunchKernelGGL(a.textured ? (stats ? vrt::render_kernel<true, true> : vrt::render_kernel<false, true>)
+                                : (stats ? vrt::render_kernel<true, false> : vrt::render_kernel<false, false>),
+                     grid,
                      dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
                      cnt ? ctx->d_cnt_rep : nullptr);
   if (cnt) hipLaunchKernelGGL(vrt::reduce_counters_kernel, dim3(1), dim3(64), 0, s, ctx->d_cnt_rep, cnt);
@@ -1243,6 +1321,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (c->d_hit) (void)hipFree(c->d_hit);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
   if (c->d_cnt_rep) (void)hipFree(c->d_cnt_rep);
+  if (c->d_atlas) (void)hipFree(c->d_atlas);
   free_history(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1381,6 +1460,13 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, f
   }
   ctx->err.clear();
   return VRT_OK;
+}
+
+int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size) {
+  if (!ctx) return VRT_ERR_INVALID;
+  const int st = upload_atlas(ctx, rgba, atlas_size);
+  if (st == VRT_OK) ctx->err.clear();
+  return st;
 }
 
 int vrt_history_reset(vrt_ctx* ctx) {

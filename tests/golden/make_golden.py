@@ -33,10 +33,15 @@ FIXTURES = [
     ("refraction16_64", "refraction", 16, 64, 64, 4, 4, {}),
     ("glass_cube16_axis_aligned_33", "glass_cube", 16, 33, 33, 4, 4,
      dict(pos=(0.0, 0.0, 0.0), rot=(0.0, 0.0, 0.0))),
+    # textured mode (the reference's default build); the fixture stores its 32x32 atlas
+    ("textured_terrain16_64", "terrain", 16, 64, 64, 4, 2, dict(atlas=(32, 16, 5))),
+    ("textured_glass_cube16_48", "glass_cube", 16, 48, 48, 4, 4,
+     dict(atlas=(32, 16, 6), reflection_noise=0.05, time=2.0)),
 ]
 
 PARAM_KEYS = ("time", "ray_noise", "reflection_noise", "refraction_noise", "max_ray_length",
-              "max_reflections", "max_transparencies", "color_only")
+              "max_reflections", "max_transparencies", "color_only", "atlas_size",
+              "atlas_texture_size")
 
 
 def main():
@@ -44,7 +49,13 @@ def main():
         extra = dict(extra)
         pose = {k: extra.pop(k) for k in ("pos", "rot") if k in extra}
         cam = vrt.make_camera(w, h, **pose)
+        atlas_spec = extra.pop("atlas", None)
         p = vrt.default_params(R, T, **extra)
+        atlas = np.zeros((0, 0, 4), np.uint8)
+        if atlas_spec:
+            size, ts, seed = atlas_spec
+            atlas = vrt.make_atlas(size, ts, seed)
+            p = vrt.textured_params(p, atlas, ts)
         vox = vrt.build_scene(scene, n)
         rgba, hits, cnt = oracle.render(cam, vox, n, p, threads=8)
         params = {k: getattr(p, k) for k in PARAM_KEYS}
@@ -60,6 +71,7 @@ def main():
             ray_length_bits=hits["ray_length"].view(np.uint32),
             steps=hits["steps"],
             flags=hits["flags"],
+            atlas=atlas,
         )
         print(name, cnt)
 

@@ -29,6 +29,8 @@ def load(path):
             p.sun_dir = (abi.C.c_float * 3)(*v)
         else:
             setattr(p, k, v)
+    if "atlas" in z.files and z["atlas"].size:
+        p = vrt.textured_params(p, z["atlas"], meta["params"]["atlas_texture_size"])
     vox = vrt.build_scene(meta["scene"], meta["n"], meta["seed"])
     return z, meta, cam, p, vox
 

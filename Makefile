@@ -10,7 +10,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -Iinclude -Wall
 SRC := voxelraytracer_amd/csrc/vrt_render.hip voxelraytracer_amd/csrc/vrt_host.cpp
 
-all: $(LIBDIR)/libvrt.so oracle
+all: $(LIBDIR)/libvrt.so oracle app
 
 $(LIBDIR)/libvrt.so: $(SRC) include/vrt.h
 	mkdir -p $(LIBDIR)
@@ -18,6 +18,14 @@ $(LIBDIR)/libvrt.so: $(SRC) include/vrt.h
 
 oracle:
 	$(MAKE) -C oracle
+
+# headless C++ host of the frame loop (examples/headless_app.cpp), linked against the C-ABI
+app: build/bin/vrt_headless
+
+build/bin/vrt_headless: examples/headless_app.cpp include/vrt.h $(LIBDIR)/libvrt.so
+	mkdir -p build/bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ examples/headless_app.cpp -L$(LIBDIR) -lvrt \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 
 # experiment variants for scripts/ab.py: make variant NAME=w5 DEFS="-DVRT_MIN_WAVES=5"
 variant: $(SRC) include/vrt.h
@@ -33,4 +41,4 @@ clean:
 	rm -rf $(LIBDIR) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean variant
+.PHONY: all oracle app asm clean variant

@@ -1,0 +1,202 @@
+// Headless AppScene: the frame loop of src/main.cpp (AppScene, :138-430) driven through the C-ABI
+// of include/vrt.h instead of GL + Greet (the drop-in demonstrated in the
+// reference's own language). What it mirrors:
+//   - volume: the _TERRAIN / _GLASS_CUBE / _REFRACTION builders (main.cpp:218-288) ->
+//     vrt_build_scene, uploaded once (replaces glTexImage3D, :315-318)
+//   - camera: Perspective(aspect, 90, 0.01, 100) at the "C" key pose (-3.45, 2.17, 3.53),
+//     (-33, -48, 0) degrees (:161, :171-172, :415-416) -> vrt_camera_make
+//   - per frame (Render, :323-361): u_Time = 1, 2, 3, ... (:343-345), u_SunDir from timeOfDay
+//     (:346-348, "Make day" = 0.9 * dayTime, :577) advanced by Update's day/night clock
+//     (:397-404) when --day-night is given, noise uniforms (:156-158)
+//   - RGB8 store + temporal filter + FBO swap (:363-393) -> vrt_render_frame
+//   - "Clear framebuffer" (key F, :417-421) -> vrt_history_reset, via --reset-at K
+//   - the GUI's FPS label from GL_TIME_ELAPSED (:350-360) -> vrt_stats.kernel_ms
+//   - Utils::Screenshot of the last frame (key F1, :424-428) -> a binary PPM (--ppm), and the raw
+//     RGBA8 frame (--raw, row 0 = bottom) for tests
+// Build: make app (-> build/vrt_headless). Usage: build/vrt_headless --help
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vrt.h"
+
+namespace {
+
+struct Options {
+  std::string scene = "refraction";
+  int n = 128, width = 1920, height = 1080, frames = 10;
+  int max_reflections = 4, max_transparencies = 4;
+  float alpha = 1.0f, ray_noise = 0.0f, reflection_noise = 0.0f, refraction_noise = 0.0f;
+  float frame_seconds = 0.0f;  // > 0: Update(timeElapsed) per frame (day/night cycle)
+  int reset_at = -1;           // frame index before which key F is pressed
+  std::string atlas_raw;       // textured mode: raw RGBA8 atlas file (size^2 * 4 bytes)
+  int atlas_size = 256, atlas_tile = 128;
+  std::string ppm, raw;
+  bool quiet = false;
+};
+
+void usage() {
+  std::puts(
+      "vrt_headless [--scene terrain|glass_cube|refraction] [--n N] [--size WxH] [--frames K]\n"
+      "             [--bounces R T] [--alpha A] [--ray-noise x] [--reflection-noise x]\n"
+      "             [--refraction-noise x] [--day-night SECONDS_PER_FRAME] [--reset-at K]\n"
+      "             [--atlas-raw FILE --atlas-size S --atlas-tile T] [--ppm FILE] [--raw FILE]\n"
+      "             [--quiet]");
+}
+
+bool parse(int argc, char** argv, Options& o) {
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto next = [&](const char* what) -> const char* {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", what);
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--scene") o.scene = next("--scene");
+    else if (a == "--n") o.n = std::atoi(next("--n"));
+    else if (a == "--size") {
+      if (std::sscanf(next("--size"), "%dx%d", &o.width, &o.height) != 2) return false;
+    } else if (a == "--frames") o.frames = std::atoi(next("--frames"));
+    else if (a == "--bounces") {
+      o.max_reflections = std::atoi(next("--bounces"));
+      o.max_transparencies = std::atoi(next("--bounces"));
+    } else if (a == "--alpha") o.alpha = std::strtof(next("--alpha"), nullptr);
+    else if (a == "--ray-noise") o.ray_noise = std::strtof(next("--ray-noise"), nullptr);
+    else if (a == "--reflection-noise") o.reflection_noise = std::strtof(next(a.c_str()), nullptr);
+    else if (a == "--refraction-noise") o.refraction_noise = std::strtof(next(a.c_str()), nullptr);
+    else if (a == "--day-night") o.frame_seconds = std::strtof(next("--day-night"), nullptr);
+    else if (a == "--reset-at") o.reset_at = std::atoi(next("--reset-at"));
+    else if (a == "--atlas-raw") o.atlas_raw = next("--atlas-raw");
+    else if (a == "--atlas-size") o.atlas_size = std::atoi(next("--atlas-size"));
+    else if (a == "--atlas-tile") o.atlas_tile = std::atoi(next("--atlas-tile"));
+    else if (a == "--ppm") o.ppm = next("--ppm");
+    else if (a == "--raw") o.raw = next("--raw");
+    else if (a == "--quiet") o.quiet = true;
+    else if (a == "--help" || a == "-h") return false;
+    else {
+      std::fprintf(stderr, "unknown option %s\n", a.c_str());
+      return false;
+    }
+  }
+  return true;
+}
+
+int scene_id(const std::string& s) {
+  if (s == "terrain") return VRT_SCENE_TERRAIN;
+  if (s == "glass_cube") return VRT_SCENE_GLASS_CUBE;
+  if (s == "refraction") return VRT_SCENE_REFRACTION;
+  return -1;
+}
+
+bool write_file(const std::string& path, const void* data, size_t bytes) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) return false;
+  const bool ok = std::fwrite(data, 1, bytes, f) == bytes;
+  return std::fclose(f) == 0 && ok;
+}
+
+// Utils::Screenshot equivalent: RGB, top row first (the frame's row 0 is the bottom)
+bool write_ppm(const std::string& path, const std::vector<uint8_t>& rgba, int w, int h) {
+  std::string img = "P6\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+  const size_t head = img.size();
+  img.resize(head + size_t(w) * h * 3);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x)
+      std::memcpy(&img[head + (size_t(h - 1 - y) * w + x) * 3], &rgba[(size_t(y) * w + x) * 4], 3);
+  return write_file(path, img.data(), img.size());
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  if (!parse(argc, argv, o)) {
+    usage();
+    return 2;
+  }
+  const int sid = scene_id(o.scene);
+  if (sid < 0 || o.frames < 1) {
+    usage();
+    return 2;
+  }
+  std::vector<uint8_t> vox(size_t(o.n) * o.n * o.n);
+  if (vrt_build_scene(sid, o.n, 0, vox.data()) != VRT_OK) {
+    std::fprintf(stderr, "vrt_build_scene failed\n");
+    return 1;
+  }
+  vrt_ctx* rt = nullptr;
+  if (vrt_create(0, &rt) != VRT_OK) {
+    std::fprintf(stderr, "vrt_create failed: %s\n", vrt_last_error(rt));
+    return 1;
+  }
+  int status = 0;
+  const vrt_volume vol{vox.data(), o.n};
+  if (vrt_upload_volume(rt, &vol) != VRT_OK) {
+    std::fprintf(stderr, "vrt_upload_volume: %s\n", vrt_last_error(rt));
+    vrt_destroy(rt);
+    return 1;
+  }
+  const float pos[3] = {-3.45f, 2.17f, 3.53f}, rot[3] = {-33.0f, -48.0f, 0.0f};
+  vrt_camera cam;
+  vrt_camera_make(pos, rot, o.width, o.height, 90.0f, 0.01f, 100.0f, &cam);
+  vrt_params p;
+  vrt_params_default(&p);
+  p.max_reflections = o.max_reflections;
+  p.max_transparencies = o.max_transparencies;
+  p.ray_noise = o.ray_noise;
+  p.reflection_noise = o.reflection_noise;
+  p.refraction_noise = o.refraction_noise;
+  std::vector<uint8_t> atlas;
+  if (!o.atlas_raw.empty()) {  // textured mode (the reference's default build)
+    atlas.resize(size_t(o.atlas_size) * o.atlas_size * 4);
+    FILE* f = std::fopen(o.atlas_raw.c_str(), "rb");
+    if (!f || std::fread(atlas.data(), 1, atlas.size(), f) != atlas.size()) {
+      std::fprintf(stderr, "cannot read %zu atlas bytes from %s\n", atlas.size(), o.atlas_raw.c_str());
+      if (f) std::fclose(f);
+      vrt_destroy(rt);
+      return 1;
+    }
+    std::fclose(f);
+    p.color_only = 0;
+    p.atlas_rgba = atlas.data();
+    p.atlas_size = o.atlas_size;
+    p.atlas_texture_size = o.atlas_tile;
+  }
+  const float day_time = 50.0f;        // dayTime (main.cpp:153)
+  float time_of_day = 0.9f * day_time;  // "Make day" (main.cpp:577)
+  std::vector<uint8_t> frame(size_t(o.width) * o.height * 4);
+  double ms_sum = 0.0;
+  for (int f = 0; f < o.frames && status == 0; ++f) {
+    if (f == o.reset_at) vrt_history_reset(rt);  // key F
+    p.time = float(f + 1);                       // static i; i++ (main.cpp:343-345)
+    vrt_sun_dir(time_of_day, day_time, p.sun_dir);
+    vrt_stats st;
+    if (vrt_render_frame(rt, &cam, &p, o.alpha, frame.data(), &st) != VRT_OK) {
+      std::fprintf(stderr, "vrt_render_frame: %s\n", vrt_last_error(rt));
+      status = 1;
+      break;
+    }
+    ms_sum += st.kernel_ms;
+    const uint64_t rays = st.counters[VRT_CNT_PRIMARY_RAYS] + st.counters[VRT_CNT_SECONDARY_RAYS] +
+                          st.counters[VRT_CNT_SHADOW_RAYS];
+    if (!o.quiet)
+      std::printf("frame %d  %.3f ms  fps %.0f  rays %llu  %.0f Mrays/s\n", f, st.kernel_ms,
+                  1000.0 / st.kernel_ms, (unsigned long long)rays, rays / (st.kernel_ms * 1e3));
+    if (o.frame_seconds > 0.0f) {  // Update(): day/night cycle (main.cpp:397-404)
+      time_of_day += o.frame_seconds;
+      while (time_of_day > day_time) time_of_day -= day_time;
+    }
+  }
+  if (status == 0 && !o.quiet)
+    std::printf("%d frames, mean %.3f ms (kernel + counters, synchronous API)\n", o.frames,
+                ms_sum / o.frames);
+  if (status == 0 && !o.raw.empty() && !write_file(o.raw, frame.data(), frame.size())) status = 1;
+  if (status == 0 && !o.ppm.empty() && !write_ppm(o.ppm, frame, o.width, o.height)) status = 1;
+  vrt_destroy(rt);
+  return status;
+}

@@ -88,3 +88,15 @@ def test_create_without_gpu_fails_loudly(built):
         pytest.skip("GPU present")
     with pytest.raises(vrt.VrtError):
         vrt.Renderer(0)
+
+
+def test_headless_app_builds_and_parses(built):
+    """examples/headless_app.cpp links against the C-ABI (make app); --help needs no GPU."""
+    import subprocess
+
+    app = os.path.join(ROOT, "build", "bin", "vrt_headless")
+    assert os.path.exists(app)
+    r = subprocess.run([app, "--help"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and "--scene" in r.stdout
+    r = subprocess.run([app, "--bogus"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2

@@ -14,7 +14,7 @@ dur = []
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         # the timed (stats-free) instance; older profiles have a single render_kernel
-        if "render_kernel" not in r["Kernel_Name"] or "render_kernel<true>" in r["Kernel_Name"]:
+        if "render_kernel" not in r["Kernel_Name"] or "render_kernel<true" in r["Kernel_Name"]:
             continue
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))

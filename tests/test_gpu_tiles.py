@@ -30,7 +30,7 @@ def frame_params(vrt, t):
     return vrt.default_params(4, 2, time=float(t + 1), ray_noise=0.03)
 
 
-def worker(rank, world, port, q):
+def worker(rank, world, port, q, parts):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -49,12 +49,12 @@ def worker(rank, world, port, q):
     state = {"t": 0}
 
     def render_band(row0, rows, step, out, prev):
-        ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"]), ALPHA, row0, rows, step,
-                                       prev.data_ptr(), out.data_ptr(),
+        ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"] // parts), ALPHA, row0,
+                                       rows, step, prev.data_ptr(), out.data_ptr(),
                                        stream=torch.cuda.current_stream().cuda_stream)
         state["t"] += 1
 
-    tiler = FrameTiler(W, H, render_band, dev, dtype=torch.uint8)
+    tiler = FrameTiler(W, H, render_band, dev, dtype=torch.uint8, parts=parts)
     got = []
     for _ in range(FRAMES):
         f = tiler.frame()
@@ -72,13 +72,14 @@ def worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_single_process(built):
+@pytest.mark.parametrize("parts", [1, 2])
+def test_two_ranks_on_one_gpu_match_single_process(built, parts):
     import voxelraytracer_amd as vrt
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, 2, port, q, parts)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)
@@ -95,3 +96,33 @@ def test_two_ranks_on_one_gpu_match_single_process(built):
                                            hist.data_ptr(), hist.data_ptr())
             torch.cuda.synchronize()
             assert np.array_equal(got[t], hist.cpu().numpy()), t
+
+
+def test_single_rank_two_streams_match(built):
+    """One rank, two interleaved parts on two HIP streams (the bench default): each frame
+    returned by the tiler equals the single-stream filtered frame."""
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import FrameTiler
+
+    with vrt.Renderer(0) as ren:
+        ren.upload_volume(vrt.build_scene("terrain", N), N)
+        cam = vrt.make_camera(W, H)
+        state = {"t": 0}
+
+        def render_band(row0, rows, step, out, prev):
+            ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"] // 2), ALPHA, row0,
+                                           rows, step, prev.data_ptr(), out.data_ptr(),
+                                           stream=torch.cuda.current_stream().cuda_stream)
+            state["t"] += 1
+
+        tiler = FrameTiler(W, H, render_band, torch.device("cuda", 0), dtype=torch.uint8, parts=2)
+        hist = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        for t in range(FRAMES):
+            f = tiler.frame()
+            torch.cuda.synchronize()
+            got = f.cpu().numpy()
+            ren.render_temporal_rows_async(cam, frame_params(vrt, t), ALPHA, 0, H, 1,
+                                           hist.data_ptr(), hist.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(got, hist.cpu().numpy()), t
+        tiler.finish()

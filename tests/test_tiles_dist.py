@@ -24,7 +24,7 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5):
+def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -43,7 +43,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5):
     state = {"i": 0}
 
     def render_band(row0, rows, step, out, prev):
-        rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"]], row0=row0, rows=rows,
+        rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"] // parts], row0=row0, rows=rows,
                                    row_step=step, threads=1)
         if mode == "rgba8":   # the fused temporal filter + RGB8 store, band-local history
             _, cur = oracle.temporal(rgba, prev.numpy().copy(), alpha)
@@ -53,7 +53,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5):
         state["i"] += 1
 
     tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
-                       dtype=torch.uint8 if mode == "rgba8" else torch.float32)
+                       dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts)
     got = []
     for _ in range(frames):
         f = tiler.frame()
@@ -68,8 +68,8 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_tiled_frames_match_single_process(built, world):
+@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (2, 3)])
+def test_tiled_frames_match_single_process(built, world, parts):
     import oracle
     import voxelraytracer_amd as vrt
 
@@ -77,8 +77,8 @@ def test_tiled_frames_match_single_process(built, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "f32", 0.5,
+                                              parts)) for r in range(world)]
     for p in procs:
         p.start()
     got, vox_bytes = q.get(timeout=120)
@@ -106,7 +106,8 @@ def test_band_spec_and_assembly():
     assert torch.equal(assemble_cyclic(bands), frame)
 
 
-def test_tiled_temporal_rgba8_frames(built):
+@pytest.mark.parametrize("parts", [1, 2])
+def test_tiled_temporal_rgba8_frames(built, parts):
     """RGBA8 bands with the temporal filter: each rank's history is its own band of the previous
     frame, so the assembled sequence equals the single-process filtered sequence bit for bit."""
     import oracle
@@ -116,8 +117,8 @@ def test_tiled_temporal_rgba8_frames(built):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha))
-             for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
+                                              parts)) for r in range(world)]
     for p in procs:
         p.start()
     got, _ = q.get(timeout=120)
@@ -133,3 +134,47 @@ def test_tiled_temporal_rgba8_frames(built):
                                                                    ray_noise=0.05))
         _, hist = oracle.temporal(rgba, hist, alpha)
         assert np.array_equal(got[t], hist), t
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_single_rank_parts(built, parts):
+    """One rank, several interleaved parts (the bench's tail-hiding split): the frame returned
+    each step equals the single-part filtered sequence."""
+    import oracle
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import FrameTiler
+
+    n, w, h, frames, alpha = 16, 20, 12, 3, 0.5
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    state = {"i": 0}
+
+    def render_band(row0, rows, step, out, prev):
+        p = vrt.default_params(1, 2, time=float(state["i"] // parts + 1), ray_noise=0.05)
+        rgba, _, _ = oracle.render(cam, vox, n, p, row0=row0, rows=rows, row_step=step)
+        _, cur = oracle.temporal(rgba, prev.numpy().copy(), alpha)
+        out.copy_(torch.from_numpy(cur))
+        state["i"] += 1
+
+    tiler = FrameTiler(w, h, render_band, torch.device("cpu"), dtype=torch.uint8, parts=parts)
+    hist = np.zeros((h, w, 4), np.uint8)
+    for t in range(frames):
+        got = tiler.frame().numpy().copy()
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert np.array_equal(got, hist), t
+    assert np.array_equal(tiler.finish().numpy(), hist)
+
+
+def test_part_spec_and_assembly():
+    from voxelraytracer_amd.tiles import assemble_parts, part_spec
+
+    assert part_spec(1, 4, 1, 2, 1080) == (5, 135, 8)
+    with pytest.raises(ValueError):
+        part_spec(0, 8, 0, 2, 1080)
+    frame = torch.arange(12 * 2, dtype=torch.float32).reshape(12, 2, 1)
+    world, parts = 2, 3
+    g = torch.stack([torch.stack([frame[s * world + r::world * parts] for s in range(parts)])
+                     for r in range(world)])
+    assert torch.equal(assemble_parts(g), frame)

@@ -3,15 +3,23 @@
 The per-pixel program has no halo and no inter-ray exchange, so a frame splits into row bands,
 one per rank (one process per GPU). Bands are cyclic — rank r owns rows r, r+N, r+2N, ... — so
 every rank gets the same mix of cheap sky rows and expensive geometry rows. Each rank renders its
-band into HBM; the only exchange is one gather of the RGBA bands to rank 0 per frame (RCCL over
-xGMI with the "nccl" backend; gloo on CPU for tests), after which rank 0 re-interleaves the bands
-into the frame. The volume is replicated once per GPU (broadcast_volume).
+band into HBM; the only exchange is one gather of the bands to rank 0 per frame (RCCL over xGMI
+with the "nccl" backend; gloo on CPU for tests), after which rank 0 re-interleaves the bands into
+the frame. The volume is replicated once per GPU (broadcast_volume).
 
-FrameTiler double-buffers the band so that, over a sequence of frames, the gather of frame k
-overlaps the render of frame k+1 on the compute stream. Bands are RGBA8 words when the renderer
-runs the fused temporal filter + RGB8 store (the reference's stored frame format, main.cpp:363-393):
-4 B per pixel on the wire instead of 16. The temporal history is band-local (each rank blends its
-own rows), so it adds no exchange; the previous frame's band buffer IS the history.
+Within a rank the band is rendered as P interleaved parts on P HIP streams (default P = 1; the
+bench uses 2): global part q = s*N + r owns frame rows q, q + N*P, q + 2*N*P, ... . One launch's
+last dispatch round leaves wave slots idle while its final waves finish; a second stream's launch
+fills them, so consecutive frames' parts overlap their tails (measured: C3 0.241 -> 0.220 ms per
+frame with P = 2, scripts/streams_exp.py). Ordering uses events only: a part stream waits for the
+gather that last read its buffer, the gather waits for every part of its frame — a part never
+waits for another part, so the overlap is real.
+
+FrameTiler double-buffers the band (N > 1) so that the gather of frame k overlaps the render of
+frame k+1. Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8 store
+(the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire instead of 16.
+The temporal history is part-local (each part blends its own rows, on its own stream), so it adds
+no exchange and no cross-stream dependency; the previous frame's part buffer IS the history.
 """
 from __future__ import annotations
 
@@ -28,6 +36,15 @@ def band_spec(rank: int, world: int, height: int):
     return rank, height // world, world
 
 
+def part_spec(rank: int, world: int, part: int, parts: int, height: int):
+    """(row0, rows, row_step) of part `part` of rank's band: global part q = part*world + rank
+    owns frame rows q, q + world*parts, ...; height must divide by world*parts."""
+    total = world * parts
+    if height % total:
+        raise ValueError(f"frame height {height} is not divisible by {world} ranks x {parts} parts")
+    return part * world + rank, height // total, total
+
+
 def assemble_cyclic(bands: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bands[world, rows, W, C] (rank-major) -> frame[rows*world, W, C] with frame row i*world+r
     = bands[r, i]."""
@@ -35,6 +52,17 @@ def assemble_cyclic(bands: torch.Tensor, out: Optional[torch.Tensor] = None) -> 
     if out is None:
         out = torch.empty((rows * world, w, c), dtype=bands.dtype, device=bands.device)
     out.view(rows, world, w, c).copy_(bands.permute(1, 0, 2, 3))
+    return out
+
+
+def assemble_parts(gathered: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """gathered[world, parts, rows, W, C] -> frame[rows*parts*world, W, C] with frame row
+    j*(world*parts) + part*world + rank = gathered[rank, part, j]."""
+    world, parts, rows, w, c = gathered.shape
+    if out is None:
+        out = torch.empty((rows * parts * world, w, c), dtype=gathered.dtype,
+                          device=gathered.device)
+    out.view(rows, parts, world, w, c).copy_(gathered.permute(2, 1, 0, 3, 4))
     return out
 
 
@@ -46,74 +74,98 @@ def broadcast_volume(vox: torch.Tensor, src: int = 0, group=None) -> torch.Tenso
 
 
 class FrameTiler:
-    """Renders a sequence of frames across `world` ranks.
+    """Renders a sequence of frames across `world` ranks, `parts` streams per rank.
 
-    render_band(row0, rows, row_step, out, prev) must enqueue the band render into `out`
-    ([rows, W, channels] of `dtype` on `device`) on the current stream (the HIP kernel through the
-    C-ABI, or the oracle in CPU tests); `prev` holds this rank's band of the previous frame (the
+    render_band(row0, rows, row_step, out, prev) must enqueue the render of one part into `out`
+    ([rows, W, channels] of `dtype` on `device`) on the CURRENT stream (the HIP kernel through the
+    C-ABI, or the oracle in CPU tests); `prev` holds that part's rows of the previous frame (the
     temporal history; zeros before the first frame; it is `out` itself with one buffer).
-    frame() renders the next frame and issues its gather asynchronously; on rank 0 it returns the
-    PREVIOUS frame, assembled (None on the first call and on other ranks), so the gather of frame
-    k overlaps the render of frame k+1 on every rank. Rank 0 re-interleaves on a side stream
-    (returned frames are ordered on `self.assembly_stream`). finish() drains the pipeline and
-    returns the last frame on rank 0.
+    frame() renders the next frame; with one rank it returns that frame (for parts > 1 each part
+    copies its rows into it on its own stream); with several ranks the gather is issued
+    asynchronously and rank 0 returns the PREVIOUS frame, assembled on `self.assembly_stream`
+    (None on the first call and on other ranks), so the gather of frame k overlaps the render of
+    frame k+1. finish() drains the pipeline and returns the last frame on rank 0. A returned
+    frame is valid until the next frame() call; synchronise the device before reading it.
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
-                 channels: int = 4, dtype=torch.float32):
+                 channels: int = 4, dtype=torch.float32, parts: int = 1):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.group = group
-        self.width, self.height = width, height
+        self.width, self.height, self.parts = width, height, parts
         self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
+        self.specs = [part_spec(self.rank, self.world, s, parts, height) for s in range(parts)]
+        self.rows_p = self.specs[0][1]
         self.render_band = render_band
-        shape = (self.rows, width, channels)
+        self.cuda = torch.device(device).type == "cuda"
+        shape = (parts, self.rows_p, width, channels)
         nbuf = 2 if self.world > 1 else 1
         self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.part_streams = ([torch.cuda.Stream(device=device) for _ in range(parts)]
+                             if self.cuda and parts > 1 else None)
         self.assembly_stream = None
-        if self.rank == 0 and self.world > 1 and torch.device(device).type == "cuda":
-            self.assembly_stream = torch.cuda.Stream(device=device)
         self.gathered = None
         self.frame_buf = None
+        if self.rank == 0 and (self.world > 1 or parts > 1):
+            self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
         if self.rank == 0 and self.world > 1:
             self.gathered = [torch.empty((self.world,) + shape, dtype=dtype, device=device)
                              for _ in range(nbuf)]
-            self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
-        self.pending = [None] * nbuf   # gather that still reads bands[b]
-        self.assembled = [None] * nbuf  # rank 0: assembly that still reads gathered[b]
-        self.prev = None               # rank 0: buffer index of the frame awaiting assembly
+            if self.cuda:
+                self.assembly_stream = torch.cuda.Stream(device=device)
+        self.pending = [None] * nbuf    # gather that still reads bands[b]
+        self.assembled = [None] * nbuf  # rank 0: assembly that still reads gathered[b] / bands[b]
+        self.prev = None                # rank 0: buffer index of the frame awaiting assembly
         self.k = 0
 
-    def _assemble_prev(self) -> Optional[torch.Tensor]:
-        if self.prev is None:
+    # ---- helpers ---------------------------------------------------------------------------
+    def _render_parts(self, band: torch.Tensor, prev: torch.Tensor, wait_work, assemble: bool):
+        """Enqueue every part (each waits for `wait_work`, the gather that last read its buffer;
+        with one rank and several parts each part then copies its rows into frame_buf on its own
+        stream). Returns the events that mark the parts' completion (CUDA, parts > 1)."""
+        if self.part_streams is None:
+            if wait_work is not None:
+                wait_work.wait()
+            for s, (row0, rows, step) in enumerate(self.specs):
+                self.render_band(row0, rows, step, band[s], prev[s])
+                if assemble:
+                    self._frame_rows(s).copy_(band[s])
             return None
-        b = self.prev
-        self.prev = None
-        if self.assembly_stream is not None:
-            with torch.cuda.stream(self.assembly_stream):
-                self.pending[b].wait()          # the side stream waits for the gather
-                self.pending[b] = None
-                out = assemble_cyclic(self.gathered[b], self.frame_buf)
-            self.assembled[b] = self.assembly_stream.record_event()
-            return out
-        self.pending[b].wait()
-        self.pending[b] = None
-        return assemble_cyclic(self.gathered[b], self.frame_buf)
+        events = []
+        for s, (row0, rows, step) in enumerate(self.specs):
+            st = self.part_streams[s]
+            with torch.cuda.stream(st):
+                if wait_work is not None:
+                    wait_work.wait()
+                self.render_band(row0, rows, step, band[s], prev[s])
+                if assemble:
+                    self._frame_rows(s).copy_(band[s])
+                events.append(st.record_event())
+        return events
 
+    def _frame_rows(self, s: int) -> torch.Tensor:
+        """frame_buf rows of this (single) rank's part s: rows s, s + parts, ..."""
+        return self.frame_buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
+
+    # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
-        if self.world == 1:
-            self.render_band(self.row0, self.rows, self.step, self.bands[0], self.bands[0])
-            return self.bands[0]
-        b = self.k % len(self.bands)
-        prev = self.bands[(self.k - 1) % len(self.bands)]
+        nb = len(self.bands)
+        b = self.k % nb
+        prev = self.bands[(self.k - 1) % nb]
         self.k += 1
-        if self.pending[b] is not None:   # the gather that last read this buffer must be done
-            self.pending[b].wait()
-            self.pending[b] = None
         band = self.bands[b]
-        self.render_band(self.row0, self.rows, self.step, band, prev)
+        if self.world == 1:
+            self._render_parts(band, prev, None, assemble=self.parts > 1)
+            return band[0] if self.parts == 1 else self.frame_buf
+        wait_work, self.pending[b] = self.pending[b], None
+        events = self._render_parts(band, prev, wait_work, assemble=False)
+        cur = torch.cuda.current_stream() if self.cuda else None
+        if events is not None:   # the gather (issued from the current stream) needs every part
+            for e in events:
+                cur.wait_event(e)
         if self.assembled[b] is not None:   # rank 0: the assembly that read gathered[b]
-            torch.cuda.current_stream().wait_event(self.assembled[b])
+            cur.wait_event(self.assembled[b])
             self.assembled[b] = None
         glist = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
         work = dist.gather(band, glist, dst=0, group=self.group, async_op=True)
@@ -123,12 +175,39 @@ class FrameTiler:
             self.prev = b
         return out
 
+    def _assemble_prev(self) -> Optional[torch.Tensor]:
+        """Rank 0: re-interleave the previous frame's gathered parts into frame_buf once its
+        gather is done (on the assembly stream when there is one). pending[b] is left for the
+        next render into bands[b] to wait on."""
+        if self.prev is None:
+            return None
+        b = self.prev
+        self.prev = None
+        work = self.pending[b]
+        if self.assembly_stream is None:
+            work.wait()
+            return assemble_parts(self.gathered[b], self.frame_buf)
+        with torch.cuda.stream(self.assembly_stream):
+            work.wait()
+            out = assemble_parts(self.gathered[b], self.frame_buf)
+        self.assembled[b] = self.assembly_stream.record_event()
+        return out
+
     def finish(self) -> Optional[torch.Tensor]:
         if self.world == 1:
-            return self.bands[0]
+            if self.part_streams is not None:
+                cur = torch.cuda.current_stream()
+                for st in self.part_streams:
+                    cur.wait_stream(st)
+            return self.bands[0][0] if self.parts == 1 else self.frame_buf
         out = self._assemble_prev() if self.rank == 0 else None
         for i, w in enumerate(self.pending):
             if w is not None:
                 w.wait()
                 self.pending[i] = None
+        cur = torch.cuda.current_stream() if self.cuda else None
+        for st in self.part_streams or ():
+            cur.wait_stream(st)
+        if self.assembly_stream is not None:
+            cur.wait_stream(self.assembly_stream)
         return out

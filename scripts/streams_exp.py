@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--configs", default="C3")
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--parts", default="1,2,3,4,1,2")
     a = ap.parse_args()
     for cfg in a.configs.split(","):
         scene, n, w, h, R, T, _ = CONFIGS[cfg]
@@ -59,13 +60,15 @@ def main():
             cam = vrt.make_camera(w, h)
             p = vrt.default_params(R, T)
             base = None
-            for parts in (1, 2, 3, 4, 1, 2):
+            for parts in (int(x) for x in a.parts.split(",")):
                 if h % parts:
                     continue
                 ms, img = run(ren, cam, p, w, h, parts, a.frames, a.warmup)
                 same = True if base is None else bool(np.array_equal(img, base))
                 base = img if base is None else base
-                print(f"{cfg} parts={parts}: {ms:.4f} ms/frame  identical={same}", flush=True)
+                lib = os.path.basename(os.environ.get("VRT_LIB", "libvrt.so"))
+                print(f"{cfg} {lib} parts={parts}: {ms:.4f} ms/frame  identical={same}",
+                      flush=True)
 
 
 if __name__ == "__main__":

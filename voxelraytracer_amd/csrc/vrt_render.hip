@@ -891,7 +891,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
 constexpr int kCntReplicas = 256;
 
 #ifndef VRT_MIN_WAVES
-#define VRT_MIN_WAVES 6
+#define VRT_MIN_WAVES 7
 #endif
 
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.

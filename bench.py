@@ -28,6 +28,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4). A part
+# stream that shares the null stream's queue loses its overlap (measured: C3 0.21 -> 0.35 ms per
+# frame, scripts/streams_exp.py with STREAMS_FRESH=1); with the RCCL and assembly streams of the
+# multi-GPU path there are more streams than 4 queues. Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 CONFIGS = {
     # name: (scene, N, W, H, R, T, description)
@@ -115,6 +120,8 @@ def main():
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # all host-issued work on a dedicated stream, never the null stream (see GPU_MAX_HW_QUEUES)
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

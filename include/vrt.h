@@ -128,6 +128,11 @@ const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
  * outside, capped at 32), to `out` (count >= (N+1)^3). Synchronous. */
 int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count);
 
+/* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
+ * pairs, out = n float3. Synchronous. */
+int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
+                        float randomness, float seed, float* out);
+
 /* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats
  * (alpha = 1, voxel.glsl:451) to the HOST buffer out_rgba. out_hit (W*H records) and stats may
  * be NULL. */

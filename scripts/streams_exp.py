@@ -18,8 +18,16 @@ import voxelraytracer_amd as vrt  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 
 
+_STREAMS = []
+
+
 def run(ren, cam, p, w, h, parts, frames, warmup):
-    streams = [torch.cuda.Stream() for _ in range(parts)]
+    if os.environ.get("STREAMS_FRESH"):   # a new set of streams per run (the old behaviour)
+        streams = [torch.cuda.Stream() for _ in range(parts)]
+    else:                                 # one set of streams for the whole process
+        while len(_STREAMS) < parts:
+            _STREAMS.append(torch.cuda.Stream())
+        streams = _STREAMS[:parts]
     rows = h // parts
     bufs = [torch.zeros((rows, w, 4), dtype=torch.uint8, device="cuda") for _ in range(parts)]
     main = torch.cuda.current_stream()

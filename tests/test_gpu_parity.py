@@ -189,3 +189,30 @@ def test_errors_are_reported(renderer):
         renderer.upload_atlas(np.zeros((48, 48, 4), np.uint8))   # not a power of two
     with pytest.raises(vrt.VrtError):
         renderer.upload_volume(np.zeros(27, np.uint8), 3)   # N must be a power of two
+
+
+def test_randomize_direction_bit_exact(renderer):
+    """The kernel's RandomizeDirection (vrt_debug_randomize) against the oracle, bit for bit:
+    random directions, directions with exact +0 / -0 components (where the hash decides the sign
+    of a zero at noise 0, voxel.glsl:132-140), at noise +0, -0 and > 0."""
+    rng = np.random.default_rng(11)
+    n = 512
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    z = np.float32(0.0)
+    nz = np.float32(-0.0)
+    d[0:64, 0] = nz
+    d[64:128, 1] = nz
+    d[128:192, 2] = z
+    d[192:256, 0] = nz
+    d[192:256, 2] = nz
+    d[256:272] = [z, nz, np.float32(1.0)]
+    p = (rng.uniform(-2, 130, size=(n, 3))).astype(np.float32)
+    for randomness, seed in [(0.0, 1.0), (-0.0, 3.0), (0.05, 7.0), (1.0, 2.0)]:
+        got = renderer.debug_randomize(d, p, randomness, seed)
+        ref = np.stack([oracle.randomize_direction(d[i], p[i], randomness, seed) for i in range(n)])
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), randomness
+    # at noise 0 the -0 components really do depend on the hash (both signs occur)
+    got = renderer.debug_randomize(d[:64], p[:64], 0.0, 1.0)
+    signs = np.signbit(got[:, 0])
+    assert signs.any() and (~signs).any()

@@ -274,3 +274,15 @@ class Renderer:
         a = np.ascontiguousarray(atlas, np.uint8)
         self._check(self._lib.vrt_upload_atlas(self._h, a.ctypes.data, a.shape[0]),
                     "vrt_upload_atlas")
+
+
+    def debug_randomize(self, dirs: np.ndarray, pos: np.ndarray, randomness: float,
+                        seed: float) -> np.ndarray:
+        """The kernel's RandomizeDirection on [n, 3] inputs (vrt_debug_randomize), for tests."""
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        p = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        out = np.empty_like(d)
+        self._check(self._lib.vrt_debug_randomize(self._h, d.ctypes.data, p.ctypes.data, len(d),
+                                                  randomness, seed, out.ctypes.data),
+                    "vrt_debug_randomize")
+        return out

@@ -128,6 +128,8 @@ SIGNATURES = {
     ),
     "vrt_history_reset": (C.c_int, [C.c_void_p]),
     "vrt_upload_atlas": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
+    "vrt_debug_randomize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_float,
+                                      C.c_float, C.c_void_p]),
     "vrt_terrain_noise": (C.c_int, [C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_build_scene": (C.c_int, [C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_camera_make": (
@@ -175,6 +177,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if name.startswith("vrt_debug_") and not hasattr(lib, name):
+            continue   # diagnostics may be absent from older A/B variant builds
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -99,12 +99,23 @@ __device__ __forceinline__ float random4(float x, float y, float z, float w) {
   return __uint_as_float((h & 0x007FFFFFu) | 0x3F800000u) - 1.0f;
 }
 // RandomizeDirection, voxel.glsl:132-140 (runs even at noise 0: it decides the sign of zeros)
+// With randomness == ±0 (every bench config) the added vector is (±0, ±0, ±0), and dir + r equals
+// dir bit for bit (x + ±0 = x for x != 0, +0 + ±0 = +0) unless a component is -0.0 (-0 + +0 = +0)
+// or NaN: only then do the hashes decide the result, so only then are they computed. Exact.
+__device__ __forceinline__ bool zero_noise_exact(f3 d) {
+  const uint32_t nz = 0x80000000u;
+  return int(__float_as_uint(d.x) != nz) & int(__float_as_uint(d.y) != nz) &
+         int(__float_as_uint(d.z) != nz) & int(d.x == d.x) & int(d.y == d.y) & int(d.z == d.z);
+}
 __device__ __forceinline__ f3 randomize(f3 dir, f3 pos, float randomness, float seed) {
-  const f3 p = mk((pos.x + dir.x) + seed, (pos.y + dir.y) + seed, (pos.z + dir.z) + seed);
-  const float dx = random4(p.x, p.y, p.z, 0.0f + seed);
-  const float dy = random4(p.x, p.y, p.z, 0.5f + seed);
-  const float dz = random4(p.x, p.y, p.z, 1.0f + seed);
-  const f3 r = mk((dx + -0.5f) * randomness, (dy + -0.5f) * randomness, (dz + -0.5f) * randomness);
+  f3 r = mk(0.0f, 0.0f, 0.0f);
+  if (!(randomness == 0.0f && zero_noise_exact(dir))) {
+    const f3 p = mk((pos.x + dir.x) + seed, (pos.y + dir.y) + seed, (pos.z + dir.z) + seed);
+    const float dx = random4(p.x, p.y, p.z, 0.0f + seed);
+    const float dy = random4(p.x, p.y, p.z, 0.5f + seed);
+    const float dz = random4(p.x, p.y, p.z, 1.0f + seed);
+    r = mk((dx + -0.5f) * randomness, (dy + -0.5f) * randomness, (dz + -0.5f) * randomness);
+  }
   return normalize3(dir + r);
 }
 
@@ -1040,6 +1051,20 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   }
 }
 
+// Diagnostic: RandomizeDirection for n (dir, pos) pairs (vrt_debug_randomize).
+__global__ void __launch_bounds__(64) randomize_kernel(const float* __restrict__ dir,
+                                                       const float* __restrict__ pos, int n,
+                                                       float randomness, float seed,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const f3 r = randomize(mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]),
+                         mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]), randomness, seed);
+  out[3 * i] = r.x;
+  out[3 * i + 1] = r.y;
+  out[3 * i + 2] = r.z;
+}
+
 // Sum the counter replicas into `dst` (accumulating) and zero them for the next render.
 __global__ void __launch_bounds__(64) reduce_counters_kernel(unsigned long long* __restrict__ rep,
                                                              unsigned long long* __restrict__ dst) {
@@ -1371,6 +1396,35 @@ int vrt_debug_stamps(uint64_t* out, uint64_t count) {
                                                                                      : VRT_ERR_DEVICE;
 }
 #endif
+
+int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
+                        float randomness, float seed, float* out) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!dir || !pos || !out || n < 0) return fail(ctx, VRT_ERR_INVALID, "null buffer or n < 0");
+  if (n == 0) return VRT_OK;
+  VRT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t bytes = size_t(n) * 3 * sizeof(float);
+  float *d_dir = nullptr, *d_pos = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_dir, bytes) != hipSuccess || hipMalloc(&d_pos, bytes) != hipSuccess ||
+      hipMalloc(&d_out, bytes) != hipSuccess) {
+    (void)hipFree(d_dir);
+    (void)hipFree(d_pos);
+    return fail(ctx, VRT_ERR_OOM, "hipMalloc");
+  }
+  hipError_t e = hipMemcpy(d_dir, dir, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_pos, pos, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(vrt::randomize_kernel, dim3((n + 63) / 64), dim3(64), 0, nullptr, d_dir,
+                       d_pos, n, randomness, seed, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(d_dir);
+  (void)hipFree(d_pos);
+  (void)hipFree(d_out);
+  if (e != hipSuccess) return hip_fail(ctx, e, "vrt_debug_randomize");
+  return VRT_OK;
+}
 
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
                           int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,

@@ -841,7 +841,13 @@ __device__ __forceinline__ uint32_t unorm8(float f) {
   const float c = __builtin_fminf(__builtin_fmaxf(f, 0.0f), 1.0f);
   return uint32_t(__builtin_rintf(c * 255.0f));
 }
-__device__ __forceinline__ float unorm8_read(uint32_t b) { return float(b) / 255.0f; }
+// b / 255 rounded correctly, as q0 = b * RN(1/255) plus one fma correction: equal to the IEEE
+// division for every byte (exhaustive check, tests/test_div255.py)
+__device__ __forceinline__ float unorm8_read(uint32_t b) {
+  const float a = float(b), y = 1.0f / 255.0f;
+  const float q0 = a * y;
+  return __builtin_fmaf(__builtin_fmaf(-255.0f, q0, a), y, q0);
+}
 __device__ __forceinline__ uint32_t pack_rgb8(float r, float g, float b) {
   return unorm8(r) | (unorm8(g) << 8) | (unorm8(b) << 16) | 0xFF000000u;
 }

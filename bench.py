@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--parts", type=int, default=2,
                     help="interleaved row parts per rank, each on its own HIP stream, so one "
                          "launch's tail overlaps the next part's launch (tiles.py)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
+                         "multi-rank rehearsal test)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: N ranks render an N-fold taller frame (each a config-sized band); "
                          "strong: the config's frame is split N ways")
@@ -118,12 +123,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if args.same_device:   # test rehearsal of the multi-rank path on a one-GPU box
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # all host-issued work on a dedicated stream, never the null stream (see GPU_MAX_HW_QUEUES)
     torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     scene, n, w, h, R, T, desc = CONFIGS[args.config]
     # weak: the framebuffer is H*N rows of the same view (N-fold vertical sample density), so every

@@ -1,0 +1,46 @@
+"""Rehearsal of bench.py's multi-rank path on a one-GPU box: torch.distributed.run with two ranks
+sharing cuda:0 over gloo (RCCL needs one GPU per rank; the driver's 8-GPU run uses it). Checks the
+JSON contract of rank 0's line for N = 2, weak scaling (the frame is 2 x 1080 rows), the gather of
+RGBA8 parts and the max-over-ranks timing — the code path the scaling runs take."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_bench_two_ranks_json(built, scaling):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           "--backend", "gloo", "--same-device", "--scaling", scaling, "--cpu-seconds", "0"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints exactly one JSON line
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
+              "cpu_baseline"):
+        assert k in out, k
+    assert out["n_gpus"] == 2 and out["steps"] == 6 and out["scaling"] == scaling
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert out["config"]["frame"].startswith("1920x2160" if scaling == "weak" else "1920x1080")
+    assert out["roofline"]["kernel_ms_max_over_ranks"] >= out["roofline"]["kernel_ms"]
+    assert out["cpu_baseline"] is None        # rank 0 at N=1 only

@@ -89,6 +89,12 @@ def test_parity_full_size_baseline_configs(renderer, scene, R, T):
     compare(rg, hg, st, ro, ho, co)
 
 
+def test_parity_full_size_c4(renderer):
+    """BASELINE.json configs[4] at full size: _TERRAIN 512^3, 3840x2160, (R,T)=(4,2)."""
+    (rg, hg, st), (ro, ho, co) = run_both(renderer, "terrain", 512, 3840, 2160, 4, 2)
+    compare(rg, hg, st, ro, ho, co)
+
+
 def test_row_bands_compose_to_full_frame(renderer):
     """Cyclic and contiguous row bands (the multi-GPU tiling) reproduce the full frame exactly."""
     import torch

@@ -240,10 +240,20 @@ def main():
         own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
         achieved = own_bytes / (frame_gpu_ms * 1e-3) / 1e9
         traffic = None
+        valu = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{args.output}.json")
-        if os.path.exists(pmc) and world == 1:
+        if os.path.exists(pmc) and world == 1 and args.shading == "color":
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pj = json.load(f)
+            traffic = pj.get("hbm_bytes_per_launch")
+            if pj.get("valu_insts_per_launch"):
+                # VALU-issue bound of the same frame: wave64 VALU ops take 2 cycles on a SIMD32;
+                # 1024 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+                floor_ms = pj["valu_insts_per_launch"] * 2 / (1024 * 2.4e9) * 1e3
+                valu = {"insts_per_frame": pj["valu_insts_per_launch"],
+                        "issue_bound_ms": round(floor_ms, 4),
+                        "frac": round(floor_ms / frame_gpu_ms, 4),
+                        "source": os.path.relpath(pmc, ROOT)}
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
             cam1 = vrt.make_camera(w, h)
@@ -296,6 +306,7 @@ def main():
                 "launches_per_frame": parts,
                 "launch_ms": round(launch_ms, 4),
                 "kernel_ms_max_over_ranks": round(frame_ms_max, 4),
+                "valu_issue": valu,
             },
             "cpu_baseline": cpu,
         }

@@ -119,6 +119,12 @@ int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol);
  * the volume to every GPU of the node), ordered on `hip_stream`; returns after the copy. */
 int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream);
 
+/* Build the _TERRAIN / _GLASS_CUBE / _REFRACTION volume of main.cpp:218-288 directly on the device
+ * (bytes identical to vrt_build_scene; only the n*n terrain heightfield is computed on the host)
+ * and make it the context's volume, ordered on `hip_stream`; returns after the build. N must be
+ * a power of two in [8, 1024]. Replaces the host build + glTexImage3D upload (main.cpp:315-318). */
+int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed, void* hip_stream);
+
 /* Device pointer of the resident volume (N^3 bytes, canonical layout), e.g. for a broadcast.
  * NULL if none. */
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);

@@ -50,3 +50,26 @@ def test_packed_volume_layout_and_distance(built, scene, n):
     assert np.array_equal(packed[:n, :n, n] & 0xFF, v[:, :, 0])
     assert np.all(packed[n] >> 8 == 0) and np.all(packed[:, n] >> 8 == 0)
     assert np.array_equal(packed[:n, :n, :n] >> 8, chebyshev_reference(vox, n))
+
+
+@pytest.mark.parametrize("scene", ["terrain", "glass_cube", "refraction"])
+@pytest.mark.parametrize("n", [16, 32, 64, 128])
+def test_device_scene_builder_matches_host(built, scene, n):
+    """vrt_build_scene_device (main.cpp:218-288 on the GPU) yields the same packed volume (voxel
+    bytes + distance field) as uploading vrt_build_scene's host bytes, and the same frame."""
+    with vrt.Renderer(0) as a, vrt.Renderer(0) as b:
+        a.upload_volume(vrt.build_scene(scene, n), n)
+        b.build_scene_device(scene, n)
+        assert np.array_equal(a.debug_packed_volume(), b.debug_packed_volume())
+        cam = vrt.make_camera(96, 54)
+        p = vrt.default_params(4, 2)
+        ra, _, _ = a.render(cam, p, want_hits=False)
+        rb, _, _ = b.render(cam, p, want_hits=False)
+        assert np.array_equal(ra.view(np.uint32), rb.view(np.uint32))
+
+
+def test_device_scene_builder_512_terrain(built):
+    with vrt.Renderer(0) as a, vrt.Renderer(0) as b:
+        a.upload_volume(vrt.build_scene("terrain", 512), 512)
+        b.build_scene_device("terrain", 512)
+        assert np.array_equal(a.debug_packed_volume(), b.debug_packed_volume())

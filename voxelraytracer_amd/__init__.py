@@ -286,3 +286,10 @@ class Renderer:
                                                   randomness, seed, out.ctypes.data),
                     "vrt_debug_randomize")
         return out
+
+
+    def build_scene_device(self, scene: str, n: int, seed: int = 0, stream: int = 0):
+        """Build a scene's volume on the device (vrt_build_scene_device) and make it current."""
+        self._check(self._lib.vrt_build_scene_device(self._h, SCENES[scene], n, seed,
+                                                     stream or None), "vrt_build_scene_device")
+        self.n = n

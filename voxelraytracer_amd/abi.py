@@ -97,6 +97,7 @@ SIGNATURES = {
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),
     "vrt_upload_volume_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
     "vrt_volume_device_ptr": (C.c_void_p, [C.c_void_p]),
+    "vrt_build_scene_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_debug_packed_volume": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "vrt_render": (
         C.c_int,

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "vrt.h"
 
@@ -1057,6 +1058,47 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   }
 }
 
+// Scene builders of main.cpp:218-288 on the device (vrt_build_scene_device): one work-item per
+// voxel applies the host builders' writes in their order (csrc/vrt_host.cpp vrt_build_scene);
+// `noise` is the n*n terrain heightfield (x + z*n), only read for _TERRAIN.
+__global__ void __launch_bounds__(256) build_scene_kernel(uint8_t* __restrict__ vox, int scene,
+                                                          uint32_t n, const float* __restrict__ noise) {
+  const uint64_t total = uint64_t(n) * n * n;
+  const float fs = float(n);
+  const uint32_t lo = n / 4, hi = 3 * n / 4, c = n / 2;
+  for (uint64_t idx = uint64_t(blockIdx.x) * 256 + threadIdx.x; idx < total;
+       idx += uint64_t(gridDim.x) * 256) {
+    const uint32_t x = uint32_t(idx % n), y = uint32_t((idx / n) % n), z = uint32_t(idx / (uint64_t(n) * n));
+    uint8_t v = 0;
+    if (scene == VRT_SCENE_TERRAIN) {  // main.cpp:219-257
+      const float h = noise[x + z * n] * fs;
+      if (float(int(y)) < h) v = 1;                     // stone column
+      if (int(y) == int(h)) v = 3;                      // grass cap
+      if (n <= 64) {                                    // glass walls (main.cpp:233)
+        if (x == 0 && z >= 2 && z < n - 2 && int(y) >= int(noise[z * n] * fs + 1.0f)) v = 2;
+        if (z == n - 4 && x >= 2 && x < n - 1 && int(y) >= int(noise[x * n + n - 4] * fs + 1.0f) &&
+            int(y) < int(n) - 4)
+          v = 2;
+      }
+      if (x == n - 1 && z >= 2 && z < n - 2 && int(y) >= int(noise[n - 1 + z * n] * fs + 1.0f) &&
+          int(y) < int(n) - 4)
+        v = 3;
+    } else if (scene == VRT_SCENE_GLASS_CUBE) {  // main.cpp:258-271
+      if (x == 0 || x == n - 1 || y == 0 || y == n - 1 || z == 0 || z == n - 1) v = 2;
+      if (x == c && y == c && z == c) v = 3;
+    } else {  // VRT_SCENE_REFRACTION, main.cpp:272-287
+      if (x == c && y == c && z == c) v = 2;
+      const bool in_yz = y >= lo && y < hi && z >= lo && z < hi;
+      const bool in_xy = x >= lo && x < hi && y >= lo && y < hi;
+      const bool in_xz = x >= lo && x < hi && z >= lo && z < hi;
+      if (((x == 0 || x == n - 1) && in_yz) || ((z == 0 || z == n - 1) && in_xy) ||
+          ((y == 0 || y == n - 1) && in_xz))
+        v = 3;
+    }
+    vox[idx] = v;
+  }
+}
+
 // Diagnostic: RandomizeDirection for n (dir, pos) pairs (vrt_debug_randomize).
 __global__ void __launch_bounds__(64) randomize_kernel(const float* __restrict__ dir,
                                                        const float* __restrict__ pos, int n,
@@ -1379,6 +1421,32 @@ int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, v
   const size_t bytes = size_t(n) * n * n;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   VRT_HIP(ctx, hipMemcpyAsync(ctx->d_vox, d_voxels, bytes, hipMemcpyDeviceToDevice, s));
+  return volume_finish(ctx, s);
+}
+
+int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (scene != VRT_SCENE_TERRAIN && scene != VRT_SCENE_GLASS_CUBE && scene != VRT_SCENE_REFRACTION)
+    return fail(ctx, VRT_ERR_INVALID, "unknown scene");
+  if (n < 8) return fail(ctx, VRT_ERR_INVALID, "scene edge must be >= 8");
+  const int st = volume_alloc(ctx, n);
+  if (st != VRT_OK) return st;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  std::vector<float> noise;
+  const float* d_noise = nullptr;
+  if (scene == VRT_SCENE_TERRAIN) {  // the heightfield (n*n floats) is built on the host
+    noise.resize(size_t(n) * n);
+    if (vrt_terrain_noise(n, seed, noise.data()) != VRT_OK) return fail(ctx, VRT_ERR_INVALID, "noise");
+    // d_tmp (2*N^3 bytes >= 4*N^2) is free until volume_finish's distance passes
+    VRT_HIP(ctx, hipMemcpyAsync(ctx->d_tmp, noise.data(), noise.size() * sizeof(float),
+                                hipMemcpyHostToDevice, s));
+    d_noise = reinterpret_cast<const float*>(ctx->d_tmp);
+  }
+  const uint64_t vol = uint64_t(n) * n * n;
+  const unsigned blocks = unsigned(std::min<uint64_t>((vol + 255) / 256, 16384));
+  hipLaunchKernelGGL(vrt::build_scene_kernel, dim3(blocks), dim3(256), 0, s, ctx->d_vox, scene,
+                     uint32_t(n), d_noise);
+  VRT_HIP(ctx, hipGetLastError());
   return volume_finish(ctx, s);
 }
 

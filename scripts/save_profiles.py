@@ -18,7 +18,7 @@ ap.add_argument("--config", default="C3")
 ap.add_argument("--output", default="rgba8")
 a = ap.parse_args()
 src = os.path.join(ROOT, "gpurun_out", a.tag)
-dst = os.path.join(ROOT, "profiles", f"r01_{a.tag}")
+dst = os.path.join(ROOT, "profiles", a.tag if a.tag.startswith("r01_") else f"r01_{a.tag}")
 os.makedirs(dst, exist_ok=True)
 for name in ("bench.log", "pytest_gpu.log", "smoke.log"):
     p = os.path.join(src, name)
@@ -43,7 +43,7 @@ if passes:
     s = json.loads(summ)
     if "fetch_bytes" in s and "write_bytes" in s:
         out = {"config": a.config, "output": a.output, "kernel": "vrt::render_kernel<false, false> (stats-free, colour-only)",
-               "source": f"profiles/r01_{a.tag}/pmc (rocprofv3 --pmc FETCH_SIZE and --pmc "
+               "source": f"profiles/{os.path.basename(dst)}/pmc (rocprofv3 --pmc FETCH_SIZE and --pmc "
                          "WRITE_SIZE in separate passes over bench.py --steps 5 --warmup 1 --parts 1: one launch = one frame)",
                "fetch_size_bytes_raw": s["fetch_bytes"], "write_size_bytes": s["write_bytes"],
                "correction": "gfx950: FETCH_SIZE reports half the bytes of 128-B requests "

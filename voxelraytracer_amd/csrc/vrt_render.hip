@@ -481,40 +481,46 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
   const float s_len = c.max_len - len0;
-  f3 t = w.t, cur = w.cur;
+  f3 t = w.t;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
   bool check = w.check_cube;
   int result;
+  constexpr uint32_t kOutside = 0x100u;
   for (;;) {
-    // loop-top tests of the reference, in its order: length, TestCube, then our step cap
-    if (!(len < c.max_len) || (check && !test_cube(cur, dir, c.fn))) {
+    // loop-top tests of the reference, in its order: length, TestCube, then our step cap.
+    // check is only set after an outside sample; currentPos is that step's (len unchanged since),
+    // recomputed with the same two ops rather than carried through the step loop
+    if (!(len < c.max_len)) {
       result = WALK_MISS;
       break;
+    }
+    if (check) {
+      const float sc = len - len0;
+      if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
+        result = WALK_MISS;
+        break;
+      }
     }
     if (it >= VRT_MAX_STEPS) {
       result = WALK_CAP;
       break;
     }
-    f3 tp;
-    // v_ev = the sampled byte, or kOutside for a sample outside the volume (which reads 0 but
-    // must stop the inner loop); pidx = its padded index. Both are written only by sampled
-    // steps: a skip window opens only after an in-volume empty sample, so during it they hold
-    // the values of an empty in-volume texel, exactly what a skipped step would read.
-    constexpr uint32_t kOutside = 0x100u;
-    uint32_t vi = 0, vj = 0, vk = 0, v_ev = 0u;
     const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
     const uint32_t it0 = it;
     uint32_t k = 0;
     // this lane's step count at its exit: set by the stopping (sampled) step; lanes that run
     // into the uniform bound leave with k == k_max. Keeps k from being copied to a VGPR per step.
     uint32_t k_exit = k_max;
+    // recorded by the stopping (sampled) step only; lanes that leave on the bound: no event
+    uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;  // x_out: sample was outside
+    int32_t x_vidx = -1;
     float s_lim = -1.0f;  // no skip window yet: the first step samples
     for (;;) {
       if (k >= k_max) break;  // wave-uniform step bound (scalar branch)
       ++k;
       const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
-      tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+      const f3 tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
       len += tmin;
       const float s = len - len0;
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
@@ -545,7 +551,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
 #ifdef VRT_DIAG_SAMPLED  // diagnostic build: the TIE3 counter counts sampled fast-path steps
         ++ties;
 #endif
-        cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+        const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
         const bool ex = tp.x == 0.0f;
         const f3 smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f),
                           cur.z + (ez ? hs.z : 0.0f));
@@ -553,14 +559,12 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
         const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
         const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
-        vi = cvt_flr(qx);
-        vj = cvt_flr(qy);
-        vk = cvt_flr(qz);
+        const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
         const uint32_t packed = load_u16(c.vox, pidx);
         const uint32_t v_raw = packed & 0xFFu;
         const uint32_t dist = packed >> 8;
-        v_ev = inb ? v_raw : kOutside;
+        const uint32_t v_ev = inb ? v_raw : kOutside;
         // exit parameter of the pulled-in box face per axis, ((v + c0) + sgn*fd - pos) * rcp,
         // as v*rcp + (fd*|rcp| + boff): only has to be conservative (error <~ 4e-4 |rcp| for
         // N <= 1024, against the 1/256 * |rcp| face margin), so it may contract
@@ -576,30 +580,31 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const bool stop = SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium);
         if (stop | !(len < c.max_len)) {
           k_exit = k;
-          asm volatile("" : "+v"(k_exit));
+          x_v = inb ? v_raw : 0u;  // outside samples read 0 (GetVoxel :151-152)
+          x_out = inb ? 0u : 1u;
+          x_axis = axis_index(mey, mez);
+          x_vidx = inb ? int32_t(canonical_index(c, vi, vj, vk)) : -1;
+          // integers in VGPRs: a bool carried out of a divergent loop costs SALU mask merges
+          asm volatile("" : "+v"(k_exit), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
           break;
         }
       }
     }
     it = it0 + k_exit;
-    asm volatile("" : "+v"(v_ev));  // decide here, from the VGPR (no per-step live-out masks)
-    const bool inb = v_ev != kOutside;
-    const uint32_t v = inb ? v_ev : 0u;  // outside samples read 0 (GetVoxel :151-152)
-    const bool event = SHADOW ? (v != 0u && v != 2u) : (v != medium);
-    if (event) {  // events only come from sampled steps, whose cur and texel are fresh
-      float ty = tp.y, tz = tp.z;
-      asm volatile("" : "+v"(ty), "+v"(tz));  // recompute here: no per-step live-out masks
-      axis_out = tz == 0.0f ? 2 : (ty == 0.0f ? 1 : 0);
-      vidx_out = inb ? canonical_index(c, vi, vj, vk) : -1;
-      v_out = v;
-      check = !inb;
+    const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
+    asm volatile("" : "+v"(x_out));
+    check = x_out != 0u;
+    if (event) {  // events only come from sampled steps
+      axis_out = int(x_axis);
+      vidx_out = x_vidx;
+      v_out = x_v;
       result = WALK_EVENT;
       break;
     }
-    check = !inb;  // not an event: evaluate the next iteration's loop-top tests
   }
+  const float s_end = len - len0;  // currentPos of the last step (the hit point on an event)
   w.t = t;
-  w.cur = cur;
+  w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
   w.len = len;
   w.it = it;
   w.ties = ties;
@@ -909,7 +914,7 @@ __device__ __forceinline__ uint32_t xcc_id() {
 constexpr int kCntReplicas = 256;
 
 #ifndef VRT_MIN_WAVES
-#define VRT_MIN_WAVES 7
+#define VRT_MIN_WAVES 8
 #endif
 
 // fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.

@@ -189,18 +189,30 @@ struct Ctx {
   float atlas_fs, atlas_fts;  // (float)u_AtlasSize, (float)u_AtlasTextureSize
 };
 
-// a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024)
+// a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024).
+// b is wave-uniform (the padded pitch) and goes in as the instruction's one SGPR operand.
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
-  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
   return r;
 }
 
 // 16-bit load at a 32-bit byte offset from a wave-uniform base: global_load_ushort with an SGPR
 // base (no 64-bit address arithmetic per lane)
 __device__ __forceinline__ uint32_t load_u16(const uint16_t* __restrict__ base, uint32_t idx) {
+#if VRT_U8_VOL
+  return reinterpret_cast<const uint8_t*>(base)[idx];
+#else
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(base) + (idx << 1));
+#endif
 }
+// texel fields of the packed word: voxel byte and capped distance D. Experiment VRT_U8_VOL: one
+// byte per texel, v | D << 2 (valid only for volumes whose bytes are all <= 3; A/B builds only)
+#ifndef VRT_U8_VOL
+#define VRT_U8_VOL 0
+#endif
+constexpr uint32_t kVoxMask = VRT_U8_VOL ? 0x3u : 0xFFu;
+constexpr uint32_t kDistShift = VRT_U8_VOL ? 2u : 8u;
 
 __device__ __forceinline__ int32_t canonical_index(const Ctx& c, uint32_t i, uint32_t j, uint32_t k) {
   const uint32_t n = uint32_t(c.n);
@@ -218,7 +230,7 @@ __device__ __forceinline__ uint32_t get_voxel(const Ctx& c, f3 p) {
   const uint32_t i = uint32_t(__builtin_floorf(p.x));
   const uint32_t j = uint32_t(__builtin_floorf(p.y));
   const uint32_t k = uint32_t(__builtin_floorf(p.z));
-  return load_u16(c.vox, mad24(mad24(k, c.p, j), c.p, i)) & 0xFFu;
+  return load_u16(c.vox, mad24(mad24(k, c.p, j), c.p, i)) & kVoxMask;
 }
 
 // TestCube (voxel.glsl:248-257) with centre N/2 and size N; bitwise ops, no short-circuit branches.
@@ -395,7 +407,7 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
       vj = cvt_flr(qy);
       vk = cvt_flr(qz);
       const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-      v_raw = load_u16(c.vox, pidx) & 0xFFu;
+      v_raw = load_u16(c.vox, pidx) & kVoxMask;
       if (ey & ez) ties++;  // intersectionAxis[3]: rare, a skipped branch otherwise
       // t update for the crossed axis (voxel.glsl:296/381), while the load is in flight
       const bool az = ez, ay = ey & !ez, ax = !ey & !ez;  // axis = ez ? 2 : ey ? 1 : 0
@@ -526,7 +538,6 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
 #ifndef VRT_DIAG_SAMPLED
       if (STATS) ties = add_if_both(ties, ey, ez);  // intersectionAxis[3] (counter/flag only)
-#endif
       // t update for the crossed axis (voxel.glsl:296/381)
       // crossed axis: z if ez (index 2, and 3 clamped), else y if ey, else x. Selected with the
       // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
@@ -547,6 +558,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float q = div_rn(num, da, ra) - s;
       t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
       asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
+#endif
       if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
 #ifdef VRT_DIAG_SAMPLED  // diagnostic build: the TIE3 counter counts sampled fast-path steps
         ++ties;
@@ -562,8 +574,8 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
         const uint32_t packed = load_u16(c.vox, pidx);
-        const uint32_t v_raw = packed & 0xFFu;
-        const uint32_t dist = packed >> 8;
+        const uint32_t v_raw = packed & kVoxMask;
+        const uint32_t dist = packed >> kDistShift;
         const uint32_t v_ev = inb ? v_raw : kOutside;
         // exit parameter of the pulled-in box face per axis, ((v + c0) + sgn*fd - pos) * rcp,
         // as v*rcp + (fd*|rcp| + boff): only has to be conservative (error <~ 4e-4 |rcp| for
@@ -885,11 +897,36 @@ static_assert(VRT_WG_WAVES == 1 || VRT_WG_WAVES == 2 || VRT_WG_WAVES == 4, "1, 2
 constexpr int kWgThreads = 64 * VRT_WG_WAVES;
 constexpr int kTileW = VRT_WG_WAVES >= 2 ? 16 : 8;
 constexpr int kTileH = VRT_WG_WAVES == 4 ? 16 : 8;
+// XCD-aware tile order: the dispatcher hands workgroup L (linear, row-major over the grid) to XCD
+// L % 8, so neighbouring tiles land on different XCDs and every XCD's L2 ends up holding the whole
+// visible volume. With VRT_XCD_CHUNK = C > 0, XCD x renders runs of C consecutive tiles instead
+// (tile T = ((L/8)/C*8 + L%8)*C + (L/8)%C: a bijection on the first floor(G/8C)*8C workgroups;
+// the remainder keeps L). 0 = dispatch order.
+#ifndef VRT_XCD_CHUNK
+#define VRT_XCD_CHUNK 0
+#endif
+#if VRT_XCD_CHUNK > 0
+__device__ __forceinline__ uint32_t tile_id() {
+  const uint32_t L = blockIdx.y * gridDim.x + blockIdx.x;
+  constexpr uint32_t C = VRT_XCD_CHUNK;
+  const uint32_t full = (gridDim.x * gridDim.y) / (8u * C) * (8u * C);
+  if (L < full) {
+    const uint32_t pos = L >> 3;
+    return ((pos / C) * 8u + (L & 7u)) * C + pos % C;
+  }
+  return L;
+}
+__device__ __forceinline__ int tile_x() { return int(tile_id() % gridDim.x); }
+__device__ __forceinline__ int tile_y() { return int(tile_id() / gridDim.x); }
+#else
+__device__ __forceinline__ int tile_x() { return int(blockIdx.x); }
+__device__ __forceinline__ int tile_y() { return int(blockIdx.y); }
+#endif
 __device__ __forceinline__ int pixel_x(int wave, uint32_t lane) {
-  return int(blockIdx.x) * kTileW + (wave & 1) * 8 + int(lane & 7u);
+  return tile_x() * kTileW + (wave & 1) * 8 + int(lane & 7u);
 }
 __device__ __forceinline__ int pixel_row(int wave, uint32_t lane) {
-  return int(blockIdx.y) * kTileH + (wave >> 1) * 8 + int(lane >> 3);
+  return tile_y() * kTileH + (wave >> 1) * 8 + int(lane >> 3);
 }
 
 #ifdef VRT_STAMPS
@@ -1173,7 +1210,11 @@ __global__ void __launch_bounds__(256) pack_volume_kernel(const uint8_t* __restr
     const bool edge = i == n || j == n || k == n;
     const uint32_t si = i == n ? 0u : i, sj = j == n ? 0u : j, sk = k == n ? 0u : k;
     const uint64_t sq = si + (uint64_t(sj) + uint64_t(sk) * n) * n;
+#if VRT_U8_VOL
+    reinterpret_cast<uint8_t*>(dst)[q] = uint8_t((src[sq] & 3u) | (edge ? 0u : uint32_t(dist[sq]) << 2));
+#else
     dst[q] = uint16_t(src[sq] | (edge ? 0u : uint32_t(dist[sq]) << 8));
+#endif
   }
 }
 

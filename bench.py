@@ -116,7 +116,7 @@ def main():
     import torch.distributed as dist
 
     import voxelraytracer_amd as vrt
-    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume
+    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume, row_pitch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -161,11 +161,16 @@ def main():
 
     def launch(row0, rows, step, out, prev, cnt_ptr=0):
         sp = torch.cuda.current_stream(dev).cuda_stream   # the part's stream (FrameTiler)
+        # a part may be a row-strided view into the frame (FrameTiler's single-rank mode)
+        pitch = row_pitch(out) if out.dim() == 3 else 0
         if rgba8:
+            assert prev.dim() != 3 or row_pitch(prev) == pitch, "one pitch for history and output"
             ren.render_temporal_rows_async(cam, params, args.alpha, row0, rows, step,
-                                           prev.data_ptr(), out.data_ptr(), 0, 0, cnt_ptr, sp)
+                                           prev.data_ptr(), out.data_ptr(), 0, 0, cnt_ptr, sp,
+                                           pitch=pitch)
         else:
-            ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sp)
+            ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sp,
+                                  pitch=pitch)
 
     def render_band(row0, rows, step, out, prev):
         e = None

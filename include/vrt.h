@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 3
+#define VRT_ABI_VERSION 4
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -131,7 +131,7 @@ const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
 
 /* Diagnostic: copy the kernel's device volume, (N+1)^3 u16 = voxel | D << 8 (x fastest; plane N
  * repeats plane 0 with D = 0; D = Chebyshev distance to the nearest non-empty voxel or the volume
- * outside, capped at 32), to `out` (count >= (N+1)^3). Synchronous. */
+ * outside, capped at 64), to `out` (count >= (N+1)^3). Synchronous. */
 int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
@@ -155,6 +155,14 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
                           int32_t row0, int32_t rows, int32_t row_step,
                           float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
                           void* hip_stream);
+
+/* Pitched form (ABI v4): output row i starts i*pitch pixels after d_out_rgba (pitch >= width),
+ * so a band can be written straight into its rows of a whole frame: d_out = frame + row0*width,
+ * pitch = row_step*width. vrt_render_rows_async is this with pitch = width. */
+int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
+                                  int32_t row0, int32_t rows, int32_t row_step, int64_t pitch,
+                                  float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                  void* hip_stream);
 
 /* ---- textured mode (voxel.glsl without _COLOR_ONLY) --------------------- */
 /* With vrt_params.color_only = 0 the kernel shades with the textured material table
@@ -186,6 +194,17 @@ int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vr
                                    const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
                                    uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
                                    void* hip_stream);
+
+/* Pitched form (ABI v4): row i of d_prev_rgba8, d_cur_rgba8, d_raw_rgba8 and d_out_hit starts
+ * i*pitch pixels after the pointer (pitch >= width). With d_prev = d_cur = frame + row0*width and
+ * pitch = row_step*width a band filters its rows of one full-frame history in place — the
+ * single-GPU frame loop needs no per-band buffers and no assembly copy. */
+int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
+                                           const vrt_params* params, float alpha, int32_t row0,
+                                           int32_t rows, int32_t row_step, int64_t pitch,
+                                           const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
+                                           uint64_t* d_counters, void* hip_stream);
 
 /* Synchronous frame loop of main.cpp:323-393 with the two history FBOs and the ray-trace FBO kept
  * in the context: render, filter against the last filtered frame, copy the new filtered frame to

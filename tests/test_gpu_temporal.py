@@ -133,3 +133,33 @@ def test_temporal_errors(renderer):
         renderer.render_temporal_rows_async(cam, p, 1.0, 0, 8, 1, 0, d.data_ptr())
     with pytest.raises(vrt.VrtError):
         renderer.render_temporal_rows_async(cam, p, 1.0, 4, 8, 1, d.data_ptr(), d.data_ptr())
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_pitched_bands_write_the_frame_in_place(renderer, k):
+    """ABI v4 pitched forms: band r (rows r, r+k, ...) written through pitch = k*W straight into
+    a full frame, filtered in place against the same rows, equals the whole-frame render; the
+    float form likewise; a pitch below the width is rejected."""
+    w, h = 96, 72
+    _, cam, p = scene(renderer, "refraction", 32, w, h, 4, 4, ray_noise=0.02, time=3.0)
+    rng = np.random.default_rng(k)
+    prev = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+    ref = torch.from_numpy(prev).cuda()
+    renderer.render_temporal_rows_async(cam, p, 0.6, 0, h, 1, ref.data_ptr(), ref.data_ptr())
+    frame = torch.from_numpy(prev).cuda()
+    raw = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
+    for r in range(k):
+        renderer.render_temporal_rows_async(cam, p, 0.6, r, h // k, k, frame[r].data_ptr(),
+                                            frame[r].data_ptr(), raw[r].data_ptr(), pitch=k * w)
+    fref = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    renderer.render_rows_async(cam, p, 0, h, 1, fref.data_ptr())
+    fpart = torch.full((h, w, 4), -1.0, dtype=torch.float32, device="cuda")
+    for r in range(k):
+        renderer.render_rows_async(cam, p, r, h // k, k, fpart[r].data_ptr(), pitch=k * w)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy(), ref.cpu().numpy())
+    assert np.all(raw.cpu().numpy()[..., 3] == 255)   # every raw row was written too
+    assert np.array_equal(fpart.cpu().numpy(), fref.cpu().numpy())
+    with pytest.raises(vrt.VrtError):
+        renderer.render_temporal_rows_async(cam, p, 1.0, 0, h, 1, frame.data_ptr(),
+                                            frame.data_ptr(), pitch=w - 1)

@@ -37,7 +37,7 @@ def worker(rank, world, port, q, parts):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import voxelraytracer_amd as vrt
-    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume
+    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume, row_pitch
 
     dev = torch.device("cuda", 0)
     vox = torch.from_numpy(vrt.build_scene("terrain", N)).to(dev) if rank == 0 else \
@@ -51,7 +51,8 @@ def worker(rank, world, port, q, parts):
     def render_band(row0, rows, step, out, prev):
         ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"] // parts), ALPHA, row0,
                                        rows, step, prev.data_ptr(), out.data_ptr(),
-                                       stream=torch.cuda.current_stream().cuda_stream)
+                                       stream=torch.cuda.current_stream().cuda_stream,
+                                       pitch=row_pitch(out))
         state["t"] += 1
 
     tiler = FrameTiler(W, H, render_band, dev, dtype=torch.uint8, parts=parts)
@@ -99,10 +100,11 @@ def test_two_ranks_on_one_gpu_match_single_process(built, parts):
 
 
 def test_single_rank_two_streams_match(built):
-    """One rank, two interleaved parts on two HIP streams (the bench default): each frame
+    """One rank, two interleaved parts on two HIP streams (the bench default): each part renders
+    into its rows of the frame through the row pitch and filters them in place; each frame
     returned by the tiler equals the single-stream filtered frame."""
     import voxelraytracer_amd as vrt
-    from voxelraytracer_amd.tiles import FrameTiler
+    from voxelraytracer_amd.tiles import FrameTiler, row_pitch
 
     with vrt.Renderer(0) as ren:
         ren.upload_volume(vrt.build_scene("terrain", N), N)
@@ -112,7 +114,8 @@ def test_single_rank_two_streams_match(built):
         def render_band(row0, rows, step, out, prev):
             ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"] // 2), ALPHA, row0,
                                            rows, step, prev.data_ptr(), out.data_ptr(),
-                                           stream=torch.cuda.current_stream().cuda_stream)
+                                           stream=torch.cuda.current_stream().cuda_stream,
+                                           pitch=row_pitch(out))
             state["t"] += 1
 
         tiler = FrameTiler(W, H, render_band, torch.device("cuda", 0), dtype=torch.uint8, parts=2)

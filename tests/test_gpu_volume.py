@@ -8,7 +8,7 @@ import pytest
 import voxelraytracer_amd as vrt
 
 pytestmark = pytest.mark.gpu
-CAP = 32
+CAP = 64  # kDistCap (VRT_DIST_CAP) of csrc/vrt_render.hip
 
 
 def chebyshev_reference(vox, n):

@@ -231,8 +231,18 @@ class Renderer:
         return rgba, hits, stats
 
     def render_rows_async(self, cam: Camera, params: Params, row0: int, rows: int, row_step: int,
-                          d_out: int, d_hit: int = 0, d_counters: int = 0, stream: int = 0):
-        """Band render into device pointers (e.g. torch tensors' data_ptr()) on a HIP stream."""
+                          d_out: int, d_hit: int = 0, d_counters: int = 0, stream: int = 0,
+                          pitch: int = 0):
+        """Band render into device pointers (e.g. torch tensors' data_ptr()) on a HIP stream.
+        pitch: pixels from one band row to the next (0 = width: a compact band buffer)."""
+        if pitch:
+            self._check(
+                self._lib.vrt_render_rows_pitched_async(
+                    self._h, C.byref(cam), C.byref(params), row0, rows, row_step, pitch, d_out,
+                    d_hit or None, d_counters or None, stream or None),
+                "vrt_render_rows_pitched_async",
+            )
+            return
         self._check(
             self._lib.vrt_render_rows_async(self._h, C.byref(cam), C.byref(params), row0, rows,
                                             row_step, d_out, d_hit or None, d_counters or None,
@@ -243,9 +253,19 @@ class Renderer:
     def render_temporal_rows_async(self, cam: Camera, params: Params, alpha: float, row0: int,
                                    rows: int, row_step: int, d_prev: int, d_cur: int,
                                    d_raw: int = 0, d_hit: int = 0, d_counters: int = 0,
-                                   stream: int = 0):
+                                   stream: int = 0, pitch: int = 0):
         """Band render with the fused temporal filter + RGB8 store (vrt_render_temporal_rows_async)
-        into device RGBA8 buffers (e.g. torch uint8 [rows, W, 4] tensors' data_ptr())."""
+        into device RGBA8 buffers (e.g. torch uint8 [rows, W, 4] tensors' data_ptr()). pitch:
+        pixels from one band row to the next in every buffer (0 = width)."""
+        if pitch:
+            self._check(
+                self._lib.vrt_render_temporal_rows_pitched_async(
+                    self._h, C.byref(cam), C.byref(params), alpha, row0, rows, row_step, pitch,
+                    d_prev, d_cur, d_raw or None, d_hit or None, d_counters or None,
+                    stream or None),
+                "vrt_render_temporal_rows_pitched_async",
+            )
+            return
         self._check(
             self._lib.vrt_render_temporal_rows_async(
                 self._h, C.byref(cam), C.byref(params), alpha, row0, rows, row_step, d_prev, d_cur,

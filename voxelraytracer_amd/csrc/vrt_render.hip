@@ -34,6 +34,7 @@ struct KArgs {
   float fn;
   int32_t n, width, height;
   int32_t row0, rows, row_step;
+  int32_t pitch;  // pixels from one band row to the next in every output/history buffer (>= width)
   int32_t max_refl, max_transp;
   // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom
   int32_t textured, atlas_size, atlas_tex_size;
@@ -324,6 +325,15 @@ __device__ __forceinline__ uint32_t axis_index(unsigned long long mey, unsigned 
   return r;
 }
 
+#ifdef VRT_DIAG_WAVE
+// diagnostic builds only: true on the lowest active lane (one count per wave and event)
+__device__ __forceinline__ bool diag_leader() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return (__builtin_amdgcn_ballot_w64(true) & ((1ull << l) - 1ull)) == 0ull;
+}
+#endif
+
 // m's lane bit ? if_set : if_clear, as one v_cndmask on an SGPR lane mask
 __device__ __forceinline__ float sel_mask(unsigned long long m, float if_set, float if_clear) {
   float r;
@@ -462,7 +472,11 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 // inside the volume — no event, no TestCube — and needs only the exact DDA state update; the
 // sample, its address and the load are skipped. Every float op that defines the walk's state is
 // still executed, in the reference's order, so the walk is bit-identical.
-constexpr uint32_t kDistCap = 32;
+#ifndef VRT_DIST_CAP
+#define VRT_DIST_CAP 64
+#endif
+constexpr uint32_t kDistCap = VRT_DIST_CAP;
+static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
 template <bool SHADOW, bool STATS>
@@ -536,8 +550,11 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       len += tmin;
       const float s = len - len0;
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
-#ifndef VRT_DIAG_SAMPLED
+#if !defined(VRT_DIAG_SAMPLED) && !defined(VRT_DIAG_WAVE)
       if (STATS) ties = add_if_both(ties, ey, ez);  // intersectionAxis[3] (counter/flag only)
+#elif defined(VRT_DIAG_WAVE) && VRT_DIAG_WAVE == 1  // diagnostic: TIE3 counts wave-level steps
+      ties += diag_leader() ? 1u : 0u;
+#endif
       // t update for the crossed axis (voxel.glsl:296/381)
       // crossed axis: z if ez (index 2, and 3 clamped), else y if ey, else x. Selected with the
       // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
@@ -558,10 +575,11 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float q = div_rn(num, da, ra) - s;
       t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
       asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
-#endif
       if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
 #ifdef VRT_DIAG_SAMPLED  // diagnostic build: the TIE3 counter counts sampled fast-path steps
         ++ties;
+#elif defined(VRT_DIAG_WAVE) && VRT_DIAG_WAVE == 2  // diagnostic: wave-level sampled branches
+        ties += diag_leader() ? 1u : 0u;
 #endif
         const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
         const bool ex = tp.x == 0.0f;
@@ -1059,7 +1077,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       }
     }
     const uint32_t l2 = lane_id();
-    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.width) + size_t(pixel_x(wave, l2));
+    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
     if (a.cur) {  // fused reference post-pass: RGB8 ray-trace store, temporal blend, RGB8 store
       const uint32_t rw = pack_rgb8(color.x, color.y, color.z);
       if (a.raw) a.raw[o] = rw;
@@ -1324,6 +1342,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.row0 = row0;
   a.rows = rows;
   a.row_step = row_step;
+  a.pitch = cam->width;
   a.max_refl = p->max_reflections;
   a.max_transp = p->max_transparencies;
   a.textured = p->color_only ? 0 : 1;
@@ -1546,20 +1565,64 @@ int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_
   return VRT_OK;
 }
 
-int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
-                          int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,
-                          uint64_t* d_counters, void* hip_stream) {
+// Band arguments shared by the async entry points: rows inside the image, pitch >= width.
+static int check_band(vrt_ctx* ctx, const vrt_camera* cam, int32_t row0, int32_t rows,
+                      int32_t row_step, int64_t pitch) {
+  if (rows < 0 || row_step < 1 || row0 < 0 ||
+      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
+    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
+  if (pitch < cam->width || pitch > INT32_MAX)
+    return fail(ctx, VRT_ERR_INVALID, "row pitch must be >= the image width");
+  return VRT_OK;
+}
+
+int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
+                                  int32_t row0, int32_t rows, int32_t row_step, int64_t pitch,
+                                  float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                  void* hip_stream) {
   if (!ctx) return VRT_ERR_INVALID;
   int st = check_render_args(ctx, cam, p);
   if (st != VRT_OK) return st;
   if (!d_out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
-  if (rows < 0 || row_step < 1 || row0 < 0 ||
-      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
-    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
   if (rows == 0) return VRT_OK;
-  const vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
+  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
+  a.pitch = int32_t(pitch);
   launch(ctx, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
          reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                          int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,
+                          uint64_t* d_counters, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
+  return vrt_render_rows_pitched_async(ctx, cam, p, row0, rows, row_step, cam->width, d_out_rgba,
+                                       d_out_hit, d_counters, hip_stream);
+}
+
+int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
+                                           const vrt_params* p, float alpha, int32_t row0,
+                                           int32_t rows, int32_t row_step, int64_t pitch,
+                                           const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
+                                           uint64_t* d_counters, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
+  if (rows == 0) return VRT_OK;
+  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
+  a.pitch = int32_t(pitch);
+  a.alpha = alpha;
+  a.prev = d_prev_rgba8;
+  a.cur = d_cur_rgba8;
+  a.raw = d_raw_rgba8;
+  launch(ctx, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
+         static_cast<hipStream_t>(hip_stream));
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
 }
@@ -1570,22 +1633,10 @@ int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vr
                                    uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
                                    void* hip_stream) {
   if (!ctx) return VRT_ERR_INVALID;
-  int st = check_render_args(ctx, cam, p);
-  if (st != VRT_OK) return st;
-  if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
-  if (rows < 0 || row_step < 1 || row0 < 0 ||
-      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
-    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
-  if (rows == 0) return VRT_OK;
-  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
-  a.alpha = alpha;
-  a.prev = d_prev_rgba8;
-  a.cur = d_cur_rgba8;
-  a.raw = d_raw_rgba8;
-  launch(ctx, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
-         static_cast<hipStream_t>(hip_stream));
-  VRT_HIP(ctx, hipGetLastError());
-  return VRT_OK;
+  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
+  return vrt_render_temporal_rows_pitched_async(ctx, cam, p, alpha, row0, rows, row_step,
+                                                cam->width, d_prev_rgba8, d_cur_rgba8, d_raw_rgba8,
+                                                d_out_hit, d_counters, hip_stream);
 }
 
 int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,

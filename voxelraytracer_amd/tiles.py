@@ -15,6 +15,11 @@ frame with P = 2, scripts/streams_exp.py). Ordering uses events only: a part str
 gather that last read its buffer, the gather waits for every part of its frame — a part never
 waits for another part, so the overlap is real.
 
+With one rank and P > 1 parts, every part renders straight into its rows of the frame buffer
+(a row-strided view; the renderer's row pitch, ABI v4) and filters them in place against the same
+rows, which hold the previous frame: no band buffers, no assembly copy (it cost ≈4 % of a C3
+frame as two strided copy kernels per frame).
+
 FrameTiler double-buffers the band (N > 1) so that the gather of frame k overlaps the render of
 frame k+1. Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8 store
 (the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire instead of 16.
@@ -66,6 +71,14 @@ def assemble_parts(gathered: torch.Tensor, out: Optional[torch.Tensor] = None) -
     return out
 
 
+def row_pitch(t: torch.Tensor) -> int:
+    """Pixels from one row to the next of a [rows, W, C] band tensor that render_band receives
+    (it may be a row-strided view into the frame): the renderer's `pitch` argument."""
+    if t.dim() != 3 or t.stride(2) != 1 or t.stride(1) != t.shape[2]:
+        raise ValueError("band tensors are [rows, W, C] with contiguous pixels")
+    return t.stride(0) // t.stride(1)
+
+
 def broadcast_volume(vox: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
     """Replicate the N^3 volume (uint8 tensor on this rank's device) from `src` to every rank."""
     if dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -77,11 +90,12 @@ class FrameTiler:
     """Renders a sequence of frames across `world` ranks, `parts` streams per rank.
 
     render_band(row0, rows, row_step, out, prev) must enqueue the render of one part into `out`
-    ([rows, W, channels] of `dtype` on `device`) on the CURRENT stream (the HIP kernel through the
-    C-ABI, or the oracle in CPU tests); `prev` holds that part's rows of the previous frame (the
-    temporal history; zeros before the first frame; it is `out` itself with one buffer).
+    ([rows, W, channels] of `dtype` on `device`; possibly a row-strided view, see row_pitch) on
+    the CURRENT stream (the HIP kernel through the C-ABI, or the oracle in CPU tests); `prev` holds
+    that part's rows of the previous frame (the temporal history; zeros before the first frame;
+    it is `out` itself with one buffer: each pixel is read before it is written).
     frame() renders the next frame; with one rank it returns that frame (for parts > 1 each part
-    copies its rows into it on its own stream); with several ranks the gather is issued
+    renders into its rows of it directly, in place); with several ranks the gather is issued
     asynchronously and rank 0 returns the PREVIOUS frame, assembled on `self.assembly_stream`
     (None on the first call and on other ranks), so the gather of frame k overlaps the render of
     frame k+1. finish() drains the pipeline and returns the last frame on rank 0. A returned
@@ -101,13 +115,19 @@ class FrameTiler:
         self.cuda = torch.device(device).type == "cuda"
         shape = (parts, self.rows_p, width, channels)
         nbuf = 2 if self.world > 1 else 1
-        self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        # one rank, several parts: the parts render into (and filter in place) the frame itself
+        self.direct = self.world == 1 and parts > 1
+        self.frame_buf = None
+        if self.direct:
+            self.frame_buf = torch.zeros((height, width, channels), dtype=dtype, device=device)
+            self.bands = [self.frame_buf.view(shape)]   # same storage (bench's counted launch)
+        else:
+            self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
         self.part_streams = ([torch.cuda.Stream(device=device) for _ in range(parts)]
                              if self.cuda and parts > 1 else None)
         self.assembly_stream = None
         self.gathered = None
-        self.frame_buf = None
-        if self.rank == 0 and (self.world > 1 or parts > 1):
+        if self.rank == 0 and self.world > 1:
             self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
         if self.rank == 0 and self.world > 1:
             self.gathered = [torch.empty((self.world,) + shape, dtype=dtype, device=device)
@@ -120,17 +140,22 @@ class FrameTiler:
         self.k = 0
 
     # ---- helpers ---------------------------------------------------------------------------
-    def _render_parts(self, band: torch.Tensor, prev: torch.Tensor, wait_work, assemble: bool):
-        """Enqueue every part (each waits for `wait_work`, the gather that last read its buffer;
-        with one rank and several parts each part then copies its rows into frame_buf on its own
-        stream). Returns the events that mark the parts' completion (CUDA, parts > 1)."""
+    def _part_buffers(self, s: int, band: torch.Tensor, prev: torch.Tensor):
+        """(out, prev) of part s: its rows of the frame (in place) in direct mode, else its slot
+        of the band buffers."""
+        if self.direct:
+            rows = self._frame_rows(s)
+            return rows, rows
+        return band[s], prev[s]
+
+    def _render_parts(self, band: torch.Tensor, prev: torch.Tensor, wait_work):
+        """Enqueue every part (each waits for `wait_work`, the gather that last read its buffer).
+        Returns the events that mark the parts' completion (CUDA, parts > 1)."""
         if self.part_streams is None:
             if wait_work is not None:
                 wait_work.wait()
             for s, (row0, rows, step) in enumerate(self.specs):
-                self.render_band(row0, rows, step, band[s], prev[s])
-                if assemble:
-                    self._frame_rows(s).copy_(band[s])
+                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
             return None
         events = []
         for s, (row0, rows, step) in enumerate(self.specs):
@@ -138,9 +163,7 @@ class FrameTiler:
             with torch.cuda.stream(st):
                 if wait_work is not None:
                     wait_work.wait()
-                self.render_band(row0, rows, step, band[s], prev[s])
-                if assemble:
-                    self._frame_rows(s).copy_(band[s])
+                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
                 events.append(st.record_event())
         return events
 
@@ -156,10 +179,10 @@ class FrameTiler:
         self.k += 1
         band = self.bands[b]
         if self.world == 1:
-            self._render_parts(band, prev, None, assemble=self.parts > 1)
+            self._render_parts(band, prev, None)
             return band[0] if self.parts == 1 else self.frame_buf
         wait_work, self.pending[b] = self.pending[b], None
-        events = self._render_parts(band, prev, wait_work, assemble=False)
+        events = self._render_parts(band, prev, wait_work)
         cur = torch.cuda.current_stream() if self.cuda else None
         if events is not None:   # the gather (issued from the current stream) needs every part
             for e in events:

@@ -173,6 +173,11 @@ struct Counters {
 #ifndef VRT_LDS_AXIS
 #define VRT_LDS_AXIS 1
 #endif
+// The LDS entry address selected from three per-lane addresses (2 VALU, 2 more
+// VGPRs) instead of index + shift-add (3 VALU).
+#ifndef VRT_AX_ADDR_SEL
+#define VRT_AX_ADDR_SEL 1
+#endif
 
 struct Ctx {
   const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | D << 8 (see pack kernel)
@@ -341,6 +346,25 @@ __device__ __forceinline__ float sel_mask(unsigned long long m, float if_set, fl
   return r;
 }
 
+// m's lane bit ? if_set : if_clear on 32-bit integers (one v_cndmask)
+__device__ __forceinline__ uint32_t sel_mask_u(unsigned long long m, uint32_t if_set, uint32_t if_clear) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+}
+
+// LDS loads through a 32-bit LDS byte address
+typedef __attribute__((address_space(3))) const float4 lds_float4;
+__device__ __forceinline__ uint32_t lds_addr(const float4* p) {
+  return uint32_t(reinterpret_cast<size_t>((lds_float4*)p));
+}
+__device__ __forceinline__ float4 lds_load(uint32_t addr) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const v4f lds_v4f;
+  const v4f r = *(lds_v4f*)(size_t)addr;
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+
 // keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
@@ -496,6 +520,10 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
   c.ax[1] = make_float4(pos.y, dir.y, rcp.y, step.y);
   c.ax[2] = make_float4(pos.z, dir.z, rcp.z, step.z);
+#if VRT_AX_ADDR_SEL
+  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u, ax_a2 = ax_a0 + 32u;
+  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));  // three VGPRs, not re-derived
+#endif
 #else
   f3 dv = dir, rv = rcp;
   if (SHADOW) {
@@ -560,7 +588,11 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
       const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
       const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
-#if VRT_LDS_AXIS
+#if VRT_LDS_AXIS && VRT_AX_ADDR_SEL
+      // the crossed axis' entry address straight from the masks: two v_cndmask, no index math
+      const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+      const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
+#elif VRT_LDS_AXIS
       const uint32_t ai = axis_index(mey, mez);
       const float4 ae = c.ax[ai];
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 4
+#define VRT_ABI_VERSION 5
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -129,10 +129,23 @@ int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed
  * NULL if none. */
 const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx);
 
-/* Diagnostic: copy the kernel's device volume, (N+1)^3 u16 = voxel | D << 8 (x fastest; plane N
- * repeats plane 0 with D = 0; D = Chebyshev distance to the nearest non-empty voxel or the volume
- * outside, capped at 64), to `out` (count >= (N+1)^3). Synchronous. */
+/* Diagnostic: copy the kernel's device volume to `out` (count >= octants x (N+1)^3, see
+ * vrt_volume_octants): per octant o (bit 0: dir.x < 0, bit 1: dir.y < 0, bit 2: dir.z < 0), a padded
+ * (N+1)^3 u16 volume = voxel | G << 8 (x fastest; plane N repeats plane 0 with G = 0). Octant
+ * layout (N <= 512): G(v) = F(v - s) - 1, F(u) = edge of the largest empty in-volume cube anchored
+ * at u extending along s = the octant's step (capped at 64). Single layout (N = 1024): G = the
+ * Chebyshev distance to the nearest non-empty voxel or the volume outside, capped at 64.
+ * Synchronous. */
 int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count);
+
+/* ABI v5: number of packed volumes of the resident volume (8 octant volumes, or 1 for N = 1024;
+ * 0 when none is uploaded). */
+int vrt_volume_octants(const vrt_ctx* ctx);
+
+/* ABI v5: skip-distance layout of the NEXT volume upload: 0 = automatic (8 octant volumes for
+ * N <= 512, else 1), 1 = one volume with the centred Chebyshev distance (the N = 1024 layout, at
+ * any N: tests and A/B timing), 8 = octant volumes where they fit. Images are identical. */
+int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
  * pairs, out = n float3. Synchronous. */

@@ -205,12 +205,18 @@ class Renderer:
         self.n = n
 
     def debug_packed_volume(self) -> np.ndarray:
-        """The kernel's device volume ((N+1)^3 u16 voxel | D << 8), for tests."""
+        """The kernel's device volumes [octant][z][y][x] ((N+1)^3 u16 voxel | G << 8 each; 8
+        octant volumes, or 1 for N = 1024), for tests."""
         p = self.n + 1
-        out = np.empty(p ** 3, np.uint16)
+        k = self._lib.vrt_volume_octants(self._h)
+        out = np.empty(k * p ** 3, np.uint16)
         self._check(self._lib.vrt_debug_packed_volume(self._h, out.ctypes.data, out.size),
                     "vrt_debug_packed_volume")
-        return out.reshape(p, p, p)
+        return out.reshape(k, p, p, p)
+
+    def set_skip_layout(self, octants: int):
+        """Skip-distance layout of the next upload: 0 auto, 1 centred single volume, 8 octants."""
+        self._check(self._lib.vrt_set_skip_layout(self._h, octants), "vrt_set_skip_layout")
 
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0

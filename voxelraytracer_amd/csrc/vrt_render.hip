@@ -35,6 +35,7 @@ struct KArgs {
   int32_t n, width, height;
   int32_t row0, rows, row_step;
   int32_t pitch;  // pixels from one band row to the next in every output/history buffer (>= width)
+  uint32_t ostride;  // bytes from one direction octant's packed volume to the next (0: one volume)
   int32_t max_refl, max_transp;
   // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom
   int32_t textured, atlas_size, atlas_tex_size;
@@ -180,7 +181,8 @@ struct Counters {
 #endif
 
 struct Ctx {
-  const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | D << 8 (see pack kernel)
+  const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | G << 8, one per octant (see pack kernels)
+  uint32_t ostride;  // bytes between the octant volumes (0: a single centred-distance volume)
   int32_t n;
   uint32_t p;  // N + 1
   float fn;
@@ -206,19 +208,18 @@ __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
 // 16-bit load at a 32-bit byte offset from a wave-uniform base: global_load_ushort with an SGPR
 // base (no 64-bit address arithmetic per lane)
 __device__ __forceinline__ uint32_t load_u16(const uint16_t* __restrict__ base, uint32_t idx) {
-#if VRT_U8_VOL
-  return reinterpret_cast<const uint8_t*>(base)[idx];
-#else
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(base) + (idx << 1));
-#endif
 }
-// texel fields of the packed word: voxel byte and capped distance D. Experiment VRT_U8_VOL: one
-// byte per texel, v | D << 2 (valid only for volumes whose bytes are all <= 3; A/B builds only)
-#ifndef VRT_U8_VOL
-#define VRT_U8_VOL 0
-#endif
-constexpr uint32_t kVoxMask = VRT_U8_VOL ? 0x3u : 0xFFu;
-constexpr uint32_t kDistShift = VRT_U8_VOL ? 2u : 8u;
+// the same texel in the volume of the ray's direction octant, `obase` bytes after the first one:
+// the byte offset (idx << 1) + obase is one v_lshl_add_u32, as the plain shift was
+__device__ __forceinline__ uint32_t load_u16_at(const uint16_t* __restrict__ base, uint32_t idx,
+                                                uint32_t obase) {
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(base) + ((idx << 1) + obase));
+}
+// texel fields of the packed word: voxel byte and the skip distance (forward distance G of the
+// octant, or the centred Chebyshev D of the single-volume layout; see the skip walk)
+constexpr uint32_t kVoxMask = 0xFFu;
+constexpr uint32_t kDistShift = 8u;
 
 __device__ __forceinline__ int32_t canonical_index(const Ctx& c, uint32_t i, uint32_t j, uint32_t k) {
   const uint32_t n = uint32_t(c.n);
@@ -487,12 +488,26 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 
 // ---------------------------------------------------------------- empty-space step skipping --
 //
-// The packed volume carries, per voxel v, D(v) = the Chebyshev distance (in voxels, capped at
-// kDistCap) to the nearest non-empty voxel or to the outside of the volume, so every voxel of the
-// box [v-D+1, v+D-1]^3 is empty and inside. After a sampled step whose texel is empty with D >= 2,
-// an air ray (or a shadow ray) computes s_lim, the ray parameter up to which its position provably
-// stays inside that box on every axis (box faces v+D and v+1-D pulled in by kSkipMargin, far above
-// the float error of cur = pos + s*dir). A step with s < s_lim therefore samples an empty voxel
+// The packed volume carries, per voxel v, a skip distance G(v) such that every voxel of a box
+// B(v) is empty and inside the volume, where B(v) reaches G voxels ahead of v along the ray's
+// direction on every axis (faces (v + c0) + sgn*G, c0 = 0 / 1 for d > 0 / < 0) and at least one
+// voxel behind v:
+//  - octant layout (N <= 512; 8 volumes, one per direction octant, step s = sign(d)):
+//    G(v) = F(v - s) - 1, F(u) = edge of the largest empty in-volume cube anchored at u and
+//    extending along s, so B(v) = [v - s, v + (G - 1) s] (capped at kFwdCap - 1). Looking only
+//    ahead, it is far larger than the centred distance behind surfaces: shadow rays leaving the
+//    ground and rays moving away from geometry skip up to ~4x fewer sampled steps
+//    (scripts/skipsim.py);
+//  - single layout (N = 1024, where 8 volumes would overflow 32-bit offsets): G = D, the
+//    centred Chebyshev distance to the nearest non-empty voxel or the outside (capped at
+//    kDistCap), B(v) = [v - D + 1, v + D - 1]^3.
+// Why one voxel behind: on an axis crossed at the sampled step, currentPos = pos + s*dir may round
+// to just short of the crossed plane, and a later step that crosses another axis within that
+// rounding distance samples floor(currentPos) there, i.e. the voxel behind v on that axis.
+// After a sampled step whose texel is empty with G >= 2, an air ray (or a shadow ray) computes
+// s_lim, the ray parameter up to which its position provably stays inside B(v) (forward faces
+// pulled in by kSkipMargin, far above the float error of cur = pos + s*dir; positions only move
+// forward, so the back faces need no test). A step with s < s_lim therefore samples an empty voxel
 // inside the volume — no event, no TestCube — and needs only the exact DDA state update; the
 // sample, its address and the load are skipped. Every float op that defines the walk's state is
 // still executed, in the reference's order, so the walk is bit-identical.
@@ -501,6 +516,11 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 #endif
 constexpr uint32_t kDistCap = VRT_DIST_CAP;
 static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
+#ifndef VRT_FWD_CAP
+#define VRT_FWD_CAP 64
+#endif
+constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F; G = F - 1 is stored in 8 bits
+static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
 template <bool SHADOW, bool STATS>
@@ -532,6 +552,10 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   }
 #endif
   const bool skip_ok = SHADOW || medium == 0u;
+  // this ray's octant volume (its skip distances look along the ray's direction); uniform for
+  // shadow rays. Every octant volume holds the same voxel bytes.
+  const uint32_t obase =
+      ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
   const float s_len = c.max_len - len0;
@@ -623,7 +647,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
         const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-        const uint32_t packed = load_u16(c.vox, pidx);
+        const uint32_t packed = load_u16_at(c.vox, pidx, obase);
         const uint32_t v_raw = packed & kVoxMask;
         const uint32_t dist = packed >> kDistShift;
         const uint32_t v_ev = inb ? v_raw : kOutside;
@@ -1034,6 +1058,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   if (valid) {
     Ctx c;
     c.vox = vox;
+    c.ostride = a.ostride;
     c.n = a.n;
     c.p = uint32_t(a.n) + 1u;
     c.fn = a.fn;
@@ -1249,6 +1274,7 @@ __global__ void __launch_bounds__(256) dist_pass_kernel(const uint8_t* __restric
 
 // Pack into the kernel's padded (N+1)^3 format: voxel | D << 8, plane N repeats plane 0 (GL_REPEAT
 // folded into the layout) with D = 0 there (those texels are only read at c == N exactly).
+// Single-volume layout (N = 1024).
 __global__ void __launch_bounds__(256) pack_volume_kernel(const uint8_t* __restrict__ src,
                                                           const uint8_t* __restrict__ dist,
                                                           uint16_t* __restrict__ dst, uint32_t n) {
@@ -1260,11 +1286,58 @@ __global__ void __launch_bounds__(256) pack_volume_kernel(const uint8_t* __restr
     const bool edge = i == n || j == n || k == n;
     const uint32_t si = i == n ? 0u : i, sj = j == n ? 0u : j, sk = k == n ? 0u : k;
     const uint64_t sq = si + (uint64_t(sj) + uint64_t(sk) * n) * n;
-#if VRT_U8_VOL
-    reinterpret_cast<uint8_t*>(dst)[q] = uint8_t((src[sq] & 3u) | (edge ? 0u : uint32_t(dist[sq]) << 2));
-#else
     dst[q] = uint16_t(src[sq] | (edge ? 0u : uint32_t(dist[sq]) << 8));
-#endif
+  }
+}
+
+// One-sided pass of the octant forward distance along `axis` in direction sg = +-1:
+// out(v) = min(kFwdCap, distance to the outside pseudo-voxel ahead (N - c or c + 1),
+//              min over 0 <= o of max(o, in(v + sg*o*e_axis))),
+// where the first (x) pass reads in = 0 for a non-empty voxel and kFwdCap otherwise. x, then y,
+// then z: F(v) = min over non-empty / outside u in v's forward octant of max_a |u_a - v_a| (max
+// and min commute through the passes), i.e. the edge of the largest empty in-volume cube
+// anchored at v and extending along (sx, sy, sz). max(o, .) >= o, so the scan stops at o = d.
+__global__ void __launch_bounds__(256) fwd_pass_kernel(const uint8_t* __restrict__ in,
+                                                       uint8_t* __restrict__ out, uint32_t n,
+                                                       int axis, int sg, int first) {
+  const uint64_t total = uint64_t(n) * n * n;
+  const uint64_t stride = axis == 0 ? 1u : (axis == 1 ? uint64_t(n) : uint64_t(n) * n);
+  const int64_t step = sg > 0 ? int64_t(stride) : -int64_t(stride);
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
+       q += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t coord = uint32_t((q / stride) % n);
+    uint32_t d = min(sg > 0 ? n - coord : coord + 1u, kFwdCap);
+    // o < d <= the outside distance keeps v + sg*o inside the volume
+    for (uint32_t o = 0; o < d; ++o) {
+      const uint8_t v = in[uint64_t(int64_t(q) + int64_t(o) * step)];
+      const uint32_t val = first ? (v != 0 ? 0u : kFwdCap) : uint32_t(v);
+      d = min(d, max(o, val));
+    }
+    out[q] = uint8_t(d);
+  }
+}
+
+// Pack octant (sx, sy, sz)'s padded (N+1)^3 volume: voxel | G << 8 with G(v) = F(v - s) - 1
+// (0 when v - s is outside or F(v - s) = 0), plane N a copy of plane 0 with G = 0.
+__global__ void __launch_bounds__(256) fwd_pack_kernel(const uint8_t* __restrict__ src,
+                                                       const uint8_t* __restrict__ fwd,
+                                                       uint16_t* __restrict__ dst, uint32_t n,
+                                                       int sx, int sy, int sz) {
+  const uint32_t p = n + 1u;
+  const uint64_t total = uint64_t(p) * p * p;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < total;
+       q += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t i = uint32_t(q % p), j = uint32_t((q / p) % p), k = uint32_t(q / (uint64_t(p) * p));
+    const bool edge = i == n || j == n || k == n;
+    const uint32_t si = i == n ? 0u : i, sj = j == n ? 0u : j, sk = k == n ? 0u : k;
+    const uint64_t sq = si + (uint64_t(sj) + uint64_t(sk) * n) * n;
+    uint32_t g = 0;
+    const int64_t a = int64_t(i) - sx, b = int64_t(j) - sy, c = int64_t(k) - sz;
+    if (!edge && a >= 0 && b >= 0 && c >= 0 && a < int64_t(n) && b < int64_t(n) && c < int64_t(n)) {
+      const uint32_t f = fwd[uint64_t(a) + (uint64_t(b) + uint64_t(c) * n) * n];
+      g = f > 0u ? f - 1u : 0u;
+    }
+    dst[q] = uint16_t(src[sq] | (g << 8));
   }
 }
 
@@ -1275,9 +1348,11 @@ __global__ void __launch_bounds__(256) pack_volume_kernel(const uint8_t* __restr
 struct vrt_ctx {
   int device = 0;
   uint8_t* d_vox = nullptr;       // canonical N^3
-  uint8_t* d_tmp = nullptr;       // 2 x N^3 distance-field scratch
-  uint16_t* d_vox_pad = nullptr;  // padded (N+1)^3 voxel | D << 8, the kernel's format
+  uint8_t* d_tmp = nullptr;       // 3 x N^3 distance-field scratch (2 x for the single layout)
+  uint16_t* d_vox_pad = nullptr;  // octants x padded (N+1)^3 voxel | G << 8, the kernel's format
   int32_t n = 0;
+  int32_t octants = 0;            // 8 (octant forward distances, N <= 512) or 1 (centred, N = 1024)
+  int32_t layout_req = 0;         // vrt_set_skip_layout: 0 auto, 1 single centred volume, 8 octants
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
   unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of vrt_render
@@ -1375,6 +1450,9 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.rows = rows;
   a.row_step = row_step;
   a.pitch = cam->width;
+  a.ostride = ctx->octants == 8
+                  ? uint32_t(uint64_t(ctx->n + 1) * (ctx->n + 1) * (ctx->n + 1) * sizeof(uint16_t))
+                  : 0u;
   a.max_refl = p->max_reflections;
   a.max_transp = p->max_transparencies;
   a.textured = p->color_only ? 0 : 1;
@@ -1413,7 +1491,10 @@ int volume_alloc(vrt_ctx* ctx, int32_t n) {
   if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
     return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
   VRT_HIP(ctx, hipSetDevice(ctx->device));
-  if (ctx->d_vox && ctx->n != n) {
+  // octant layout while 8 padded u16 volumes stay addressable by a 32-bit byte offset
+  const bool fits = uint64_t(n + 1) * (n + 1) * (n + 1) * 2 * 8 <= (uint64_t(1) << 32);
+  const int32_t octants = fits && ctx->layout_req != 1 ? 8 : 1;
+  if (ctx->d_vox && (ctx->n != n || ctx->octants != octants)) {
     (void)hipFree(ctx->d_vox);
     (void)hipFree(ctx->d_tmp);
     (void)hipFree(ctx->d_vox_pad);
@@ -1421,8 +1502,10 @@ int volume_alloc(vrt_ctx* ctx, int32_t n) {
     ctx->d_vox_pad = nullptr;
   }
   if (!ctx->d_vox) {
-    const size_t bytes = size_t(n) * n * n, pbytes = size_t(n + 1) * (n + 1) * (n + 1) * 2;
-    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess || hipMalloc(&ctx->d_tmp, 2 * bytes) != hipSuccess ||
+    const size_t bytes = size_t(n) * n * n,
+                 pbytes = size_t(n + 1) * (n + 1) * (n + 1) * 2 * size_t(octants);
+    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess ||
+        hipMalloc(&ctx->d_tmp, (octants == 8 ? 3 : 2) * bytes) != hipSuccess ||
         hipMalloc(&ctx->d_vox_pad, pbytes) != hipSuccess) {
       if (ctx->d_vox) (void)hipFree(ctx->d_vox);
       if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
@@ -1433,6 +1516,7 @@ int volume_alloc(vrt_ctx* ctx, int32_t n) {
     }
   }
   ctx->n = n;
+  ctx->octants = octants;
   return VRT_OK;
 }
 
@@ -1444,11 +1528,28 @@ int volume_finish(vrt_ctx* ctx, hipStream_t s) {
   const unsigned b2 = unsigned(std::min<uint64_t>((pvol + 255) / 256, 16384));
   uint8_t* da = ctx->d_tmp;
   uint8_t* db = ctx->d_tmp + vol;
-  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, 1);
-  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, 0);
-  hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, db, da, n, 2, 0);
-  hipLaunchKernelGGL(vrt::pack_volume_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, da,
-                     ctx->d_vox_pad, n);
+  if (ctx->octants == 8) {
+    // octant forward distances: 2 x passes, 4 y passes, 8 z passes + packs (x -> y -> z nesting)
+    uint8_t* dc = ctx->d_tmp + 2 * vol;
+    for (int sx = 1; sx >= -1; sx -= 2) {
+      hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, sx, 1);
+      for (int sy = 1; sy >= -1; sy -= 2) {
+        hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, sy, 0);
+        for (int sz = 1; sz >= -1; sz -= 2) {
+          hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, db, dc, n, 2, sz, 0);
+          const int o = (sx < 0 ? 1 : 0) | (sy < 0 ? 2 : 0) | (sz < 0 ? 4 : 0);
+          hipLaunchKernelGGL(vrt::fwd_pack_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, dc,
+                             ctx->d_vox_pad + size_t(o) * pvol, n, sx, sy, sz);
+        }
+      }
+    }
+  } else {
+    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, 1);
+    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, 0);
+    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, db, da, n, 2, 0);
+    hipLaunchKernelGGL(vrt::pack_volume_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, da,
+                       ctx->d_vox_pad, n);
+  }
   VRT_HIP(ctx, hipGetLastError());
   VRT_HIP(ctx, hipStreamSynchronize(s));
   ctx->err.clear();
@@ -1552,11 +1653,25 @@ const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->d_v
 int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count) {
   if (!ctx) return VRT_ERR_INVALID;
   if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
-  const uint64_t p = uint64_t(ctx->n) + 1, total = p * p * p;
-  if (!out || count < total) return fail(ctx, VRT_ERR_INVALID, "output smaller than (N+1)^3");
+  const uint64_t p = uint64_t(ctx->n) + 1, total = p * p * p * uint64_t(ctx->octants);
+  if (!out || count < total)
+    return fail(ctx, VRT_ERR_INVALID, "output smaller than octants x (N+1)^3");
   VRT_HIP(ctx, hipSetDevice(ctx->device));
   VRT_HIP(ctx, hipMemcpy(out, ctx->d_vox_pad, total * sizeof(uint16_t), hipMemcpyDeviceToHost));
   return VRT_OK;
+}
+
+int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (octants != 0 && octants != 1 && octants != 8)
+    return fail(ctx, VRT_ERR_INVALID, "skip layout must be 0 (auto), 1 or 8");
+  ctx->layout_req = octants;
+  return VRT_OK;
+}
+
+int vrt_volume_octants(const vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  return ctx->d_vox_pad ? ctx->octants : 0;
 }
 
 #ifdef VRT_STAMPS

@@ -179,6 +179,23 @@ struct Counters {
 #ifndef VRT_AX_ADDR_SEL
 #define VRT_AX_ADDR_SEL 1
 #endif
+// Table layout: axis-major (entry a of work-item t at [a * threads + t]) keeps a wave's 16-byte
+// reads on distinct banks whatever axis each lane picks; lane-major ([3t + a], 48-byte lane
+// stride) collides whenever neighbouring lanes pick different axes.
+#ifndef VRT_AX_AXIS_MAJOR
+#define VRT_AX_AXIS_MAJOR 0
+#endif
+#ifndef VRT_WG_WAVES
+#define VRT_WG_WAVES 4
+#endif
+#ifndef VRT_CMP_T
+#define VRT_CMP_T 0
+#endif
+#ifndef VRT_LEN0_SPLIT
+#define VRT_LEN0_SPLIT 0
+#endif
+constexpr int kAxStride = VRT_AX_AXIS_MAJOR ? 64 * VRT_WG_WAVES : 1;  // float4s between axes
+constexpr int kAxLane = VRT_AX_AXIS_MAJOR ? 1 : 3;                      // float4s between lanes
 
 struct Ctx {
   const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | G << 8, one per octant (see pack kernels)
@@ -523,7 +540,9 @@ constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F; G = F - 1 is stored in 8
 static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
-template <bool SHADOW, bool STATS>
+// LEN0Z: the caller guarantees len0 == +0 (the primary ray, voxel.glsl:430), so
+// s = rayLength - ray.rayLength is rayLength itself (x - (+0) == x): one VALU less per step.
+template <bool SHADOW, bool STATS, bool LEN0Z = false>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
@@ -538,10 +557,10 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   // read): materialise shadow rays' uniform sun constants once, not per step
 #if VRT_LDS_AXIS
   c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
-  c.ax[1] = make_float4(pos.y, dir.y, rcp.y, step.y);
-  c.ax[2] = make_float4(pos.z, dir.z, rcp.z, step.z);
+  c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
+  c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
 #if VRT_AX_ADDR_SEL
-  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u, ax_a2 = ax_a0 + 32u;
+  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
   asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));  // three VGPRs, not re-derived
 #endif
 #else
@@ -558,7 +577,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
-  const float s_len = c.max_len - len0;
+  const float s_len = LEN0Z ? c.max_len : c.max_len - len0;
   f3 t = w.t;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
@@ -574,7 +593,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       break;
     }
     if (check) {
-      const float sc = len - len0;
+      const float sc = LEN0Z ? len : len - len0;
       if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
         result = WALK_MISS;
         break;
@@ -600,8 +619,14 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
       const f3 tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
       len += tmin;
-      const float s = len - len0;
+      const float s = LEN0Z ? len : len - len0;
+#if VRT_CMP_T
+      // t.a - tmin == 0 <=> t.a == tmin (finite t, gradual underflow): the masks no longer wait
+      // for the subtractions
+      const bool ey = t.y == tmin, ez = t.z == tmin;
+#else
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
+#endif
 #if !defined(VRT_DIAG_SAMPLED) && !defined(VRT_DIAG_WAVE)
       if (STATS) ties = add_if_both(ties, ey, ez);  // intersectionAxis[3] (counter/flag only)
 #elif defined(VRT_DIAG_WAVE) && VRT_DIAG_WAVE == 1  // diagnostic: TIE3 counts wave-level steps
@@ -618,7 +643,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
 #elif VRT_LDS_AXIS
       const uint32_t ai = axis_index(mey, mez);
-      const float4 ae = c.ax[ai];
+      const float4 ae = c.ax[ai * kAxStride];
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
 #else
       const float pa = sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x));
@@ -688,7 +713,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       break;
     }
   }
-  const float s_end = len - len0;  // currentPos of the last step (the hit point on an event)
+  const float s_end = LEN0Z ? len : len - len0;  // currentPos of the last step (the hit point on an event)
   w.t = t;
   w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
   w.len = len;
@@ -699,13 +724,14 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
 }
 
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)
-template <bool STATS>
+template <bool STATS, bool LEN0Z = false>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS, LEN0Z && VRT_LEN0_SPLIT>(c, pos, dir, rcp, len0, medium, w, axis,
+                                                            vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -816,7 +842,8 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
-template <bool STATS, bool TEX>
+// PRIMARY: the primary ray (len 0, medium air: every event is a hit, no in-volume refraction)
+template <bool STATS, bool TEX, bool PRIMARY = false>
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -835,11 +862,13 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk_ray<STATS>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    r = walk_ray<STATS, PRIMARY>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
-    if (v != 0u) {  // HasVoxel(voxel) && voxel != rayVoxel (:353)
+    // HasVoxel(voxel) && voxel != rayVoxel (:353); a primary ray's medium is air, so its
+    // every event is a hit
+    if (PRIMARY || v != 0u) {
       h.found = true;
       h.voxel = v;
       h.vidx = vidx;
@@ -880,10 +909,10 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
 }
 
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, bool PRIMARY = false>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS, TEX>(c, ray, k, steps, flags);
+  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
   if (h.found) {
     Ray sr;  // GetShadowRay (:191-201)
     sr.voxel = h.voxel;
@@ -1075,7 +1104,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     c.atlas_fts = float(a.atlas_tex_size);
 #if VRT_LDS_AXIS
     __shared__ float4 ax_tab[kWgThreads * 3];
-    c.ax = &ax_tab[threadIdx.x * 3];
+    c.ax = &ax_tab[threadIdx.x * kAxLane];
 #endif
 
     const int py = a.row0 + li * a.row_step;
@@ -1106,7 +1135,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     uint32_t steps = 0, flags = 0;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
-    const Hit h0 = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
+    const Hit h0 = trace_with_shadow<STATS, TEX, true>(c, ray, color, k, steps, flags);
     const int32_t hit_vidx = h0.found ? h0.vidx : -1;
     const float hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images

@@ -908,6 +908,38 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
   return h;
 }
 
+// Brightness of a hit that is not in shadow (voxel.glsl:405-409)
+template <bool TEX>
+__device__ __forceinline__ float lit_brightness(const Hit& h, const f3 sun_dir, const f3 ray_dir) {
+  const uint32_t m = mat_id(h.voxel);
+  const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sun_dir), 0.0f);
+  const float specular =
+      mat_ks(m, TEX) * gpow(gmax(dot3(reflect3(sun_dir, h.normal), ray_dir), 0.0f), mat_exp(m, TEX));
+  return kAmbient + diffuse + specular;
+}
+
+// RayColor (:184-188)
+template <bool TEX>
+__device__ __forceinline__ void apply_hit_color(const Ctx& c, const Hit& h, float energy,
+                                                float brightness, f3& color) {
+  const float4 col = get_color<TEX>(c, h);
+  color.x = mixf(color.x, col.x * col.w * brightness, energy);
+  color.y = mixf(color.y, col.y * col.w * brightness, energy);
+  color.z = mixf(color.z, col.z * col.w * brightness, energy);
+}
+
+// GetSkyboxColor (:386-393), then the second mix at :420
+__device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3& color) {
+  const f3 u = normalize3(ray.dir);
+  const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
+  const float grad = (u.y + 1.0f) * 0.5f;
+  const float sy = gmax(c.sun.y, 0.0f);
+  const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
+  const float a1 = 1.0f - ray.energy;
+  const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
+  color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
+}
+
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
 template <bool STATS, bool TEX, bool PRIMARY = false>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
@@ -924,33 +956,307 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
     sr.tdepth = 0;
     k.c[VRT_CNT_SHADOW_RAYS]++;
     const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
-    const uint32_t m = mat_id(h.voxel);
-    float brightness;
-    if (in_shadow) {
-      brightness = kAmbient;
-    } else {
-      const float diffuse = mat_kd(m) * gmax(dot3(h.normal, sr.dir), 0.0f);
-      const float specular =
-          mat_ks(m, TEX) * gpow(gmax(dot3(reflect3(sr.dir, h.normal), ray.dir), 0.0f), mat_exp(m, TEX));
-      brightness = kAmbient + diffuse + specular;
-    }
-    const float4 col = get_color<TEX>(c, h);  // RayColor (:184-188)
-    const float e = ray.energy;
-    color.x = mixf(color.x, col.x * col.w * brightness, e);
-    color.y = mixf(color.y, col.y * col.w * brightness, e);
-    color.z = mixf(color.z, col.z * col.w * brightness, e);
+    const float brightness = in_shadow ? kAmbient : lit_brightness<TEX>(h, sr.dir, ray.dir);
+    apply_hit_color<TEX>(c, h, ray.energy, brightness, color);
   } else {
-    // GetSkyboxColor (:386-393), then the second mix at :420
-    const f3 u = normalize3(ray.dir);
-    const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
-    const float grad = (u.y + 1.0f) * 0.5f;
-    const float sy = gmax(c.sun.y, 0.0f);
-    const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
-    const float a1 = 1.0f - ray.energy;
-    const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
-    color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
+    apply_sky_color(c, ray, color);
   }
   return h;
+}
+
+// ------------------------------------------------------------ certified walks (stats-free) --
+//
+// The colour-only image depends on a primary walk only through its outcome — miss, or the first
+// event's byte and face axis — and on a shadow walk only through blocked / not blocked
+// (voxel.glsl:395-423: no hit point, length or texel index enters the colour of a non-glass hit;
+// the sky colour depends on the direction alone). The exact walk (skip_walk) replays every DDA
+// step's float state to be bit-identical; the CERTIFIED walk below instead follows the real ray
+// with a float DDA that jumps through the empty boxes of the octant distance field, and returns
+// the exact walk's outcome only when no rounding of the exact walk can change it:
+//  - the exact walk's parameter at any plane crossing differs from the real one by at most
+//    gam_b(u) (`cert_gamma`): its len accumulates at most u*|d|_1 + 3 non-zero steps, each adding
+//    <= 2^-24 len; each t is re-anchored from currentPos (roundings of magnitude <= N + 2, times
+//    1/|d_b|) and then decremented at most K times; zero-length tie steps add no rounding;
+//  - crossings of two axes closer than gam_a + gam_b may come in either order or as a tie: the
+//    cells the exact walk could sample instead (`alternatives`) must be non-events, else UNSURE;
+//  - an event cell is a certified hit only if its entry crossing is isolated (the exact walk
+//    then enters it across the same face, index = that axis) and the length test cannot stop
+//    the walk first; a walk that leaves the volume or whose previous crossing lies beyond the
+//    length budget (by more than the bound) is a certified miss;
+//  - cells with an index N are outside on the path (the exact walk reads the GL_REPEAT plane N
+//    only at a coordinate exactly N, i.e. at a near-edge crossing, where the alternatives read
+//    the padded layout's plane N).
+// UNSURE rays (~0.2 % of pixels at the BASELINE configs, scripts/certsim.py) and every pixel
+// whose primary hit is glass (its secondary rays start at the exact hit point) take the exact
+// path. Only the stats-free colour-only instance uses it: hit records and counters need the
+// exact walk, and textured shading reads the hit point.
+#ifndef VRT_CERT
+#define VRT_CERT 1
+#endif
+#ifdef VRT_CERT_DIAG  // diagnostic build only (scripts/cert_diag.py): outcome counts per pixel
+__device__ unsigned long long g_cert_diag[16];
+#define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
+#else
+#define CERT_DIAG(i) ((void)0)
+#endif
+enum : int { CERT_MISS = 0, CERT_HIT = 1, CERT_UNSURE = 2 };
+constexpr float kCertMargin = 1.0f / 64.0f;  // jump boxes' forward faces pulled in (position)
+constexpr int kCertMaxIter = 1024;
+
+struct CertResult {
+  int res;
+  uint32_t byte;
+  int axis;
+  int cx, cy, cz;  // hit cell
+  float u;         // crossing parameter of the hit
+  float eu;        // bound of the exact walk's parameter error there
+};
+
+__device__ __forceinline__ uint32_t cell_texel(const Ctx& c, int i, int j, int k, uint32_t obase) {
+  return load_u16_at(c.vox, mad24(mad24(uint32_t(k), c.p, uint32_t(j)), c.p, uint32_t(i)), obase);
+}
+// texel of a cell on the certified path: cells outside [0, N)^3 read 0 (empty, G = 0)
+__device__ __forceinline__ uint32_t path_texel(const Ctx& c, int i, int j, int k, uint32_t obase) {
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(i) >= n || uint32_t(j) >= n || uint32_t(k) >= n) return 0u;
+  return cell_texel(c, i, j, k, obase);
+}
+// byte of a cell the exact walk might sample at a near-edge crossing (plane N: GL_REPEAT copy)
+__device__ __forceinline__ uint32_t alt_byte(const Ctx& c, int i, int j, int k, uint32_t obase) {
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(i) > n || uint32_t(j) > n || uint32_t(k) > n) return 0u;
+  return cell_texel(c, i, j, k, obase) & kVoxMask;
+}
+template <bool SHADOW>
+__device__ __forceinline__ bool cert_event(uint32_t b) {
+  return SHADOW ? (b & ~2u) != 0u : b != 0u;  // shadow: opaque (not air, not glass)
+}
+__device__ __forceinline__ int icomp(int x, int y, int z, int a) { return a == 0 ? x : (a == 1 ? y : z); }
+
+// Certified walk from P along D (every |d| in the fast-path range) with rcp = RN(1/D), starting in
+// cell (cx, cy, cz) (inside the volume), budget U = max_len - len0 (the exact walk samples the
+// crossing at u iff its len before that step is < max_len). e0: extra parameter uncertainty of
+// the start (a shadow origin is the exact primary hit point, known to +-e0 along the primary);
+// ed: extra per-axis crossing-order uncertainty from it; len0b: bound of len0.
+template <bool SHADOW>
+__device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 rcp, const float U,
+                                int cx, int cy, int cz, const float e0, const f3 ed,
+                                const float len0b) {
+  CertResult r;
+  r.res = CERT_UNSURE;
+  r.byte = 0u;
+  r.axis = 0;
+  r.cx = r.cy = r.cz = 0;
+  r.u = 0.0f;
+  r.eu = 0.0f;
+  const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
+  const f3 ar = mk(__builtin_fabsf(rcp.x), __builtin_fabsf(rcp.y), __builtin_fabsf(rcp.z));
+  const float l1 = __builtin_fabsf(D.x) + __builtin_fabsf(D.y) + __builtin_fabsf(D.z);
+  const uint32_t obase = ((D.x < 0.0f ? 1u : 0u) | (D.y < 0.0f ? 2u : 0u) | (D.z < 0.0f ? 4u : 0u)) * c.ostride;
+  // rounding-bound constants (float, with a 2x safety factor on the derived bound)
+  constexpr float k24 = 2.0f * 0x1p-24f;
+  const float inv2l1 = 0.5f / l1;
+  const float nterm = 3.0f * c.fn + 8.0f;
+  f3 sig = mk((float(cx + (sx > 0)) - P.x) * rcp.x, (float(cy + (sy > 0)) - P.y) * rcp.y,
+              (float(cz + (sz > 0)) - P.z) * rcp.z);
+  uint32_t tex = path_texel(c, cx, cy, cz, obase);
+  for (int guard = 0; guard < kCertMaxIter; ++guard) {
+    const int a = sig.y < sig.x ? (sig.z < sig.y ? 2 : 1) : (sig.z < sig.x ? 2 : 0);
+    const float s1 = a == 0 ? sig.x : (a == 1 ? sig.y : sig.z);
+    const float uu = gmax(s1, 0.0f);
+    const float K = uu * l1 + 3.0f;
+    const float sumlen = (K + 3.0f) * (K + 3.0f) * inv2l1 + K * (len0b + 1.0f);
+    const float gbase = k24 * (sumlen + 2.0f * (uu + len0b)) + 4e-5f + e0;
+    const float gK = k24 * (K + nterm);
+    const f3 gam = mk(gbase + gK * ar.x + ed.x, gbase + gK * ar.y + ed.y, gbase + gK * ar.z + ed.z);
+    const float gL = 2.0f * k24 * sumlen + 1e-4f + e0;
+    // empty-space jump: the box [v - s, v + (G - 1) s] of this cell is empty and in the volume
+    const uint32_t G = tex >> kDistShift;
+    if (G >= 2u) {
+      const float fg = float(G) - kCertMargin;
+      const float lx = (float(sx > 0 ? cx : cx + 1) + float(sx) * fg - P.x) * rcp.x;
+      const float ly = (float(sy > 0 ? cy : cy + 1) + float(sy) * fg - P.y) * rcp.y;
+      const float lz = (float(sz > 0 ? cz : cz + 1) + float(sz) * fg - P.z) * rcp.z;
+      const float slim = __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, U + 2.0f));
+      const float uj = slim - __builtin_fmaxf(gam.x, __builtin_fmaxf(gam.y, gam.z));
+      if (uj > s1) {
+        const float x = P.x + uj * D.x, y = P.y + uj * D.y, z = P.z + uj * D.z;
+        cx = sx > 0 ? int(__builtin_floorf(x)) : int(__builtin_ceilf(x)) - 1;
+        cy = sy > 0 ? int(__builtin_floorf(y)) : int(__builtin_ceilf(y)) - 1;
+        cz = sz > 0 ? int(__builtin_floorf(z)) : int(__builtin_ceilf(z)) - 1;
+        sig = mk((float(cx + (sx > 0)) - P.x) * rcp.x, (float(cy + (sy > 0)) - P.y) * rcp.y,
+                 (float(cz + (sz > 0)) - P.z) * rcp.z);
+        tex = path_texel(c, cx, cy, cz, obase);
+        continue;
+      }
+    }
+    // one crossing, s1 on axis a; prev = the crossing before it (the exact walk's len there)
+    const f3 back = mk(sig.x - ar.x, sig.y - ar.y, sig.z - ar.z);
+    const float prev = gmax(gmax(back.x, 0.0f), gmax(back.y, back.z));
+    if (prev > U + gL) {
+      r.res = CERT_MISS;
+      return r;
+    }
+    const int sa = a == 0 ? sx : (a == 1 ? sy : sz);
+    const int nx = cx + (a == 0 ? sx : 0), ny = cy + (a == 1 ? sy : 0), nz = cz + (a == 2 ? sz : 0);
+    const float ga = a == 0 ? gam.x : (a == 1 ? gam.y : gam.z);
+    // near-edge flags per other axis: ahead (crossed within the bound after s1) / behind (before)
+    const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
+               ahz = a != 2 && sig.z - s1 < ga + gam.z;
+    const bool bhx = a != 0 && back.x >= 0.0f && s1 - back.x < ga + gam.x;
+    const bool bhy = a != 1 && back.y >= 0.0f && s1 - back.y < ga + gam.y;
+    const bool bhz = a != 2 && back.z >= 0.0f && s1 - back.z < ga + gam.z;
+    const int nah = int(ahx) + int(ahy) + int(ahz), nbh = int(bhx) + int(bhy) + int(bhz);
+    const uint32_t ntex = path_texel(c, nx, ny, nz, obase);
+    const uint32_t nb = ntex & kVoxMask;
+    if (cert_event<SHADOW>(nb)) {
+      if (SHADOW && nah + nbh == 1) {
+        // blocked whichever way the exact walk goes: near-behind b still samples nc (or nc - e_b
+        // first); near-ahead b samples nc, or cell + e_b and then nc + e_b
+        bool ok = true;
+        if (nah) {
+          const int b = ahx ? 0 : (ahy ? 1 : 2);
+          const int bx = b == 0 ? sx : 0, by = b == 1 ? sy : 0, bz = b == 2 ? sz : 0;
+          ok = cert_event<true>(alt_byte(c, cx + bx, cy + by, cz + bz, obase)) ||
+               cert_event<true>(alt_byte(c, nx + bx, ny + by, nz + bz, obase));
+        }
+        if (ok && prev + gL < U) {
+          r.res = CERT_HIT;
+          r.byte = nb;
+          return r;
+        }
+      }
+      if (nah + nbh == 0 && prev + gL < U) {
+        r.res = CERT_HIT;
+        r.byte = nb;
+        r.axis = a;
+        r.cx = nx;
+        r.cy = ny;
+        r.cz = nz;
+        r.u = s1;
+        r.eu = ga;
+      }
+      return r;  // hit or unsure
+    }
+    if (nah + nbh >= 2) {  // near a corner: the 2x2x2 block ahead and the cells behind nc
+      for (int q = 1; q < 8; ++q)
+        if (cert_event<SHADOW>(alt_byte(c, cx + ((q & 1) ? sx : 0), cy + ((q & 2) ? sy : 0),
+                                        cz + ((q & 4) ? sz : 0), obase)))
+          return r;
+      if ((bhx && cert_event<SHADOW>(alt_byte(c, nx - sx, ny, nz, obase))) ||
+          (bhy && cert_event<SHADOW>(alt_byte(c, nx, ny - sy, nz, obase))) ||
+          (bhz && cert_event<SHADOW>(alt_byte(c, nx, ny, nz - sz, obase))))
+        return r;
+    } else if (nah) {  // b may be crossed first, or tie: cell + e_b, nc + e_b
+      const int b = ahx ? 0 : (ahy ? 1 : 2);
+      const int bx = b == 0 ? sx : 0, by = b == 1 ? sy : 0, bz = b == 2 ? sz : 0;
+      if (cert_event<SHADOW>(alt_byte(c, cx + bx, cy + by, cz + bz, obase)) ||
+          cert_event<SHADOW>(alt_byte(c, nx + bx, ny + by, nz + bz, obase)))
+        return r;
+    } else if (nbh) {  // a may have been crossed before b: nc - e_b
+      const int b = bhx ? 0 : (bhy ? 1 : 2);
+      if (cert_event<SHADOW>(alt_byte(c, nx - (b == 0 ? sx : 0), ny - (b == 1 ? sy : 0),
+                                      nz - (b == 2 ? sz : 0), obase)))
+        return r;
+    }
+    const int na = icomp(nx, ny, nz, a);
+    if ((sa > 0 && na >= c.n) || (sa < 0 && na < 0)) {  // left the volume, moving away
+      r.res = CERT_MISS;
+      return r;
+    }
+    cx = nx;
+    cy = ny;
+    cz = nz;
+    tex = ntex;
+    const float np = float(na + (sa > 0 ? 1 : 0));
+    if (a == 0) sig.x = (np - P.x) * rcp.x;
+    else if (a == 1) sig.y = (np - P.y) * rcp.y;
+    else sig.z = (np - P.z) * rcp.z;
+  }
+  return r;
+}
+
+// The whole pixel by certified walks, when it can be certified: a primary miss (sky) or a
+// non-glass primary hit whose shadow is certified or irrelevant (lit brightness == ambient).
+// Returns false (colour untouched) when the pixel must take the exact path.
+__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray, f3& color) {
+  const f3 P = ray.pos, D = ray.dir;
+  if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
+  const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
+  // the exact walk's first planes: d < 0 ? ceil(p - 1) : floor(p + 1) (voxel.glsl:306-309)
+  const int cx = sx > 0 ? int(__builtin_floorf(P.x)) : int(__builtin_ceilf(P.x)) - 1;
+  const int cy = sy > 0 ? int(__builtin_floorf(P.y)) : int(__builtin_ceilf(P.y)) - 1;
+  const int cz = sz > 0 ? int(__builtin_floorf(P.z)) : int(__builtin_ceilf(P.z)) - 1;
+  const float wpx = sx > 0 ? __builtin_floorf(P.x + 1.0f) : __builtin_ceilf(P.x - 1.0f);
+  const float wpy = sy > 0 ? __builtin_floorf(P.y + 1.0f) : __builtin_ceilf(P.y - 1.0f);
+  const float wpz = sz > 0 ? __builtin_floorf(P.z + 1.0f) : __builtin_ceilf(P.z - 1.0f);
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) { CERT_DIAG(0); return false; }
+  if (wpx != float(cx + (sx > 0)) || wpy != float(cy + (sy > 0)) || wpz != float(cz + (sz > 0))) {
+    CERT_DIAG(0);
+    return false;
+  }
+  const f3 rcp = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray.len, cx, cy, cz, 0.0f,
+                                        mk(0.0f, 0.0f, 0.0f), 0.0f);
+  if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }
+  if (h.res == CERT_MISS) {
+    CERT_DIAG(2);
+    apply_sky_color(c, ray, color);
+    return true;
+  }
+  if (mat_id(h.byte) == 2u) { CERT_DIAG(3); return false; }  // glass: secondary rays start at the exact hit point
+  Hit hh;
+  hh.found = true;
+  hh.voxel = h.byte;
+  hh.axis = h.axis;
+  hh.vidx = -1;
+  hh.len = 0.0f;
+  hh.point = mk(0.0f, 0.0f, 0.0f);
+  hh.normal = mk(0.0f, 0.0f, 0.0f);
+  const float da = h.axis == 0 ? D.x : (h.axis == 1 ? D.y : D.z);
+  set_comp(hh.normal, h.axis, -gsign(da));
+  const float lit = lit_brightness<false>(hh, c.sun_n, D);
+  float brightness = kAmbient;
+  if (lit != kAmbient) {  // otherwise in shadow or not, the brightness is the ambient term
+    const f3 S = c.sun_n;
+    const float sa = h.axis == 0 ? S.x : (h.axis == 1 ? S.y : S.z);
+    if (!(dot3(hh.normal, S) > 0.0f) || !fast_path_ok(S)) { CERT_DIAG(5); return false; }  // back face
+    // shadow origin: the exact hit point, within eu (parameter) of P + u D along the primary;
+    // the start cell is the air cell in front of the hit face
+    const float eH = h.eu;
+    const f3 X = mk(P.x + h.u * D.x, P.y + h.u * D.y, P.z + h.u * D.z);
+    int ax = h.cx, ay = h.cy, az = h.cz;
+    if (h.axis == 0) ax -= sx;
+    else if (h.axis == 1) ay -= sy;
+    else az -= sz;
+    const f3 ed = mk(2.0f * eH * __builtin_fabsf(D.x * c.sun_rcp.x),
+                     2.0f * eH * __builtin_fabsf(D.y * c.sun_rcp.y),
+                     2.0f * eH * __builtin_fabsf(D.z * c.sun_rcp.z));
+    // the origin may lie inside the hit cell by eH |d_axis|: the shadow walk must leave that
+    // layer before it crosses any other plane, and the air cell must not block
+    const float lead = (eH * __builtin_fabsf(da) + 1e-5f) * __builtin_fabsf(1.0f / sa);
+    const int tsx = S.x > 0.0f ? 1 : 0, tsy = S.y > 0.0f ? 1 : 0, tsz = S.z > 0.0f ? 1 : 0;
+    const float wx = (float(ax + tsx) - X.x) * c.sun_rcp.x;
+    const float wy = (float(ay + tsy) - X.y) * c.sun_rcp.y;
+    const float wz = (float(az + tsz) - X.z) * c.sun_rcp.z;
+    if ((h.axis != 0 && !(wx >= lead + ed.x + 1e-4f)) || (h.axis != 1 && !(wy >= lead + ed.y + 1e-4f)) ||
+        (h.axis != 2 && !(wz >= lead + ed.z + 1e-4f))) {
+      CERT_DIAG(6);
+      return false;
+    }
+    if (uint32_t(ax) >= n || uint32_t(ay) >= n || uint32_t(az) >= n) { CERT_DIAG(7); return false; }
+    if (cert_event<true>(cell_texel(c, ax, ay, az, 0u) & kVoxMask)) { CERT_DIAG(7); return false; }
+    const CertResult s = cert_walk<true>(c, X, S, c.sun_rcp, c.max_len - (ray.len + h.u), ax, ay,
+                                         az, eH, ed, h.u);
+    if (s.res == CERT_UNSURE) { CERT_DIAG(8); return false; }
+    CERT_DIAG(9);
+    brightness = s.res == CERT_HIT ? kAmbient : lit;
+  } else {
+    CERT_DIAG(4);
+  }
+  apply_hit_color<false>(c, hh, ray.energy, brightness, color);
+  return true;
 }
 
 constexpr int kMaxStack = 17;
@@ -1135,6 +1441,14 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     uint32_t steps = 0, flags = 0;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
+#if VRT_CERT
+    // stats-free colour-only frames: certified walks first, the exact path for the rest
+    if (!STATS && !TEX && a.ostride != 0u && cert_pixel(c, ray, color)) goto epilogue;
+#ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
+    if (!STATS && !TEX) goto epilogue;
+#endif
+#endif
+    {
     const Hit h0 = trace_with_shadow<STATS, TEX, true>(c, ray, color, k, steps, flags);
     const int32_t hit_vidx = h0.found ? h0.vidx : -1;
     const float hit_len = h0.found ? h0.len : 0.0f;
@@ -1162,6 +1476,19 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
         h = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
       }
     }
+    if (STATS && hits) {
+      const uint32_t l3 = lane_id();
+      vrt_hit hr;
+      hr.voxel_index = hit_vidx;
+      hr.ray_length = hit_len;
+      hr.steps = steps;
+      hr.flags = flags;
+      hits[size_t(pixel_row(wave, l3)) * size_t(a.pitch) + size_t(pixel_x(wave, l3))] = hr;
+    }
+    }
+#if VRT_CERT
+  epilogue:
+#endif
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
     if (a.cur) {  // fused reference post-pass: RGB8 ray-trace store, temporal blend, RGB8 store
@@ -1170,14 +1497,6 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       a.cur[o] = temporal_blend(rw, a.prev[o], a.alpha);
     } else {
       out[o] = make_float4(color.x, color.y, color.z, 1.0f);
-    }
-    if (STATS && hits) {
-      vrt_hit hr;
-      hr.voxel_index = hit_vidx;
-      hr.ray_length = hit_len;
-      hr.steps = steps;
-      hr.flags = flags;
-      hits[o] = hr;
     }
   }
 
@@ -1702,6 +2021,17 @@ int vrt_volume_octants(const vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
   return ctx->d_vox_pad ? ctx->octants : 0;
 }
+
+#ifdef VRT_CERT_DIAG
+// diagnostic build only: read and reset the certified-walk outcome counts (16 x u64)
+int vrt_debug_cert_diag(uint64_t* out) {
+  if (!out) return VRT_ERR_INVALID;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_cert_diag), 16 * 8) != hipSuccess) return VRT_ERR_DEVICE;
+  static const uint64_t zero[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vrt::g_cert_diag), zero, 16 * 8) == hipSuccess ? VRT_OK
+                                                                                    : VRT_ERR_DEVICE;
+}
+#endif
 
 #ifdef VRT_STAMPS
 // diagnostic build only: copy the per-wave stamps of the last render (count = 3 x waves)

@@ -19,7 +19,8 @@ from voxelraytracer_amd import abi  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 
 NAMES = ["exact_start", "primary_unsure", "miss", "glass_hit", "hit_ambient", "back_face",
-         "shadow_start_unsure", "air_cell", "shadow_unsure", "shadow_certified"]
+         "shadow_start_unsure", "air_cell", "shadow_unsure", "shadow_certified",
+         "primary_iters", "primary_iters_gt16", "primary_wave_max_iters"]
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="C1,C2,C3,C4")
 args = ap.parse_args()
@@ -41,5 +42,6 @@ for cfg in args.configs.split(","):
         assert lib.vrt_debug_cert_diag(cnt.ctypes.data) == 0
     px = w * h
     d = {k: round(float(cnt[i]) / px, 5) for i, k in enumerate(NAMES)}
+    d["primary_wave_max_iters"] = round(float(cnt[12]) / (px / 64), 3)
     certified = (cnt[2] + cnt[4] + cnt[9]) / px
     print(cfg, json.dumps(dict(pixels=px, certified=round(float(certified), 5), **d)), flush=True)

@@ -115,6 +115,7 @@ static cres_t cwalk(v3 P, v3 D, float U, int shadow, const int* cell0, double e0
   }
   for (int a = 0; a < 3; a++)
     if (cell[a] < 0 || cell[a] >= N) { r.res = C_UNC; r.why = 1; return r; }
+  int first = 1;
   for (int guard = 0; guard < 100000; guard++) {
     r.iters++;
     int a = 0;
@@ -136,6 +137,11 @@ static cres_t cwalk(v3 P, v3 D, float U, int shadow, const int* cell0, double e0
     const double gL = GSCALE * (2.0 * U24 * sumlen + 1e-4 + e0);
     /* empty-space jump */
     int G = gdist(cell, s, o);
+    if (first) {   /* no crossing behind the start: the unguarded box F(v) = G(v + s) + 1 */
+      int c2[3] = {cell[0] + s[0], cell[1] + s[1], cell[2] + s[2]};
+      G = gdist(c2, s, o) + 1;
+      first = 0;
+    }
     if (G >= 2) {
       float slim = 1e30f;
       for (int b = 0; b < 3; b++) {
@@ -257,6 +263,8 @@ EXPORT void cs_run(const float* inv_pv, int w, int h, const float* sun, float ma
   const int tw = (w + 7) / 8, th = (h + 7) / 8;
   double acc[32] = {0};
   uint8_t* wave_unc = calloc((size_t)tw * th, 1);
+  uint16_t* wave_it = calloc((size_t)tw * th, 2);
+  uint16_t* wave_its = calloc((size_t)tw * th, 2);
   uint8_t* wave_unc_p = calloc((size_t)tw * th, 1);
 #pragma omp parallel
   {
@@ -291,6 +299,7 @@ EXPORT void cs_run(const float* inv_pv, int w, int h, const float* sun, float ma
         int unc = 0, uncp = 0;
         cres_t cr = cwalk(ray.pos, ray.dir, max_len - 0.0f, 0, NULL, 0.0, (double[3]){0, 0, 0}, 0.0);
         loc[2] += cr.iters;
+        { uint16_t* w = &wave_it[(py / 8) * tw + px / 8]; if (cr.iters > *w) *w = (uint16_t)cr.iters; }
         loc[3] += cr.jumps;
         if (cr.res == C_UNC) { loc[4] += 1; unc = uncp = 1; loc[20 + (cr.why & 7)] += 1; }
         else if (cr.res == C_MISS) {
@@ -353,6 +362,7 @@ EXPORT void cs_run(const float* inv_pv, int w, int h, const float* sun, float ma
             else {
               cres_t cs = cwalk(X, sr.dir, max_len - is.len, 1, c0, eH, ed, xu);
               loc[14] += cs.iters;
+              { uint16_t* w = &wave_its[(py / 8) * tw + px / 8]; if (cs.iters > *w) *w = (uint16_t)cs.iters; }
               loc[15] += cs.jumps;
               if (cs.res == C_UNC) { loc[16] += 1; unc = 1; loc[24 + (cs.why & 7)] += 1; }
               else {
@@ -374,7 +384,11 @@ EXPORT void cs_run(const float* inv_pv, int w, int h, const float* sun, float ma
     for (int q = 0; q < 32; q++) acc[q] += loc[q];
   }
   double wu = 0, wup = 0;
-  for (int i = 0; i < tw * th; i++) { wu += wave_unc[i]; wup += wave_unc_p[i]; }
+  double wi = 0, wis = 0;
+  for (int i = 0; i < tw * th; i++) { wu += wave_unc[i]; wup += wave_unc_p[i]; wi += wave_it[i]; wis += wave_its[i]; }
+  fprintf(stderr, "wave-level iterations (max over 8x8): primary %.2f shadow %.2f per wave\n", wi / (tw * th), wis / (tw * th));
+  free(wave_it);
+  free(wave_its);
   free(wave_unc);
   free(wave_unc_p);
   for (int q = 0; q < 32; q++) out[q] = acc[q];

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def renderer(built):
     r = vrt.Renderer(0)
+    r.set_certified(1)   # every case below exercises the certified walks, whatever the scene
     yield r
     r.close()
 
@@ -102,3 +103,50 @@ def test_certified_camera_outside_and_noise(renderer):
     check_same(renderer, vox, n, 96, 64, 4, 2, pos=(0.0, 40.0, 0.0), rot=(-60.0, 30.0, 0.0))
     check_same(renderer, vox, n, 96, 64, 4, 2, ray_noise=0.05, time=3.0)
     check_same(renderer, vox, n, 96, 64, 4, 2, max_ray_length=20.0)
+    g = vrt.build_scene("glass_cube", n)
+    check_same(renderer, g, n, 96, 64, 4, 4, reflection_noise=0.05, time=2.0)
+    check_same(renderer, g, n, 96, 64, 4, 4, refraction_noise=0.01, time=2.0)
+    check_same(renderer, g, n, 96, 64, 1, 8, max_ray_length=40.0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_certified_glass_scenes(renderer, seed):
+    """Glass everywhere: bounce stacks, in-volume refraction, total internal reflection."""
+    rng = np.random.default_rng(200 + seed)
+    n = [16, 32, 64, 32][seed]
+    vox = np.zeros((n, n, n), np.uint8)
+    m = rng.random((n, n, n)) < [0.05, 0.02, 0.01, 0.1][seed]
+    vox[m] = rng.choice(np.array([2, 2, 2, 1, 3], np.uint8), size=int(m.sum()))
+    vox[n // 4: n // 2, n // 4: n // 2, n // 4: n // 2] = 2   # a solid glass block
+    vox[:, :2, :] = 1
+    vox = vox.reshape(-1)
+    for _ in range(3):
+        pos = tuple(float(x) for x in np.round(rng.uniform(-n / 3, n / 3, 3) * 2) / 2)
+        rot = (float(rng.choice([-60, -45, -35.26439, -20, 0])),
+               float(rng.choice([0, 45, 90, 135, 200, 33.3])), 0.0)
+        check_same(renderer, vox, n, 72, 54, 4, 4, pos=pos, rot=rot)
+
+
+def test_certified_modes(renderer):
+    """Automatic mode: on unless glass is > 1/8 of the non-empty voxels (the glass cube); every mode
+    renders the same image."""
+    try:
+        for scene, n, auto in (("glass_cube", 64, False), ("refraction", 64, True), ("terrain", 128, True)):
+            vox = vrt.build_scene(scene, n)
+            renderer.upload_volume(vox, n)
+            renderer.set_certified(0)
+            assert renderer.certified() == auto, scene
+            renderer.set_certified(-1)
+            assert not renderer.certified()
+            cam = vrt.make_camera(96, 64)
+            p = vrt.default_params(4, 4)
+            imgs = []
+            for mode in (-1, 0, 1):
+                renderer.set_certified(mode)
+                imgs.append(stats_free(renderer, cam, p, 64, 96))
+            assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
+            assert np.array_equal(imgs[0].view(np.uint32), imgs[2].view(np.uint32))
+        with pytest.raises(vrt.VrtError):
+            renderer.set_certified(2)
+    finally:
+        renderer.set_certified(1)

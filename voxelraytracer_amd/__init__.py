@@ -218,6 +218,14 @@ class Renderer:
         """Skip-distance layout of the next upload: 0 auto, 1 centred single volume, 8 octants."""
         self._check(self._lib.vrt_set_skip_layout(self._h, octants), "vrt_set_skip_layout")
 
+    def set_certified(self, mode: int):
+        """Certified walks for stats-free colour-only frames: 1 always, -1 never, 0 automatic."""
+        self._check(self._lib.vrt_set_certified(self._h, mode), "vrt_set_certified")
+
+    def certified(self) -> bool:
+        """Whether the next stats-free colour-only frame uses certified walks."""
+        return self._lib.vrt_certified(self._h) == 1
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 

@@ -101,6 +101,8 @@ SIGNATURES = {
     "vrt_debug_packed_volume": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "vrt_volume_octants": (C.c_int, [C.c_void_p]),
     "vrt_set_skip_layout": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_set_certified": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_certified": (C.c_int, [C.c_void_p]),
     "vrt_render": (
         C.c_int,
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_void_p, C.c_void_p, C.POINTER(Stats)],

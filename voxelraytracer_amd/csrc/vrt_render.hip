@@ -45,6 +45,8 @@ struct KArgs {
   const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
   uint32_t* cur;         // filtered frame written here
   uint32_t* raw;         // optional: the quantised ray-trace frame (the reference's rayTrace FBO)
+  // stats-free colour-only launches: settle pixels by certified walks first (vrt_set_certified)
+  int32_t cert;
 };
 
 // ------------------------------------------------------------------ GLSL vector semantics --
@@ -990,12 +992,23 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 // whose primary hit is glass (its secondary rays start at the exact hit point) take the exact
 // path. Only the stats-free colour-only instance uses it: hit records and counters need the
 // exact walk, and textured shading reads the hit point.
+constexpr int kMaxStack = 17;
+
 #ifndef VRT_CERT
 #define VRT_CERT 1
 #endif
 #ifdef VRT_CERT_DIAG  // diagnostic build only (scripts/cert_diag.py): outcome counts per pixel
 __device__ unsigned long long g_cert_diag[16];
 #define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
+__device__ __forceinline__ void cert_diag_iters(int slot, int it) {
+  atomicAdd(&g_cert_diag[slot], (unsigned long long)it);
+  if (it > 16) atomicAdd(&g_cert_diag[slot + 1], 1ull);
+  int m = it;
+  for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, 64));
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  if (l == 0) atomicAdd(&g_cert_diag[slot + 2], (unsigned long long)m);
+}
 #else
 #define CERT_DIAG(i) ((void)0)
 #endif
@@ -1010,6 +1023,9 @@ struct CertResult {
   int cx, cy, cz;  // hit cell
   float u;         // crossing parameter of the hit
   float eu;        // bound of the exact walk's parameter error there
+#ifdef VRT_CERT_DIAG
+  int iters;
+#endif
 };
 
 __device__ __forceinline__ uint32_t cell_texel(const Ctx& c, int i, int j, int k, uint32_t obase) {
@@ -1027,21 +1043,25 @@ __device__ __forceinline__ uint32_t alt_byte(const Ctx& c, int i, int j, int k, 
   if (uint32_t(i) > n || uint32_t(j) > n || uint32_t(k) > n) return 0u;
   return cell_texel(c, i, j, k, obase) & kVoxMask;
 }
+// an event of the exact walk: shadow rays stop at opaque bytes (not air, not glass), other rays
+// at any byte other than their medium's (voxel.glsl:353, :357)
 template <bool SHADOW>
-__device__ __forceinline__ bool cert_event(uint32_t b) {
-  return SHADOW ? (b & ~2u) != 0u : b != 0u;  // shadow: opaque (not air, not glass)
+__device__ __forceinline__ bool cert_event(uint32_t b, uint32_t medium) {
+  return SHADOW ? (b & ~2u) != 0u : b != medium;
 }
-__device__ __forceinline__ int icomp(int x, int y, int z, int a) { return a == 0 ? x : (a == 1 ? y : z); }
 
-// Certified walk from P along D (every |d| in the fast-path range) with rcp = RN(1/D), starting in
-// cell (cx, cy, cz) (inside the volume), budget U = max_len - len0 (the exact walk samples the
-// crossing at u iff its len before that step is < max_len). e0: extra parameter uncertainty of
-// the start (a shadow origin is the exact primary hit point, known to +-e0 along the primary);
-// ed: extra per-axis crossing-order uncertainty from it; len0b: bound of len0.
+// Certified walk from P along D (every |d| in the fast-path range) with rcp ~ 1/D (a few ulp
+// suffice: the walk's own rounding is inside the 4e-5 allowance of the bound), starting in cell
+// (cx, cy, cz) inside the volume. U = max_len - len0: the exact walk samples the crossing at u iff
+// its len before that step is < max_len. e0: parameter uncertainty of the start (a shadow origin
+// is the exact primary hit point, known to +-e0 along the primary); ed: per-axis crossing-order
+// uncertainty from it; len0b: bound of len0. No crossing lies behind the start, so the start
+// cell's box need not cover a cell behind it: it is read from the diagonal neighbour's texel,
+// G(v + s) = F(v) - 1, i.e. the box [v, v + G s].
 template <bool SHADOW>
 __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 rcp, const float U,
                                 int cx, int cy, int cz, const float e0, const f3 ed,
-                                const float len0b) {
+                                const float len0b, const uint32_t medium) {
   CertResult r;
   r.res = CERT_UNSURE;
   r.byte = 0u;
@@ -1050,33 +1070,47 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   r.u = 0.0f;
   r.eu = 0.0f;
   const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
+  const int ux = D.x > 0.0f ? 1 : 0, uy = D.y > 0.0f ? 1 : 0, uz = D.z > 0.0f ? 1 : 0;
   const f3 ar = mk(__builtin_fabsf(rcp.x), __builtin_fabsf(rcp.y), __builtin_fabsf(rcp.z));
   const float l1 = __builtin_fabsf(D.x) + __builtin_fabsf(D.y) + __builtin_fabsf(D.z);
   const uint32_t obase = ((D.x < 0.0f ? 1u : 0u) | (D.y < 0.0f ? 2u : 0u) | (D.z < 0.0f ? 4u : 0u)) * c.ostride;
-  // rounding-bound constants (float, with a 2x safety factor on the derived bound)
+  // Rounding bounds as polynomials in the crossing parameter u (2x safety factor on 2^-24):
+  //   K(u) = u |d|_1 + 3 non-zero exact steps, sum_k len_k <= (K + 3)^2 / (2 |d|_1) + K (len0 + 1),
+  //   gam_b(u) = 2^-24 (sum len + 2 (u + len0) + (K + 3N + 8) |1/d_b|) + 4e-5 + e0 + ed_b,
+  //   gL(u) = 2^-23 sum len + 1e-4 + e0 (the length test)
   constexpr float k24 = 2.0f * 0x1p-24f;
-  const float inv2l1 = 0.5f / l1;
-  const float nterm = 3.0f * c.fn + 8.0f;
-  f3 sig = mk((float(cx + (sx > 0)) - P.x) * rcp.x, (float(cy + (sy > 0)) - P.y) * rcp.y,
-              (float(cz + (sz > 0)) - P.z) * rcp.z);
-  uint32_t tex = path_texel(c, cx, cy, cz, obase);
+  const float q2 = 0.5f * k24 * l1;
+  const float lin = 6.0f + l1 * (len0b + 1.0f), con = 18.0f / l1 + 3.0f * (len0b + 1.0f);
+  const float nterm = 3.0f * c.fn + 11.0f;
+  const f3 q1 = mk(k24 * (lin + 2.0f + ar.x * l1), k24 * (lin + 2.0f + ar.y * l1), k24 * (lin + 2.0f + ar.z * l1));
+  const float c0 = k24 * (con + 2.0f * len0b) + 4e-5f + e0;
+  const f3 q0 = mk(c0 + k24 * ar.x * nterm + ed.x, c0 + k24 * ar.y * nterm + ed.y, c0 + k24 * ar.z * nterm + ed.z);
+  const float g2 = 2.0f * q2, g1 = 2.0f * k24 * lin, g0 = 2.0f * k24 * con + 1e-4f + e0;
+  f3 sig = mk((float(cx + ux) - P.x) * rcp.x, (float(cy + uy) - P.y) * rcp.y,
+              (float(cz + uz) - P.z) * rcp.z);
+  // start: the unguarded box from the diagonal neighbour (G(v + s) + 1 in the guarded formula)
+  uint32_t tex = path_texel(c, cx + sx, cy + sy, cz + sz, obase) + (1u << kDistShift);
+#ifdef VRT_CERT_DIAG
+  r.iters = 0;
+#endif
   for (int guard = 0; guard < kCertMaxIter; ++guard) {
-    const int a = sig.y < sig.x ? (sig.z < sig.y ? 2 : 1) : (sig.z < sig.x ? 2 : 0);
-    const float s1 = a == 0 ? sig.x : (a == 1 ? sig.y : sig.z);
+#ifdef VRT_CERT_DIAG
+    r.iters = guard + 1;
+#endif
+    const float s1 = __builtin_fminf(sig.x, __builtin_fminf(sig.y, sig.z));
+    const int a = sig.x == s1 ? 0 : (sig.y == s1 ? 1 : 2);
     const float uu = gmax(s1, 0.0f);
-    const float K = uu * l1 + 3.0f;
-    const float sumlen = (K + 3.0f) * (K + 3.0f) * inv2l1 + K * (len0b + 1.0f);
-    const float gbase = k24 * (sumlen + 2.0f * (uu + len0b)) + 4e-5f + e0;
-    const float gK = k24 * (K + nterm);
-    const f3 gam = mk(gbase + gK * ar.x + ed.x, gbase + gK * ar.y + ed.y, gbase + gK * ar.z + ed.z);
-    const float gL = 2.0f * k24 * sumlen + 1e-4f + e0;
+    const f3 gam = mk(__builtin_fmaf(__builtin_fmaf(q2, uu, q1.x), uu, q0.x),
+                      __builtin_fmaf(__builtin_fmaf(q2, uu, q1.y), uu, q0.y),
+                      __builtin_fmaf(__builtin_fmaf(q2, uu, q1.z), uu, q0.z));
     // empty-space jump: the box [v - s, v + (G - 1) s] of this cell is empty and in the volume
+    // (only for rays in air: empty cells are events in a glass medium)
     const uint32_t G = tex >> kDistShift;
-    if (G >= 2u) {
+    if (G >= 2u && (SHADOW || medium == 0u)) {
       const float fg = float(G) - kCertMargin;
-      const float lx = (float(sx > 0 ? cx : cx + 1) + float(sx) * fg - P.x) * rcp.x;
-      const float ly = (float(sy > 0 ? cy : cy + 1) + float(sy) * fg - P.y) * rcp.y;
-      const float lz = (float(sz > 0 ? cz : cz + 1) + float(sz) * fg - P.z) * rcp.z;
+      const float lx = (float(cx + 1 - ux) + float(sx) * fg - P.x) * rcp.x;
+      const float ly = (float(cy + 1 - uy) + float(sy) * fg - P.y) * rcp.y;
+      const float lz = (float(cz + 1 - uz) + float(sz) * fg - P.z) * rcp.z;
       const float slim = __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, U + 2.0f));
       const float uj = slim - __builtin_fmaxf(gam.x, __builtin_fmaxf(gam.y, gam.z));
       if (uj > s1) {
@@ -1084,8 +1118,8 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
         cx = sx > 0 ? int(__builtin_floorf(x)) : int(__builtin_ceilf(x)) - 1;
         cy = sy > 0 ? int(__builtin_floorf(y)) : int(__builtin_ceilf(y)) - 1;
         cz = sz > 0 ? int(__builtin_floorf(z)) : int(__builtin_ceilf(z)) - 1;
-        sig = mk((float(cx + (sx > 0)) - P.x) * rcp.x, (float(cy + (sy > 0)) - P.y) * rcp.y,
-                 (float(cz + (sz > 0)) - P.z) * rcp.z);
+        sig = mk((float(cx + ux) - P.x) * rcp.x, (float(cy + uy) - P.y) * rcp.y,
+                 (float(cz + uz) - P.z) * rcp.z);
         tex = path_texel(c, cx, cy, cz, obase);
         continue;
       }
@@ -1093,12 +1127,13 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     // one crossing, s1 on axis a; prev = the crossing before it (the exact walk's len there)
     const f3 back = mk(sig.x - ar.x, sig.y - ar.y, sig.z - ar.z);
     const float prev = gmax(gmax(back.x, 0.0f), gmax(back.y, back.z));
+    const float gL = __builtin_fmaf(__builtin_fmaf(g2, uu, g1), uu, g0);
     if (prev > U + gL) {
       r.res = CERT_MISS;
       return r;
     }
-    const int sa = a == 0 ? sx : (a == 1 ? sy : sz);
     const int nx = cx + (a == 0 ? sx : 0), ny = cy + (a == 1 ? sy : 0), nz = cz + (a == 2 ? sz : 0);
+    const uint32_t ntex = path_texel(c, nx, ny, nz, obase);
     const float ga = a == 0 ? gam.x : (a == 1 ? gam.y : gam.z);
     // near-edge flags per other axis: ahead (crossed within the bound after s1) / behind (before)
     const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
@@ -1106,27 +1141,11 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     const bool bhx = a != 0 && back.x >= 0.0f && s1 - back.x < ga + gam.x;
     const bool bhy = a != 1 && back.y >= 0.0f && s1 - back.y < ga + gam.y;
     const bool bhz = a != 2 && back.z >= 0.0f && s1 - back.z < ga + gam.z;
-    const int nah = int(ahx) + int(ahy) + int(ahz), nbh = int(bhx) + int(bhy) + int(bhz);
-    const uint32_t ntex = path_texel(c, nx, ny, nz, obase);
+    const bool near = ahx | ahy | ahz | bhx | bhy | bhz;
     const uint32_t nb = ntex & kVoxMask;
-    if (cert_event<SHADOW>(nb)) {
-      if (SHADOW && nah + nbh == 1) {
-        // blocked whichever way the exact walk goes: near-behind b still samples nc (or nc - e_b
-        // first); near-ahead b samples nc, or cell + e_b and then nc + e_b
-        bool ok = true;
-        if (nah) {
-          const int b = ahx ? 0 : (ahy ? 1 : 2);
-          const int bx = b == 0 ? sx : 0, by = b == 1 ? sy : 0, bz = b == 2 ? sz : 0;
-          ok = cert_event<true>(alt_byte(c, cx + bx, cy + by, cz + bz, obase)) ||
-               cert_event<true>(alt_byte(c, nx + bx, ny + by, nz + bz, obase));
-        }
-        if (ok && prev + gL < U) {
-          r.res = CERT_HIT;
-          r.byte = nb;
-          return r;
-        }
-      }
-      if (nah + nbh == 0 && prev + gL < U) {
+    if (cert_event<SHADOW>(nb, medium)) {
+      if (!(prev + gL < U)) return r;  // the length test might stop the walk first
+      if (!near) {
         r.res = CERT_HIT;
         r.byte = nb;
         r.axis = a;
@@ -1135,32 +1154,49 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
         r.cz = nz;
         r.u = s1;
         r.eu = ga;
+        return r;
+      }
+      if (SHADOW && int(ahx) + int(ahy) + int(ahz) + int(bhx) + int(bhy) + int(bhz) == 1) {
+        // blocked whichever way the exact walk goes: near-behind b still samples nc (or nc - e_b
+        // first); near-ahead b samples nc, or cell + e_b and then nc + e_b
+        bool ok = true;
+        if (ahx | ahy | ahz) {
+          const int bx = ahx ? sx : 0, by = ahy ? sy : 0, bz = ahz ? sz : 0;
+          ok = cert_event<true>(alt_byte(c, cx + bx, cy + by, cz + bz, obase), 0u) ||
+               cert_event<true>(alt_byte(c, nx + bx, ny + by, nz + bz, obase), 0u);
+        }
+        if (ok) {
+          r.res = CERT_HIT;
+          r.byte = nb;
+        }
       }
       return r;  // hit or unsure
     }
-    if (nah + nbh >= 2) {  // near a corner: the 2x2x2 block ahead and the cells behind nc
-      for (int q = 1; q < 8; ++q)
-        if (cert_event<SHADOW>(alt_byte(c, cx + ((q & 1) ? sx : 0), cy + ((q & 2) ? sy : 0),
-                                        cz + ((q & 4) ? sz : 0), obase)))
+    if (near) {  // cells the exact walk may sample instead of the path's: all must be non-events
+      const int nah = int(ahx) + int(ahy) + int(ahz), nbh = int(bhx) + int(bhy) + int(bhz);
+      if (nah + nbh >= 2) {  // near a corner: the 2x2x2 block ahead and the cells behind nc
+        for (int q = 1; q < 8; ++q)
+          if (cert_event<SHADOW>(alt_byte(c, cx + ((q & 1) ? sx : 0), cy + ((q & 2) ? sy : 0),
+                                          cz + ((q & 4) ? sz : 0), obase), medium))
+            return r;
+        if ((bhx && cert_event<SHADOW>(alt_byte(c, nx - sx, ny, nz, obase), medium)) ||
+            (bhy && cert_event<SHADOW>(alt_byte(c, nx, ny - sy, nz, obase), medium)) ||
+            (bhz && cert_event<SHADOW>(alt_byte(c, nx, ny, nz - sz, obase), medium)))
           return r;
-      if ((bhx && cert_event<SHADOW>(alt_byte(c, nx - sx, ny, nz, obase))) ||
-          (bhy && cert_event<SHADOW>(alt_byte(c, nx, ny - sy, nz, obase))) ||
-          (bhz && cert_event<SHADOW>(alt_byte(c, nx, ny, nz - sz, obase))))
-        return r;
-    } else if (nah) {  // b may be crossed first, or tie: cell + e_b, nc + e_b
-      const int b = ahx ? 0 : (ahy ? 1 : 2);
-      const int bx = b == 0 ? sx : 0, by = b == 1 ? sy : 0, bz = b == 2 ? sz : 0;
-      if (cert_event<SHADOW>(alt_byte(c, cx + bx, cy + by, cz + bz, obase)) ||
-          cert_event<SHADOW>(alt_byte(c, nx + bx, ny + by, nz + bz, obase)))
-        return r;
-    } else if (nbh) {  // a may have been crossed before b: nc - e_b
-      const int b = bhx ? 0 : (bhy ? 1 : 2);
-      if (cert_event<SHADOW>(alt_byte(c, nx - (b == 0 ? sx : 0), ny - (b == 1 ? sy : 0),
-                                      nz - (b == 2 ? sz : 0), obase)))
-        return r;
+      } else if (nah) {  // b may be crossed first, or tie: cell + e_b, nc + e_b
+        const int bx = ahx ? sx : 0, by = ahy ? sy : 0, bz = ahz ? sz : 0;
+        if (cert_event<SHADOW>(alt_byte(c, cx + bx, cy + by, cz + bz, obase), medium) ||
+            cert_event<SHADOW>(alt_byte(c, nx + bx, ny + by, nz + bz, obase), medium))
+          return r;
+      } else {  // a may have been crossed before b: nc - e_b
+        if (cert_event<SHADOW>(alt_byte(c, nx - (bhx ? sx : 0), ny - (bhy ? sy : 0),
+                                        nz - (bhz ? sz : 0), obase), medium))
+          return r;
+      }
     }
-    const int na = icomp(nx, ny, nz, a);
-    if ((sa > 0 && na >= c.n) || (sa < 0 && na < 0)) {  // left the volume, moving away
+    const int na = a == 0 ? nx : (a == 1 ? ny : nz);
+    const int sa = a == 0 ? sx : (a == 1 ? sy : sz);
+    if (uint32_t(na) >= uint32_t(c.n)) {  // left the volume (moving away on axis a)
       r.res = CERT_MISS;
       return r;
     }
@@ -1176,11 +1212,99 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   return r;
 }
 
-// The whole pixel by certified walks, when it can be certified: a primary miss (sky) or a
-// non-glass primary hit whose shadow is certified or irrelevant (lit brightness == ambient).
-// Returns false (colour untouched) when the pixel must take the exact path.
-__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray, f3& color) {
-  const f3 P = ray.pos, D = ray.dir;
+// A ray that starts at a face crossing of a certified walk (a shadow or secondary ray from a hit,
+// or a walk restarted by in-volume refraction): the exact origin lies within e (parameter) of
+// X = P + u D0 along the parent direction D0, so within e |D0_fa| of the face plane (axis fa),
+// possibly on its far side. The exact walk starts in the same cell (cx, cy, cz) on the new
+// direction's side of the plane and samples the same cells if, on every other axis, X is farther
+// than its uncertainty from a plane and the new ray's first crossing of that axis comes after it
+// has left the face plane's neighbourhood (lead). ed: the crossing-order uncertainty the origin
+// adds to the new walk.
+__device__ __forceinline__ bool cert_start(const f3 X, const f3 D0, const f3 Dn, const f3 rcpn,
+                                           int fa, float e, int cx, int cy, int cz, f3& ed) {
+  ed = mk(2.0f * e * __builtin_fabsf(D0.x * rcpn.x), 2.0f * e * __builtin_fabsf(D0.y * rcpn.y),
+          2.0f * e * __builtin_fabsf(D0.z * rcpn.z));
+  const float d0a = fa == 0 ? D0.x : (fa == 1 ? D0.y : D0.z);
+  const float rna = fa == 0 ? rcpn.x : (fa == 1 ? rcpn.y : rcpn.z);
+  const float lead = (e * __builtin_fabsf(d0a) + 1e-5f) * __builtin_fabsf(rna);
+  const float wx = (float(cx + (Dn.x > 0.0f)) - X.x) * rcpn.x;
+  const float wy = (float(cy + (Dn.y > 0.0f)) - X.y) * rcpn.y;
+  const float wz = (float(cz + (Dn.z > 0.0f)) - X.z) * rcpn.z;
+  const f3 fr = mk(X.x - __builtin_floorf(X.x), X.y - __builtin_floorf(X.y), X.z - __builtin_floorf(X.z));
+  const f3 dm = mk(e * __builtin_fabsf(D0.x) + 2e-5f, e * __builtin_fabsf(D0.y) + 2e-5f,
+                   e * __builtin_fabsf(D0.z) + 2e-5f);
+  const bool okx = fa == 0 || (wx >= lead + ed.x + 1e-4f && fr.x >= dm.x && 1.0f - fr.x >= dm.x);
+  const bool oky = fa == 1 || (wy >= lead + ed.y + 1e-4f && fr.y >= dm.y && 1.0f - fr.y >= dm.y);
+  const bool okz = fa == 2 || (wz >= lead + ed.z + 1e-4f && fr.z >= dm.z && 1.0f - fr.z >= dm.z);
+  return okx && oky && okz;
+}
+
+// The cell before a hit cell along D on its crossed axis
+__device__ __forceinline__ void cell_before(const CertResult& h, const f3 D, int& x, int& y, int& z) {
+  x = h.cx - (h.axis == 0 ? (D.x > 0.0f ? 1 : -1) : 0);
+  y = h.cy - (h.axis == 1 ? (D.y > 0.0f ? 1 : -1) : 0);
+  z = h.cz - (h.axis == 2 ? (D.z > 0.0f ? 1 : -1) : 0);
+}
+
+// A Hit record for a certified hit of `ray`: point and len approximate (within h.eu along the
+// ray); only the face, voxel and (in robust positions) the probes derived from it are used
+__device__ __forceinline__ Hit cert_hit_record(const Ray& ray, const CertResult& h) {
+  Hit hh;
+  hh.found = true;
+  hh.voxel = h.byte;
+  hh.axis = h.axis;
+  hh.vidx = -1;
+  hh.len = ray.len + h.u;
+  hh.point = mk(ray.pos.x + h.u * ray.dir.x, ray.pos.y + h.u * ray.dir.y, ray.pos.z + h.u * ray.dir.z);
+  hh.normal = mk(0.0f, 0.0f, 0.0f);
+  set_comp(hh.normal, h.axis, -gsign(comp(ray.dir, h.axis)));
+  return hh;
+}
+
+// TraceWithShadow's colour update (voxel.glsl:395-418) for a certified hit of `ray`: the shadow
+// bit by a certified shadow walk from the hit, unless it cannot change the brightness (lit ==
+// ambient). false: unsure (colour untouched).
+__device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, const CertResult& h,
+                                               const Hit& hh, f3& color) {
+  const float lit = lit_brightness<false>(hh, c.sun_n, ray.dir);
+  float brightness = kAmbient;
+  if (lit != kAmbient) {  // otherwise in shadow or not, the brightness is the ambient term
+    const f3 S = c.sun_n;
+    if (!(dot3(hh.normal, S) > 0.0f) || !fast_path_ok(S)) { CERT_DIAG(5); return false; }  // back face
+    // shadow origin: the exact hit point; start cell: the air cell in front of the hit face
+    int ax, ay, az;
+    cell_before(h, ray.dir, ax, ay, az);
+    f3 ed;
+    if (!cert_start(hh.point, ray.dir, S, c.sun_rcp, h.axis, h.eu, ax, ay, az, ed)) {
+      CERT_DIAG(6);
+      return false;
+    }
+    const uint32_t n = uint32_t(c.n);
+    if (uint32_t(ax) >= n || uint32_t(ay) >= n || uint32_t(az) >= n) { CERT_DIAG(7); return false; }
+    if (cert_event<true>(cell_texel(c, ax, ay, az, 0u) & kVoxMask, 0u)) { CERT_DIAG(7); return false; }
+#ifdef VRT_ABLATE_SHADOWCERT  // timing-only ablation build: no shadow walk, wrong images
+    CertResult s;
+    s.res = CERT_MISS;
+#else
+    const CertResult s = cert_walk<true>(c, hh.point, S, c.sun_rcp, c.max_len - hh.len, ax, ay, az,
+                                         h.eu, ed, hh.len, 0u);
+#endif
+    if (s.res == CERT_UNSURE) { CERT_DIAG(8); return false; }
+    CERT_DIAG(9);
+    brightness = s.res == CERT_HIT ? kAmbient : lit;
+  } else {
+    CERT_DIAG(4);
+  }
+  apply_hit_color<false>(c, hh, ray.energy, brightness, color);
+  return true;
+}
+
+// The whole pixel by certified walks, when it can be certified: a primary miss, or a non-glass
+// primary hit with its shadow. false (colour untouched) when any walk or any derived value could
+// differ from the exact path's, or the hit is glass (its secondary rays start at the exact hit
+// point): the pixel then takes the exact path.
+__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out) {
+  const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
   const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
   // the exact walk's first planes: d < 0 ? ceil(p - 1) : floor(p + 1) (voxel.glsl:306-309)
@@ -1196,70 +1320,33 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray, f3& col
     CERT_DIAG(0);
     return false;
   }
-  const f3 rcp = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
-  const CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray.len, cx, cy, cz, 0.0f,
-                                        mk(0.0f, 0.0f, 0.0f), 0.0f);
+  // hardware reciprocals (<= 1 ulp): the certified walk only needs its own error bounded
+  const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
+#ifdef VRT_ABLATE_WALKS  // timing-only ablation build: no walks at all (sky), wrong images
+  if (P.x > -1e30f) { apply_sky_color(c, ray0, color_out); return true; }
+#endif
+  CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f,
+                                  mk(0.0f, 0.0f, 0.0f), 0.0f, 0u);
+#ifdef VRT_CERT_DIAG
+  cert_diag_iters(10, h.iters);
+#endif
   if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }
+  f3 color = color_out;
   if (h.res == CERT_MISS) {
     CERT_DIAG(2);
-    apply_sky_color(c, ray, color);
+    apply_sky_color(c, ray0, color);
+    color_out = color;
     return true;
   }
-  if (mat_id(h.byte) == 2u) { CERT_DIAG(3); return false; }  // glass: secondary rays start at the exact hit point
-  Hit hh;
-  hh.found = true;
-  hh.voxel = h.byte;
-  hh.axis = h.axis;
-  hh.vidx = -1;
-  hh.len = 0.0f;
-  hh.point = mk(0.0f, 0.0f, 0.0f);
-  hh.normal = mk(0.0f, 0.0f, 0.0f);
-  const float da = h.axis == 0 ? D.x : (h.axis == 1 ? D.y : D.z);
-  set_comp(hh.normal, h.axis, -gsign(da));
-  const float lit = lit_brightness<false>(hh, c.sun_n, D);
-  float brightness = kAmbient;
-  if (lit != kAmbient) {  // otherwise in shadow or not, the brightness is the ambient term
-    const f3 S = c.sun_n;
-    const float sa = h.axis == 0 ? S.x : (h.axis == 1 ? S.y : S.z);
-    if (!(dot3(hh.normal, S) > 0.0f) || !fast_path_ok(S)) { CERT_DIAG(5); return false; }  // back face
-    // shadow origin: the exact hit point, within eu (parameter) of P + u D along the primary;
-    // the start cell is the air cell in front of the hit face
-    const float eH = h.eu;
-    const f3 X = mk(P.x + h.u * D.x, P.y + h.u * D.y, P.z + h.u * D.z);
-    int ax = h.cx, ay = h.cy, az = h.cz;
-    if (h.axis == 0) ax -= sx;
-    else if (h.axis == 1) ay -= sy;
-    else az -= sz;
-    const f3 ed = mk(2.0f * eH * __builtin_fabsf(D.x * c.sun_rcp.x),
-                     2.0f * eH * __builtin_fabsf(D.y * c.sun_rcp.y),
-                     2.0f * eH * __builtin_fabsf(D.z * c.sun_rcp.z));
-    // the origin may lie inside the hit cell by eH |d_axis|: the shadow walk must leave that
-    // layer before it crosses any other plane, and the air cell must not block
-    const float lead = (eH * __builtin_fabsf(da) + 1e-5f) * __builtin_fabsf(1.0f / sa);
-    const int tsx = S.x > 0.0f ? 1 : 0, tsy = S.y > 0.0f ? 1 : 0, tsz = S.z > 0.0f ? 1 : 0;
-    const float wx = (float(ax + tsx) - X.x) * c.sun_rcp.x;
-    const float wy = (float(ay + tsy) - X.y) * c.sun_rcp.y;
-    const float wz = (float(az + tsz) - X.z) * c.sun_rcp.z;
-    if ((h.axis != 0 && !(wx >= lead + ed.x + 1e-4f)) || (h.axis != 1 && !(wy >= lead + ed.y + 1e-4f)) ||
-        (h.axis != 2 && !(wz >= lead + ed.z + 1e-4f))) {
-      CERT_DIAG(6);
-      return false;
-    }
-    if (uint32_t(ax) >= n || uint32_t(ay) >= n || uint32_t(az) >= n) { CERT_DIAG(7); return false; }
-    if (cert_event<true>(cell_texel(c, ax, ay, az, 0u) & kVoxMask)) { CERT_DIAG(7); return false; }
-    const CertResult s = cert_walk<true>(c, X, S, c.sun_rcp, c.max_len - (ray.len + h.u), ax, ay,
-                                         az, eH, ed, h.u);
-    if (s.res == CERT_UNSURE) { CERT_DIAG(8); return false; }
-    CERT_DIAG(9);
-    brightness = s.res == CERT_HIT ? kAmbient : lit;
-  } else {
-    CERT_DIAG(4);
+  if (mat_id(h.byte) == 2u) {  // only glass spawns secondary rays (:440-448)
+    CERT_DIAG(3);
+    return false;
   }
-  apply_hit_color<false>(c, hh, ray.energy, brightness, color);
+  if (!cert_shade_hit(c, ray0, h, cert_hit_record(ray0, h), color)) return false;
+  color_out = color;
   return true;
 }
 
-constexpr int kMaxStack = 17;
 
 // ---- RGB8 framebuffer store + temporal filter (oracle/vrt_oracle.c oracle_temporal) ----------
 // GL float -> UNORM8 store into the RGB8 FBO attachments (FrameBuffer.cpp:8): clamp to [0,1]
@@ -1363,13 +1450,109 @@ constexpr int kCntReplicas = 256;
 #define VRT_MIN_WAVES 8
 #endif
 
-// fragment main (voxel.glsl:425-452) + vertex stage (:467-472) at the pixel centre.
-// The primary ray (stack[0] of the reference) stays in registers; the scratch stack only ever
-// holds secondary rays, so pixels that spawn none never touch it.
+// Per-launch constants of the walk context
+__device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t* __restrict__ vox) {
+  c.vox = vox;
+  c.ostride = a.ostride;
+  c.n = a.n;
+  c.p = uint32_t(a.n) + 1u;
+  c.fn = a.fn;
+  c.max_len = a.max_len;
+  c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
+  c.sun_n = mk(a.sun_n[0], a.sun_n[1], a.sun_n[2]);
+  c.sun_rcp = mk(a.sun_rcp[0], a.sun_rcp[1], a.sun_rcp[2]);
+  c.time = a.time;
+  c.refl_noise = a.refl_noise;
+  c.refr_noise = a.refr_noise;
+  c.atlas = a.atlas;
+  c.atlas_mask = uint32_t(a.atlas_size) - 1u;
+  c.atlas_fs = float(a.atlas_size);
+  c.atlas_fts = float(a.atlas_tex_size);
+}
+
+// The primary ray of pixel (px, frame row py): vertex stage (voxel.glsl:467-472) evaluated at the
+// pixel centre, then stack[0] of main (:430)
+__device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px, int py) {
+  const float ndx = (2.0f * (float(px) + 0.5f)) / float(a.width) - 1.0f;
+  const float ndy = (2.0f * (float(py) + 0.5f)) / float(a.height) - 1.0f;
+  float n4[4], f4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float base = a.inv_pv[0 * 4 + i] * ndx + a.inv_pv[1 * 4 + i] * ndy;
+    n4[i] = (base + a.inv_pv[2 * 4 + i] * -1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
+    f4[i] = (base + a.inv_pv[2 * 4 + i] * 1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
+  }
+  const f3 vnear = mk(n4[0] / n4[3], n4[1] / n4[3], n4[2] / n4[3]);
+  const f3 vdir = mk(f4[0] / f4[3], f4[1] / f4[3], f4[2] / f4[3]) - vnear;
+  Ray ray;
+  ray.pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
+  ray.dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);
+  ray.len = 0.0f;
+  ray.energy = 1.0f;
+  ray.voxel = 0;
+  ray.rdepth = 0;
+  ray.tdepth = 0;
+  return ray;
+}
+
+// fragment main (voxel.glsl:425-452) with exact walks. The primary ray (stack[0] of the
+// reference) stays in registers; the scratch stack only ever holds secondary rays, so pixels that
+// spawn none never touch it.
+template <bool STATS, bool TEX>
+__device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
+                                            Counters& k, uint32_t& steps, uint32_t& flags,
+                                            int32_t& hit_vidx, float& hit_len) {
+  Ray stack[kMaxStack];
+  const int cap = a.max_refl + a.max_transp + 1;
+  int sp = 0;
+  const Hit h0 = trace_with_shadow<STATS, TEX, true>(c, ray, color, k, steps, flags);
+  hit_vidx = h0.found ? h0.vidx : -1;
+  hit_len = h0.found ? h0.len : 0.0f;
+#ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
+  if (false) {
+#else
+  if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
+#endif
+    Hit h = h0;
+    for (;;) {
+      const uint32_t m = mat_id(h.voxel);
+      if (h.found) {
+        if (mat_reflective(m) && ray.rdepth < a.max_refl) {
+          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
+          else flags |= VRT_HIT_FLAG_STACK_FULL;
+        }
+        if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
+          if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
+          else flags |= VRT_HIT_FLAG_STACK_FULL;
+        }
+      }
+      if (sp == 0) break;
+      ray = stack[--sp];
+      k.c[VRT_CNT_SECONDARY_RAYS]++;
+      h = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
+    }
+  }
+}
+
+// output of one pixel: float RGBA, or the fused reference post-pass (RGB8 ray-trace store,
+// temporal blend, RGB8 store)
+__device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__ out, size_t o,
+                                            const f3 color) {
+  if (a.cur) {
+    const uint32_t rw = pack_rgb8(color.x, color.y, color.z);
+    if (a.raw) a.raw[o] = rw;
+    a.cur[o] = temporal_blend(rw, a.prev[o], a.alpha);
+  } else {
+    out[o] = make_float4(color.x, color.y, color.z, 1.0f);
+  }
+}
+
+// One work-item per pixel, 8x8 pixels per wave: the exact path (every launch with hit records or
+// counters, textured frames, and colour-only frames when the certified pair below cannot run).
 // STATS: this instance writes hit records and/or counters. Without it the per-lane counters,
 // step/flag/tie tracking are dead code (~20 VGPRs and a VALU per DDA step freed); the rendering
 // arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, bool CERT = false>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -1392,112 +1575,38 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 
   if (valid) {
     Ctx c;
-    c.vox = vox;
-    c.ostride = a.ostride;
-    c.n = a.n;
-    c.p = uint32_t(a.n) + 1u;
-    c.fn = a.fn;
-    c.max_len = a.max_len;
-    c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
-    c.sun_n = mk(a.sun_n[0], a.sun_n[1], a.sun_n[2]);
-    c.sun_rcp = mk(a.sun_rcp[0], a.sun_rcp[1], a.sun_rcp[2]);
-    c.time = a.time;
-    c.refl_noise = a.refl_noise;
-    c.refr_noise = a.refr_noise;
-    c.atlas = a.atlas;
-    c.atlas_mask = uint32_t(a.atlas_size) - 1u;
-    c.atlas_fs = float(a.atlas_size);
-    c.atlas_fts = float(a.atlas_tex_size);
+    init_ctx(c, a, vox);
 #if VRT_LDS_AXIS
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * kAxLane];
 #endif
-
-    const int py = a.row0 + li * a.row_step;
-    const float ndx = (2.0f * (float(px) + 0.5f)) / float(a.width) - 1.0f;
-    const float ndy = (2.0f * (float(py) + 0.5f)) / float(a.height) - 1.0f;
-    float n4[4], f4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float base = a.inv_pv[0 * 4 + i] * ndx + a.inv_pv[1 * 4 + i] * ndy;
-      n4[i] = (base + a.inv_pv[2 * 4 + i] * -1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
-      f4[i] = (base + a.inv_pv[2 * 4 + i] * 1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
-    }
-    const f3 vnear = mk(n4[0] / n4[3], n4[1] / n4[3], n4[2] / n4[3]);
-    const f3 vdir = mk(f4[0] / f4[3], f4[1] / f4[3], f4[2] / f4[3]) - vnear;
-
+    const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    Ray ray;
-    ray.pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
-    ray.dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);
-    ray.len = 0.0f;
-    ray.energy = 1.0f;
-    ray.voxel = 0;
-    ray.rdepth = 0;
-    ray.tdepth = 0;
-    Ray stack[kMaxStack];
-    const int cap = a.max_refl + a.max_transp + 1;
-    int sp = 0;
-    uint32_t steps = 0, flags = 0;
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
+    uint32_t steps = 0, flags = 0;
+    int32_t hit_vidx = -1;
+    float hit_len = 0.0f;
 #if VRT_CERT
-    // stats-free colour-only frames: certified walks first, the exact path for the rest
-    if (!STATS && !TEX && a.ostride != 0u && cert_pixel(c, ray, color)) goto epilogue;
+    // stats-free colour-only frames: certified primary + shadow walks, the exact path for the rest
 #ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
-    if (!STATS && !TEX) goto epilogue;
-#endif
-#endif
-    {
-    const Hit h0 = trace_with_shadow<STATS, TEX, true>(c, ray, color, k, steps, flags);
-    const int32_t hit_vidx = h0.found ? h0.vidx : -1;
-    const float hit_len = h0.found ? h0.len : 0.0f;
-#ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
-    if (false) {
+    if (!CERT || (cert_pixel(c, ray, color), false))
 #else
-    if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
+    if (!CERT || !cert_pixel(c, ray, color))
 #endif
-      Hit h = h0;
-      for (;;) {
-        const uint32_t m = mat_id(h.voxel);
-        if (h.found) {
-          if (mat_reflective(m) && ray.rdepth < a.max_refl) {
-            if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
-            else flags |= VRT_HIT_FLAG_STACK_FULL;
-          }
-          if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
-            if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
-            else flags |= VRT_HIT_FLAG_STACK_FULL;
-          }
-        }
-        if (sp == 0) break;
-        ray = stack[--sp];
-        k.c[VRT_CNT_SECONDARY_RAYS]++;
-        h = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
-      }
-    }
+#endif
+      exact_pixel<STATS, TEX>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    const uint32_t l2 = lane_id();
+    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
     if (STATS && hits) {
-      const uint32_t l3 = lane_id();
       vrt_hit hr;
       hr.voxel_index = hit_vidx;
       hr.ray_length = hit_len;
       hr.steps = steps;
       hr.flags = flags;
-      hits[size_t(pixel_row(wave, l3)) * size_t(a.pitch) + size_t(pixel_x(wave, l3))] = hr;
+      hits[o] = hr;
     }
-    }
-#if VRT_CERT
-  epilogue:
-#endif
-    const uint32_t l2 = lane_id();
-    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
-    if (a.cur) {  // fused reference post-pass: RGB8 ray-trace store, temporal blend, RGB8 store
-      const uint32_t rw = pack_rgb8(color.x, color.y, color.z);
-      if (a.raw) a.raw[o] = rw;
-      a.cur[o] = temporal_blend(rw, a.prev[o], a.alpha);
-    } else {
-      out[o] = make_float4(color.x, color.y, color.z, 1.0f);
-    }
+    store_pixel(a, out, o, color);
   }
 
 #ifdef VRT_STAMPS
@@ -1520,6 +1629,26 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
       if (lane_id() == 0 && v) atomicAdd(slot + q, v);
     }
+  }
+}
+
+// Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
+// one wave-reduced atomic pair per wave.
+__global__ void __launch_bounds__(256) glass_share_kernel(const uint8_t* __restrict__ vox, uint64_t total,
+                                                          unsigned long long* __restrict__ out) {
+  unsigned long long g = 0, ne = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < total; i += uint64_t(gridDim.x) * 256) {
+    const uint32_t b = vox[i];
+    ne += b != 0u ? 1ull : 0ull;
+    g += mat_id(b) == 2u ? 1ull : 0ull;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    g += __shfl_xor(g, off, 64);
+    ne += __shfl_xor(ne, off, 64);
+  }
+  if ((threadIdx.x & 63u) == 0u) {
+    if (g) atomicAdd(out, g);
+    if (ne) atomicAdd(out + 1, ne);
   }
 }
 
@@ -1701,6 +1830,9 @@ struct vrt_ctx {
   int32_t n = 0;
   int32_t octants = 0;            // 8 (octant forward distances, N <= 512) or 1 (centred, N = 1024)
   int32_t layout_req = 0;         // vrt_set_skip_layout: 0 auto, 1 single centred volume, 8 octants
+  int32_t cert_req = 0;           // vrt_set_certified: 0 automatic, 1 always, -1 never
+  bool cert_auto = true;          // the automatic choice for the resident volume (volume_finish)
+  unsigned long long* d_vstats = nullptr;  // glass and non-empty voxel counts of the last upload
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
   unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of vrt_render
@@ -1811,6 +1943,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.prev = nullptr;
   a.cur = nullptr;
   a.raw = nullptr;
+  a.cert = VRT_CERT && ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto);
   return a;
 }
 
@@ -1827,8 +1960,12 @@ void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
   dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
   const bool stats = hit || cnt;
+  // stats-free colour-only frames: the certified instance when a.cert (vrt_set_certified); the
+  // plain exact instance otherwise (the certified code's registers would slow it by ~5 %)
   hipLaunchKernelGGL(a.textured ? (stats ? vrt::render_kernel<true, true> : vrt::render_kernel<false, true>)
-                                : (stats ? vrt::render_kernel<true, false> : vrt::render_kernel<false, false>),
+                                : (stats ? vrt::render_kernel<true, false>
+                                         : (a.cert ? vrt::render_kernel<false, false, true>
+                                                   : vrt::render_kernel<false, false>)),
                      grid,
                      dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
                      cnt ? ctx->d_cnt_rep : nullptr);
@@ -1898,8 +2035,17 @@ int volume_finish(vrt_ctx* ctx, hipStream_t s) {
     hipLaunchKernelGGL(vrt::pack_volume_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, da,
                        ctx->d_vox_pad, n);
   }
+  // certified walks cannot settle glass pixels (their secondary rays start at the exact hit
+  // point) and a glass pixel pays the certified primary walk before the exact path: the automatic
+  // mode turns them off when glass makes up more than 1/8 of the non-empty voxels
+  if (!ctx->d_vstats) VRT_HIP(ctx, hipMalloc(&ctx->d_vstats, 2 * sizeof(unsigned long long)));
+  VRT_HIP(ctx, hipMemsetAsync(ctx->d_vstats, 0, 2 * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(vrt::glass_share_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, vol, ctx->d_vstats);
   VRT_HIP(ctx, hipGetLastError());
   VRT_HIP(ctx, hipStreamSynchronize(s));
+  unsigned long long vs[2] = {0, 0};
+  VRT_HIP(ctx, hipMemcpy(vs, ctx->d_vstats, sizeof(vs), hipMemcpyDeviceToHost));
+  ctx->cert_auto = vs[0] * 8 <= vs[1];
   ctx->err.clear();
   return VRT_OK;
 }
@@ -1941,6 +2087,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (c->d_cnt) (void)hipFree(c->d_cnt);
   if (c->d_cnt_rep) (void)hipFree(c->d_cnt_rep);
   if (c->d_atlas) (void)hipFree(c->d_atlas);
+  if (c->d_vstats) (void)hipFree(c->d_vstats);
   free_history(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -2015,6 +2162,18 @@ int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
     return fail(ctx, VRT_ERR_INVALID, "skip layout must be 0 (auto), 1 or 8");
   ctx->layout_req = octants;
   return VRT_OK;
+}
+
+int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (mode < -1 || mode > 1) return fail(ctx, VRT_ERR_INVALID, "certified mode must be -1, 0 or 1");
+  ctx->cert_req = mode;
+  return VRT_OK;
+}
+
+int vrt_certified(const vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  return VRT_CERT && ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto) ? 1 : 0;
 }
 
 int vrt_volume_octants(const vrt_ctx* ctx) {

@@ -997,6 +997,14 @@ constexpr int kMaxStack = 17;
 #ifndef VRT_CERT
 #define VRT_CERT 1
 #endif
+// wave priority (s_setprio 0..3) of certified-instance waves that take the exact path, and of any
+// wave entering a glass pixel's bounce stack; 0 = leave the default
+#ifndef VRT_FALLBACK_PRIO
+#define VRT_FALLBACK_PRIO 0
+#endif
+#ifndef VRT_STACK_PRIO
+#define VRT_STACK_PRIO 3
+#endif
 #ifdef VRT_CERT_DIAG  // diagnostic build only (scripts/cert_diag.py): outcome counts per pixel
 __device__ unsigned long long g_cert_diag[16];
 #define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
@@ -1513,6 +1521,9 @@ __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ra
 #else
   if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
 #endif
+#if VRT_STACK_PRIO
+    __builtin_amdgcn_s_setprio(VRT_STACK_PRIO);  // bounce stacks: the longest waves of a frame
+#endif
     Hit h = h0;
     for (;;) {
       const uint32_t m = mat_id(h.voxel);
@@ -1595,7 +1606,14 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     if (!CERT || !cert_pixel(c, ray, color))
 #endif
 #endif
+    {
+#if VRT_FALLBACK_PRIO
+      // the frame's longest waves are the ones with exact work left: let the SIMD's arbiter
+      // prefer them over the certified-only waves beside them
+      if (CERT) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
+#endif
       exact_pixel<STATS, TEX>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
     if (STATS && hits) {

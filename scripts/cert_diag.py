@@ -20,7 +20,7 @@ from bench import CONFIGS  # noqa: E402
 
 NAMES = ["exact_start", "primary_unsure", "miss", "glass_hit", "hit_ambient", "back_face",
          "shadow_start_unsure", "air_cell", "shadow_unsure", "shadow_certified",
-         "primary_iters", "primary_iters_gt16", "primary_wave_max_iters"]
+         "primary_iters", "glass_tree_certified", "primary_wave_max_iters"]
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="C1,C2,C3,C4")
 args = ap.parse_args()

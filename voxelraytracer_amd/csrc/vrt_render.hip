@@ -999,6 +999,12 @@ constexpr int kMaxStack = 17;
 #endif
 // wave priority (s_setprio 0..3) of certified-instance waves that take the exact path, and of any
 // wave entering a glass pixel's bounce stack; 0 = leave the default
+// glass pixels' bounce stacks by certified walks too (cert_tree, out of line). Correct (the GPU
+// tests pass with it) and 85 % of C3's glass pixels certify, but the call site alone makes the
+// whole kernel ~3x slower (C2 0.40 vs 0.148 ms, profiles/r01_v46_ab_cert_trees.log): off
+#ifndef VRT_CERT_TREES
+#define VRT_CERT_TREES 0
+#endif
 #ifndef VRT_FALLBACK_PRIO
 #define VRT_FALLBACK_PRIO 0
 #endif
@@ -1010,7 +1016,6 @@ __device__ unsigned long long g_cert_diag[16];
 #define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
 __device__ __forceinline__ void cert_diag_iters(int slot, int it) {
   atomicAdd(&g_cert_diag[slot], (unsigned long long)it);
-  if (it > 16) atomicAdd(&g_cert_diag[slot + 1], 1ull);
   int m = it;
   for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, 64));
   uint32_t l;
@@ -1023,6 +1028,7 @@ __device__ __forceinline__ void cert_diag_iters(int slot, int it) {
 enum : int { CERT_MISS = 0, CERT_HIT = 1, CERT_UNSURE = 2 };
 constexpr float kCertMargin = 1.0f / 64.0f;  // jump boxes' forward faces pulled in (position)
 constexpr int kCertMaxIter = 1024;
+constexpr float kCertMaxOrigin = 4e-3f;  // parameter uncertainty of a secondary start beyond which: unsure
 
 struct CertResult {
   int res;
@@ -1307,11 +1313,171 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
   return true;
 }
 
+// RayMarch (voxel.glsl:302-384) of a secondary ray by certified walks; `ray` is inout as in
+// march(): leaving a glass medium refracts it in place (:357-380), and the walk restarts from
+// that crossing. (cx, cy, cz), e0, ed: the start (cert_start). Returns the first non-air event
+// (CERT_HIT), CERT_MISS or CERT_UNSURE.
+__device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz, float e0, f3 ed) {
+  CertResult h;
+  h.res = CERT_UNSURE;
+  uint32_t medium = ray.voxel;
+  int internal = 0;
+  for (int seg = 0; seg < 32; ++seg) {
+    if (!fast_path_ok(ray.dir) || !(e0 < kCertMaxOrigin)) return h;
+    const f3 rcp = mk(__builtin_amdgcn_rcpf(ray.dir.x), __builtin_amdgcn_rcpf(ray.dir.y),
+                      __builtin_amdgcn_rcpf(ray.dir.z));
+    h = cert_walk<false>(c, ray.pos, ray.dir, rcp, c.max_len - ray.len, cx, cy, cz, e0, ed, ray.len,
+                         medium);
+    if (h.res != CERT_HIT || h.byte != 0u) return h;
+    // in-volume refraction at the crossing into the air cell (h.cx, h.cy, h.cz)
+    h.res = CERT_UNSURE;
+    const Hit eh = cert_hit_record(ray, h);
+    const f3 D0 = ray.dir;
+    // the probes at point +- normal/2 (:219-220) read the exact point's cells if the point is
+    // robust on the other axes
+    const f3 fr = mk(eh.point.x - __builtin_floorf(eh.point.x), eh.point.y - __builtin_floorf(eh.point.y),
+                     eh.point.z - __builtin_floorf(eh.point.z));
+    const f3 dm = mk(h.eu * __builtin_fabsf(D0.x) + 2e-5f, h.eu * __builtin_fabsf(D0.y) + 2e-5f,
+                     h.eu * __builtin_fabsf(D0.z) + 2e-5f);
+    if ((h.axis != 0 && !(fr.x >= dm.x && 1.0f - fr.x >= dm.x)) ||
+        (h.axis != 1 && !(fr.y >= dm.y && 1.0f - fr.y >= dm.y)) ||
+        (h.axis != 2 && !(fr.z >= dm.z && 1.0f - fr.z >= dm.z)))
+      return h;
+    // position-independent directions only (RandomizeDirection's zero-noise identity)
+    const float eta = mat_refr(get_voxel(c, eh.point + eh.normal * 0.5f)) /
+                      mat_refr(get_voxel(c, eh.point - eh.normal * 0.5f));
+    const f3 rd = refract3(normalize3(D0), eh.normal, eta);
+    const bool tir = rd.x == 0.0f && rd.y == 0.0f && rd.z == 0.0f;
+    if (tir ? !(c.refl_noise == 0.0f && zero_noise_exact(reflect3(D0, eh.normal)))
+            : !(c.refr_noise == 0.0f && zero_noise_exact(rd)))
+      return h;
+    Counters kk;
+#pragma unroll
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) kk.c[q] = 0;
+    Ray nr = refraction_ray<false>(c, ray, eh, kk);
+    nr.tdepth--;
+    if (nr.voxel == medium) {
+      internal++;
+      if (internal > 10) {
+        nr.dir = D0;
+        nr.voxel = 0u;
+      }
+    }
+    medium = nr.voxel;
+    // restart cell: the crossed cell, or the one before it when the direction turned back
+    int nx = h.cx, ny = h.cy, nz = h.cz;
+    if ((comp(nr.dir, h.axis) > 0.0f) != (comp(D0, h.axis) > 0.0f)) cell_before(h, D0, nx, ny, nz);
+    if (!fast_path_ok(nr.dir)) return h;
+    const f3 rcpn = mk(__builtin_amdgcn_rcpf(nr.dir.x), __builtin_amdgcn_rcpf(nr.dir.y),
+                       __builtin_amdgcn_rcpf(nr.dir.z));
+    f3 edn;
+    if (!cert_start(eh.point, D0, nr.dir, rcpn, h.axis, h.eu, nx, ny, nz, edn)) return h;
+    ray = nr;
+    const uint32_t n = uint32_t(c.n);
+    if (uint32_t(nx) >= n || uint32_t(ny) >= n || uint32_t(nz) >= n) {
+      // out of the volume across the crossed face, moving away: TestCube ends the walk
+      h.res = CERT_MISS;
+      return h;
+    }
+    cx = nx;
+    cy = ny;
+    cz = nz;
+    e0 = h.eu;
+    ed = edn;
+  }
+  h.res = CERT_UNSURE;
+  return h;
+}
+
+struct CertSpawn {
+  Ray ray;
+  int cx, cy, cz;
+  float e0;
+  f3 ed;
+};
+
+// The bounce stack of a glass primary hit (voxel.glsl:436-451) by certified walks: every
+// secondary ray starts at an exact hit point known to its bound, so each start is checked like a
+// shadow origin (cert_start) and its uncertainty carried into the walk. Out of line: only glass
+// pixels call it, and the main walk's registers stay free of it. false: some step could differ
+// from the exact path (the pixel then takes it; colour untouched).
+__device__ __noinline__ bool cert_tree(const Ctx& c, const Ray& ray0, const CertResult& h0,
+                                       int max_refl, int max_transp, f3& color_out) {
+  f3 color = color_out;
+  Ray ray = ray0;
+  CertResult h = h0;
+  Hit hh = cert_hit_record(ray, h);
+  if (!cert_shade_hit(c, ray, h, hh, color)) return false;
+  CertSpawn stack[kMaxStack];
+  const int cap = max_refl + max_transp + 1;
+  int sp = 0;
+  for (;;) {
+    if (h.res == CERT_HIT) {
+      const uint32_t m = mat_id(h.byte);
+      if (mat_reflective(m) && ray.rdepth < max_refl && sp < cap) {
+        if (!(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))) return false;
+        CertSpawn& e = stack[sp];
+        e.ray = reflection_ray(c, ray, hh);
+        cell_before(h, ray.dir, e.cx, e.cy, e.cz);
+        const f3 rn = mk(__builtin_amdgcn_rcpf(e.ray.dir.x), __builtin_amdgcn_rcpf(e.ray.dir.y),
+                         __builtin_amdgcn_rcpf(e.ray.dir.z));
+        if (!fast_path_ok(e.ray.dir) ||
+            !cert_start(hh.point, ray.dir, e.ray.dir, rn, h.axis, h.eu, e.cx, e.cy, e.cz, e.ed))
+          return false;
+        e.e0 = h.eu;
+        sp++;
+      }
+      if (mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f &&
+          sp < cap) {
+        // probes at the hit point +- normal/2 (:219-220): robust positions only (cert_start)
+        const float eta = mat_refr(get_voxel(c, hh.point + hh.normal * 0.5f)) /
+                          mat_refr(get_voxel(c, hh.point - hh.normal * 0.5f));
+        const f3 rd = refract3(normalize3(ray.dir), hh.normal, eta);
+        const bool tir = rd.x == 0.0f && rd.y == 0.0f && rd.z == 0.0f;
+        if (tir ? !(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))
+                : !(c.refr_noise == 0.0f && zero_noise_exact(rd)))
+          return false;
+        Counters kk;
+#pragma unroll
+        for (int q = 0; q < VRT_CNT_COUNT; ++q) kk.c[q] = 0;
+        CertSpawn& e = stack[sp];
+        e.ray = refraction_ray<false>(c, ray, hh, kk);
+        e.cx = h.cx;  // into the glass cell, or (total internal reflection) back before it
+        e.cy = h.cy;
+        e.cz = h.cz;
+        if ((comp(e.ray.dir, h.axis) > 0.0f) != (comp(ray.dir, h.axis) > 0.0f))
+          cell_before(h, ray.dir, e.cx, e.cy, e.cz);
+        const f3 rn = mk(__builtin_amdgcn_rcpf(e.ray.dir.x), __builtin_amdgcn_rcpf(e.ray.dir.y),
+                         __builtin_amdgcn_rcpf(e.ray.dir.z));
+        if (!fast_path_ok(e.ray.dir) ||
+            !cert_start(hh.point, ray.dir, e.ray.dir, rn, h.axis, h.eu, e.cx, e.cy, e.cz, e.ed))
+          return false;
+        e.e0 = h.eu;
+        sp++;
+      }
+    }
+    if (sp == 0) break;
+    --sp;
+    ray = stack[sp].ray;
+    h = cert_march(c, ray, stack[sp].cx, stack[sp].cy, stack[sp].cz, stack[sp].e0, stack[sp].ed);
+    if (h.res == CERT_UNSURE) return false;
+    if (h.res == CERT_HIT) {
+      hh = cert_hit_record(ray, h);
+      if (!cert_shade_hit(c, ray, h, hh, color)) return false;
+    } else {
+      apply_sky_color(c, ray, color);
+    }
+  }
+  color_out = color;
+  return true;
+}
+
 // The whole pixel by certified walks, when it can be certified: a primary miss, or a non-glass
 // primary hit with its shadow. false (colour untouched) when any walk or any derived value could
 // differ from the exact path's, or the hit is glass (its secondary rays start at the exact hit
 // point): the pixel then takes the exact path.
-__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out) {
+__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, int max_refl, int max_transp,
+                                           f3& color_out) {
   const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
   const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
@@ -1347,6 +1513,13 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
     return true;
   }
   if (mat_id(h.byte) == 2u) {  // only glass spawns secondary rays (:440-448)
+#if VRT_CERT_TREES
+    if (cert_tree(c, ray0, h, max_refl, max_transp, color)) {
+      CERT_DIAG(11);
+      color_out = color;
+      return true;
+    }
+#endif
     CERT_DIAG(3);
     return false;
   }
@@ -1601,9 +1774,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #if VRT_CERT
     // stats-free colour-only frames: certified primary + shadow walks, the exact path for the rest
 #ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
-    if (!CERT || (cert_pixel(c, ray, color), false))
+    if (!CERT || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
 #else
-    if (!CERT || !cert_pixel(c, ray, color))
+    if (!CERT || !cert_pixel(c, ray, a.max_refl, a.max_transp, color))
 #endif
 #endif
     {

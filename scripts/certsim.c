@@ -26,6 +26,7 @@ EXPORT void cs_build(const uint8_t* vox, int n, int cap) {
   VOX = vox;
   size_t tot = (size_t)n * n * n;
   for (int o = 0; o < 8; o++) {
+    free(FO[o]);
     FO[o] = malloc(tot);
     int sx = (o & 1) ? -1 : 1, sy = (o & 2) ? -1 : 1, sz = (o & 4) ? -1 : 1;
     for (int kk = 0; kk < n; kk++) {
@@ -99,6 +100,8 @@ static cres_t cwalk(v3 P, v3 D, float U, int shadow, const int* cell0, double e0
   cres_t r;
   memset(&r, 0, sizeof r);
   float p[3] = {P.x, P.y, P.z}, d[3] = {D.x, D.y, D.z};
+  for (int a = 0; a < 3; a++)   /* the kernel's fast_path_ok: the exact walk handles the rest */
+    if (!(fabsf(d[a]) >= 0x1p-64f && fabsf(d[a]) <= 1.0e4f)) { r.res = C_UNC; r.why = 1; return r; }
   int s[3], cell[3];
   float rcp[3], arcp[3], sig[3];
   double l1 = 0.0;

@@ -942,12 +942,35 @@ __device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3
   color = mk(mixf(s1.x, color.x, a1), mixf(s1.y, color.y, a1), mixf(s1.z, color.z, a1));
 }
 
-// TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
-template <bool STATS, bool TEX, bool PRIMARY = false>
+__device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h);
+
+// TraceWithShadow (voxel.glsl:395-423) and the colour update it performs. CSH (stats-free
+// colour-only): the shadow bit by a certified walk from the exact hit point when it settles it
+// (cert_shadow_exact), and no shadow walk when it cannot change the brightness (lit == ambient).
+template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
   const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
-  if (h.found) {
+  if (CSH && h.found) {
+    static_assert(!CSH || !STATS, "certified shadows in stats-free instances only");
+    const float lit = lit_brightness<TEX>(h, c.sun_n, ray.dir);
+    int blocked = 0;
+    if (lit != kAmbient) {
+      blocked = cert_shadow_exact(c, h);
+      if (blocked < 0) {
+        Ray sr;  // GetShadowRay (:191-201)
+        sr.voxel = h.voxel;
+        sr.pos = h.point;
+        sr.dir = c.sun_n;
+        sr.len = h.len;
+        sr.energy = ray.energy;
+        sr.rdepth = 0;
+        sr.tdepth = 0;
+        blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
+      }
+    }
+    apply_hit_color<TEX>(c, h, ray.energy, blocked ? kAmbient : lit, color);
+  } else if (h.found) {
     Ray sr;  // GetShadowRay (:191-201)
     sr.voxel = h.voxel;
     sr.pos = h.point;
@@ -1004,6 +1027,15 @@ constexpr int kMaxStack = 17;
 // whole kernel ~3x slower (C2 0.40 vs 0.148 ms, profiles/r01_v46_ab_cert_trees.log): off
 #ifndef VRT_CERT_TREES
 #define VRT_CERT_TREES 0
+#endif
+// Certified shadow walks from exact hit points on the certified instance's exact path (fallback
+// pixels and bounce stacks)
+#ifndef VRT_CERT_EXACT_SHADOWS
+#define VRT_CERT_EXACT_SHADOWS 1
+#endif
+// ... and certified walks for the bounce stacks' secondary rays in air
+#ifndef VRT_CERT_SECONDARY
+#define VRT_CERT_SECONDARY 1
 #endif
 #ifndef VRT_FALLBACK_PRIO
 #define VRT_FALLBACK_PRIO 0
@@ -1472,6 +1504,55 @@ __device__ __noinline__ bool cert_tree(const Ctx& c, const Ray& ray0, const Cert
   return true;
 }
 
+// The exact walk's start cell from P along D (voxel.glsl:306-309: first planes d < 0 ? ceil(p - 1)
+// : floor(p + 1)); false when it lies outside the volume or a plane disagrees with the cell's.
+__device__ __forceinline__ bool exact_start_cell(const Ctx& c, const f3 P, const f3 D, int& cx, int& cy,
+                                                 int& cz) {
+  const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
+  cx = sx > 0 ? int(__builtin_floorf(P.x)) : int(__builtin_ceilf(P.x)) - 1;
+  cy = sy > 0 ? int(__builtin_floorf(P.y)) : int(__builtin_ceilf(P.y)) - 1;
+  cz = sz > 0 ? int(__builtin_floorf(P.z)) : int(__builtin_ceilf(P.z)) - 1;
+  const float wpx = sx > 0 ? __builtin_floorf(P.x + 1.0f) : __builtin_ceilf(P.x - 1.0f);
+  const float wpy = sy > 0 ? __builtin_floorf(P.y + 1.0f) : __builtin_ceilf(P.y - 1.0f);
+  const float wpz = sz > 0 ? __builtin_floorf(P.z + 1.0f) : __builtin_ceilf(P.z - 1.0f);
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) return false;
+  return wpx == float(cx + (sx > 0)) && wpy == float(cy + (sy > 0)) && wpz == float(cz + (sz > 0));
+}
+
+// The shadow bit of an exact hit h by a certified walk: the shadow ray starts at the exact hit
+// point h.point with len h.len (GetShadowRay, :191-201), so its start is known exactly, as a
+// primary ray's is (e0 = 0, the exact walk's own start cell). 1 blocked, 0 lit, -1 unsure.
+__device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h) {
+  const f3 S = c.sun_n;
+  int cx, cy, cz;
+  if (!fast_path_ok(S) || !exact_start_cell(c, h.point, S, cx, cy, cz)) return -1;
+  const CertResult s = cert_walk<true>(c, h.point, S, c.sun_rcp, c.max_len - h.len, cx, cy, cz, 0.0f,
+                                       mk(0.0f, 0.0f, 0.0f), h.len, 0u);
+  return s.res == CERT_UNSURE ? -1 : (s.res == CERT_HIT ? 1 : 0);
+}
+
+// A secondary ray of a bounce stack settled by certified walks. Its origin is exact (the
+// reflection or refraction ray of an exact hit), so its walk certifies as a primary's does; in an
+// air medium every event is a hit (:353), and a non-glass hit spawns no rays (:440-448). true
+// (colour updated as TraceWithShadow's, :395-423): a miss, or a non-glass hit whose shadow
+// certifies. false (colour untouched): the exact march takes the ray.
+__device__ __forceinline__ bool cert_secondary(const Ctx& c, const Ray& ray, f3& color) {
+  const f3 D = ray.dir;
+  int cx, cy, cz;
+  if (ray.voxel != 0u || !fast_path_ok(D) || !exact_start_cell(c, ray.pos, D, cx, cy, cz)) return false;
+  const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
+  const CertResult h = cert_walk<false>(c, ray.pos, D, rcp, c.max_len - ray.len, cx, cy, cz, 0.0f,
+                                        mk(0.0f, 0.0f, 0.0f), ray.len, 0u);
+  if (h.res == CERT_UNSURE) return false;
+  if (h.res == CERT_MISS) {
+    apply_sky_color(c, ray, color);
+    return true;
+  }
+  if (mat_id(h.byte) == 2u) return false;
+  return cert_shade_hit(c, ray, h, cert_hit_record(ray, h), color);
+}
+
 // The whole pixel by certified walks, when it can be certified: a primary miss, or a non-glass
 // primary hit with its shadow. false (colour untouched) when any walk or any derived value could
 // differ from the exact path's, or the hit is glass (its secondary rays start at the exact hit
@@ -1480,20 +1561,8 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, int ma
                                            f3& color_out) {
   const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
-  const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
-  // the exact walk's first planes: d < 0 ? ceil(p - 1) : floor(p + 1) (voxel.glsl:306-309)
-  const int cx = sx > 0 ? int(__builtin_floorf(P.x)) : int(__builtin_ceilf(P.x)) - 1;
-  const int cy = sy > 0 ? int(__builtin_floorf(P.y)) : int(__builtin_ceilf(P.y)) - 1;
-  const int cz = sz > 0 ? int(__builtin_floorf(P.z)) : int(__builtin_ceilf(P.z)) - 1;
-  const float wpx = sx > 0 ? __builtin_floorf(P.x + 1.0f) : __builtin_ceilf(P.x - 1.0f);
-  const float wpy = sy > 0 ? __builtin_floorf(P.y + 1.0f) : __builtin_ceilf(P.y - 1.0f);
-  const float wpz = sz > 0 ? __builtin_floorf(P.z + 1.0f) : __builtin_ceilf(P.z - 1.0f);
-  const uint32_t n = uint32_t(c.n);
-  if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) { CERT_DIAG(0); return false; }
-  if (wpx != float(cx + (sx > 0)) || wpy != float(cy + (sy > 0)) || wpz != float(cz + (sz > 0))) {
-    CERT_DIAG(0);
-    return false;
-  }
+  int cx, cy, cz;
+  if (!exact_start_cell(c, P, D, cx, cy, cz)) { CERT_DIAG(0); return false; }
   // hardware reciprocals (<= 1 ulp): the certified walk only needs its own error bounded
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
 #ifdef VRT_ABLATE_WALKS  // timing-only ablation build: no walks at all (sky), wrong images
@@ -1679,14 +1748,14 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
 // fragment main (voxel.glsl:425-452) with exact walks. The primary ray (stack[0] of the
 // reference) stays in registers; the scratch stack only ever holds secondary rays, so pixels that
 // spawn none never touch it.
-template <bool STATS, bool TEX>
+template <bool STATS, bool TEX, bool CSH = false>
 __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
   Ray stack[kMaxStack];
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
   hit_vidx = h0.found ? h0.vidx : -1;
   hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
@@ -1713,7 +1782,13 @@ __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       if (sp == 0) break;
       ray = stack[--sp];
       k.c[VRT_CNT_SECONDARY_RAYS]++;
-      h = trace_with_shadow<STATS, TEX>(c, ray, color, k, steps, flags);
+#if VRT_CERT_SECONDARY
+      if (CSH && cert_secondary(c, ray, color)) {
+        h.found = false;  // settled: a miss or a hit without secondary rays
+        continue;
+      }
+#endif
+      h = trace_with_shadow<STATS, TEX, false, CSH>(c, ray, color, k, steps, flags);
     }
   }
 }
@@ -1785,7 +1860,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       // prefer them over the certified-only waves beside them
       if (CERT) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
 #endif
-      exact_pixel<STATS, TEX>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+      exact_pixel<STATS, TEX, CERT && VRT_CERT_EXACT_SHADOWS>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));

@@ -149,14 +149,17 @@ int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants);
 
 /* ABI v6: certified walks for stats-free colour-only frames (DESIGN.md §6 "Certified walks"): a
  * pixel whose primary outcome and shadow bit provably equal the exact walks' is shaded from a
- * few empty-space jumps; every other pixel (glass hits, near-edge crossings) takes the exact walk.
- * mode 1 = always, -1 = never, 0 = automatic (default): on with the octant layout unless glass
- * makes up more than 1/8 of the resident volume's non-empty voxels (glass pixels pay the
- * certified primary walk before the exact path). Frames with hit records or counters and textured
- * frames always take the exact walks. Images are identical in every mode. */
+ * few empty-space jumps; every other pixel (glass hits, near-edge crossings) takes the exact walk,
+ * whose shadow rays and air-medium secondary rays are again certified walks when they can be.
+ * mode 1 = always, -1 = never (exact walks only), 0 = automatic (default): with the octant layout,
+ * certified pixels unless glass makes up more than 1/8 of the resident volume's non-empty voxels
+ * (glass pixels pay the certified primary walk before the exact path), certified exact-path rays
+ * always. Frames with hit records or counters and textured frames always take the exact walks.
+ * Images are identical in every mode. */
 int vrt_set_certified(vrt_ctx* ctx, int32_t mode);
 
-/* ABI v6: 1 when the next stats-free colour-only frame uses certified walks, else 0. */
+/* ABI v6: 1 when the next stats-free colour-only frame tries certified walks for whole pixels,
+ * else 0. */
 int vrt_certified(const vrt_ctx* ctx);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3

@@ -45,7 +45,8 @@ struct KArgs {
   const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
   uint32_t* cur;         // filtered frame written here
   uint32_t* raw;         // optional: the quantised ray-trace frame (the reference's rayTrace FBO)
-  // stats-free colour-only launches: settle pixels by certified walks first (vrt_set_certified)
+  // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
+  // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
   int32_t cert;
 };
 
@@ -1747,15 +1748,17 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
 
 // fragment main (voxel.glsl:425-452) with exact walks. The primary ray (stack[0] of the
 // reference) stays in registers; the scratch stack only ever holds secondary rays, so pixels that
-// spawn none never touch it.
-template <bool STATS, bool TEX, bool CSH = false>
+// spawn none never touch it. CSH: shadow bits by certified walks from the exact hit points where
+// they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
+// (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
 __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
   Ray stack[kMaxStack];
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
   hit_vidx = h0.found ? h0.vidx : -1;
   hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
@@ -1783,12 +1786,12 @@ __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       ray = stack[--sp];
       k.c[VRT_CNT_SECONDARY_RAYS]++;
 #if VRT_CERT_SECONDARY
-      if (CSH && cert_secondary(c, ray, color)) {
+      if (CSH && CSEC && cert_secondary(c, ray, color)) {
         h.found = false;  // settled: a miss or a hit without secondary rays
         continue;
       }
 #endif
-      h = trace_with_shadow<STATS, TEX, false, CSH>(c, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
     }
   }
 }
@@ -1811,7 +1814,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // STATS: this instance writes hit records and/or counters. Without it the per-lane counters,
 // step/flag/tie tracking are dead code (~20 VGPRs and a VALU per DDA step freed); the rendering
 // arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
-template <bool STATS, bool TEX, bool CERT = false>
+template <bool STATS, bool TEX, int CERT = 0>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -1849,18 +1852,18 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #if VRT_CERT
     // stats-free colour-only frames: certified primary + shadow walks, the exact path for the rest
 #ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
-    if (!CERT || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
+    if (CERT < 2 || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
 #else
-    if (!CERT || !cert_pixel(c, ray, a.max_refl, a.max_transp, color))
+    if (CERT < 2 || !cert_pixel(c, ray, a.max_refl, a.max_transp, color))
 #endif
 #endif
     {
 #if VRT_FALLBACK_PRIO
       // the frame's longest waves are the ones with exact work left: let the SIMD's arbiter
       // prefer them over the certified-only waves beside them
-      if (CERT) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
+      if (CERT == 2) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
 #endif
-      exact_pixel<STATS, TEX, CERT && VRT_CERT_EXACT_SHADOWS>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+      exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
@@ -2209,7 +2212,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.prev = nullptr;
   a.cur = nullptr;
   a.raw = nullptr;
-  a.cert = VRT_CERT && ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto);
+  a.cert = !VRT_CERT || ctx->octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || ctx->cert_auto ? 2 : 1);
   return a;
 }
 
@@ -2226,12 +2229,14 @@ void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
             unsigned long long* cnt, hipStream_t s) {
   dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
   const bool stats = hit || cnt;
-  // stats-free colour-only frames: the certified instance when a.cert (vrt_set_certified); the
-  // plain exact instance otherwise (the certified code's registers would slow it by ~5 %)
+  // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
+  // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
+  // ~5 %), exact walks only (0)
   hipLaunchKernelGGL(a.textured ? (stats ? vrt::render_kernel<true, true> : vrt::render_kernel<false, true>)
                                 : (stats ? vrt::render_kernel<true, false>
-                                         : (a.cert ? vrt::render_kernel<false, false, true>
-                                                   : vrt::render_kernel<false, false>)),
+                                         : (a.cert == 2 ? vrt::render_kernel<false, false, 2>
+                                            : a.cert == 1 ? vrt::render_kernel<false, false, 1>
+                                                          : vrt::render_kernel<false, false, 0>)),
                      grid,
                      dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
                      cnt ? ctx->d_cnt_rep : nullptr);

@@ -945,33 +945,15 @@ __device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3
 
 __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h);
 
-// TraceWithShadow (voxel.glsl:395-423) and the colour update it performs. CSH (stats-free
-// colour-only): the shadow bit by a certified walk from the exact hit point when it settles it
-// (cert_shadow_exact), and no shadow walk when it cannot change the brightness (lit == ambient).
-template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
-__device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
-                                                 uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
-  if (CSH && h.found) {
-    static_assert(!CSH || !STATS, "certified shadows in stats-free instances only");
-    const float lit = lit_brightness<TEX>(h, c.sun_n, ray.dir);
-    int blocked = 0;
-    if (lit != kAmbient) {
-      blocked = cert_shadow_exact(c, h);
-      if (blocked < 0) {
-        Ray sr;  // GetShadowRay (:191-201)
-        sr.voxel = h.voxel;
-        sr.pos = h.point;
-        sr.dir = c.sun_n;
-        sr.len = h.len;
-        sr.energy = ray.energy;
-        sr.rdepth = 0;
-        sr.tdepth = 0;
-        blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
-      }
-    }
-    apply_hit_color<TEX>(c, h, ray.energy, blocked ? kAmbient : lit, color);
-  } else if (h.found) {
+// TraceWithShadow's colour update (voxel.glsl:395-423) for the exact march's result h. CSH
+// (stats-free colour-only): the shadow bit by a certified walk from the exact hit point when it
+// settles it (cert_shadow_exact), and no shadow walk when it cannot change the brightness
+// (lit == ambient).
+template <bool STATS, bool TEX, bool CSH>
+__device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h, f3& color, Counters& k,
+                                      uint32_t& steps, uint32_t& flags) {
+  static_assert(!CSH || !STATS, "certified shadows in stats-free instances only");
+  if (h.found) {
     Ray sr;  // GetShadowRay (:191-201)
     sr.voxel = h.voxel;
     sr.pos = h.point;
@@ -980,13 +962,32 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
     sr.energy = ray.energy;
     sr.rdepth = 0;
     sr.tdepth = 0;
-    k.c[VRT_CNT_SHADOW_RAYS]++;
-    const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
-    const float brightness = in_shadow ? kAmbient : lit_brightness<TEX>(h, sr.dir, ray.dir);
+    float brightness;
+    if (CSH) {
+      const float lit = lit_brightness<TEX>(h, c.sun_n, ray.dir);
+      int blocked = 0;
+      if (lit != kAmbient) {
+        blocked = cert_shadow_exact(c, h);
+        if (blocked < 0) blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
+      }
+      brightness = blocked ? kAmbient : lit;
+    } else {
+      k.c[VRT_CNT_SHADOW_RAYS]++;
+      const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
+      brightness = in_shadow ? kAmbient : lit_brightness<TEX>(h, sr.dir, ray.dir);
+    }
     apply_hit_color<TEX>(c, h, ray.energy, brightness, color);
   } else {
     apply_sky_color(c, ray, color);
   }
+}
+
+// TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
+template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
+__device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
+                                                 uint32_t& steps, uint32_t& flags) {
+  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
+  shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
   return h;
 }
 
@@ -1037,6 +1038,10 @@ constexpr int kMaxStack = 17;
 // ... and certified walks for the bounce stacks' secondary rays in air
 #ifndef VRT_CERT_SECONDARY
 #define VRT_CERT_SECONDARY 1
+#endif
+// ... and for the rest of a march after an in-volume refraction into air
+#ifndef VRT_CERT_CONTINUATION
+#define VRT_CERT_CONTINUATION 1
 #endif
 #ifndef VRT_FALLBACK_PRIO
 #define VRT_FALLBACK_PRIO 0
@@ -1533,18 +1538,17 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h) {
   return s.res == CERT_UNSURE ? -1 : (s.res == CERT_HIT ? 1 : 0);
 }
 
-// A secondary ray of a bounce stack settled by certified walks. Its origin is exact (the
-// reflection or refraction ray of an exact hit), so its walk certifies as a primary's does; in an
-// air medium every event is a hit (:353), and a non-glass hit spawns no rays (:440-448). true
-// (colour updated as TraceWithShadow's, :395-423): a miss, or a non-glass hit whose shadow
-// certifies. false (colour untouched): the exact march takes the ray.
-__device__ __forceinline__ bool cert_secondary(const Ctx& c, const Ray& ray, f3& color) {
+// An air segment of a bounce-stack ray by a certified walk from the exact point ray.pos (len
+// ray.len) in cell (cx, cy, cz); ed: per-axis crossing-order uncertainty of the exact walk's
+// planes. In an air medium every event is a hit (:353), and a non-glass hit spawns no rays
+// (:440-448). true (colour updated as TraceWithShadow's, :395-423): a miss, or a non-glass hit
+// whose shadow certifies. false (colour untouched): the exact march goes on.
+__device__ __forceinline__ bool cert_air_segment(const Ctx& c, const Ray& ray, int cx, int cy, int cz,
+                                                 const f3 ed, f3& color) {
   const f3 D = ray.dir;
-  int cx, cy, cz;
-  if (ray.voxel != 0u || !fast_path_ok(D) || !exact_start_cell(c, ray.pos, D, cx, cy, cz)) return false;
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
-  const CertResult h = cert_walk<false>(c, ray.pos, D, rcp, c.max_len - ray.len, cx, cy, cz, 0.0f,
-                                        mk(0.0f, 0.0f, 0.0f), ray.len, 0u);
+  const CertResult h = cert_walk<false>(c, ray.pos, D, rcp, c.max_len - ray.len, cx, cy, cz, 0.0f, ed,
+                                        ray.len, 0u);
   if (h.res == CERT_UNSURE) return false;
   if (h.res == CERT_MISS) {
     apply_sky_color(c, ray, color);
@@ -1552,6 +1556,128 @@ __device__ __forceinline__ bool cert_secondary(const Ctx& c, const Ray& ray, f3&
   }
   if (mat_id(h.byte) == 2u) return false;
   return cert_shade_hit(c, ray, h, cert_hit_record(ray, h), color);
+}
+
+// A secondary ray from an exact origin (the reflection or refraction ray of an exact hit) in air:
+// its walk certifies as a primary's does
+__device__ __forceinline__ bool cert_secondary(const Ctx& c, const Ray& ray, f3& color) {
+  int cx, cy, cz;
+  if (ray.voxel != 0u || !fast_path_ok(ray.dir) || !exact_start_cell(c, ray.pos, ray.dir, cx, cy, cz))
+    return false;
+  return cert_air_segment(c, ray, cx, cy, cz, mk(0.0f, 0.0f, 0.0f), color);
+}
+
+// The rest of a march after an in-volume refraction into air at the exact crossing w.cur of axis
+// fa (march, :357-380): the exact walk goes on from pos = cur, len0 = w.len, with the first
+// planes initial_t's on the other axes and cur_fa + sign on axis fa. That plane lies within
+// delta = |(cur_fa + sign) - (k + sign)| of the lattice plane (k = rint(cur_fa)), and every later
+// axis-fa plane of the walk (cur_fa + sign at each crossing) keeps that offset: the certified walk
+// starts in the cell beyond k and takes delta |1/d_fa| (doubled) as that axis's crossing-order
+// uncertainty. The step cap (VRT_MAX_STEPS per march) must be out of reach: <= 3N + 4 more steps.
+__device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, const WalkState& w, int fa,
+                                                  f3& color) {
+  const f3 D = ray.dir, P = ray.pos;
+  if (!fast_path_ok(D) || w.it + 3u * uint32_t(c.n) + 16u > uint32_t(VRT_MAX_STEPS)) return false;
+  int cx, cy, cz;
+  const float pa = comp(P, fa), da = comp(D, fa);
+  const float k = __builtin_rintf(pa);
+  const float sa = da > 0.0f ? 1.0f : -1.0f;
+  const float delta = __builtin_fabsf((pa + sa) - (k + sa));
+  if (!(delta < 1e-3f)) return false;
+  // the other axes as a fresh walk's start; axis fa replaced below
+  {
+    const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
+    cx = sx > 0 ? int(__builtin_floorf(P.x)) : int(__builtin_ceilf(P.x)) - 1;
+    cy = sy > 0 ? int(__builtin_floorf(P.y)) : int(__builtin_ceilf(P.y)) - 1;
+    cz = sz > 0 ? int(__builtin_floorf(P.z)) : int(__builtin_ceilf(P.z)) - 1;
+    const float wpx = sx > 0 ? __builtin_floorf(P.x + 1.0f) : __builtin_ceilf(P.x - 1.0f);
+    const float wpy = sy > 0 ? __builtin_floorf(P.y + 1.0f) : __builtin_ceilf(P.y - 1.0f);
+    const float wpz = sz > 0 ? __builtin_floorf(P.z + 1.0f) : __builtin_ceilf(P.z - 1.0f);
+    if ((fa != 0 && wpx != float(cx + (sx > 0))) || (fa != 1 && wpy != float(cy + (sy > 0))) ||
+        (fa != 2 && wpz != float(cz + (sz > 0))))
+      return false;
+    const int ka = int(k) - (da > 0.0f ? 0 : 1);
+    if (fa == 0) cx = ka;
+    else if (fa == 1) cy = ka;
+    else cz = ka;
+  }
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) return false;
+  f3 ed = mk(0.0f, 0.0f, 0.0f);
+  set_comp(ed, fa, 2.0f * delta * __builtin_fabsf(__builtin_amdgcn_rcpf(da)) + 1e-6f);
+  return cert_air_segment(c, ray, cx, cy, cz, ed, color);
+}
+
+// RayMarch + TraceWithShadow of a bounce-stack ray (stats-free, colour-only) with its air
+// segments — the whole ray from its exact origin, or the rest after an in-volume refraction into
+// air — settled by certified walks where they can be (settled: colour updated, no secondary
+// rays); the exact march (as march()) otherwise.
+__device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k, uint32_t& steps,
+                          uint32_t& flags) {
+  Hit h;
+  h.found = false;
+  h.vidx = -1;
+  h.len = 0.0f;
+  h.voxel = 0;
+  h.point = mk(0.0f, 0.0f, 0.0f);
+  h.normal = h.point;
+  h.axis = 0;
+  settled = cert_secondary(c, ray, color);
+  if (settled) return h;
+  WalkState w;
+  walk_init(w, ray);
+  uint32_t medium = ray.voxel;
+  int internal = 0;
+  for (;;) {
+    int axis;
+    int32_t vidx;
+    uint32_t v;
+    const int r = walk_ray<false, false>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    if (r != WALK_EVENT) break;
+    f3 normal = mk(0.0f, 0.0f, 0.0f);
+    set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
+    if (v != 0u) {
+      h.found = true;
+      h.voxel = v;
+      h.vidx = vidx;
+      h.point = w.cur;
+      h.len = w.len;
+      h.normal = normal;
+      h.axis = axis;
+      break;
+    }
+    Hit e;
+    e.found = true;
+    e.voxel = 0;
+    e.vidx = vidx;
+    e.point = w.cur;
+    e.len = w.len;
+    e.normal = normal;
+    e.axis = axis;
+    const f3 old_dir = ray.dir;
+    ray = refraction_ray<false>(c, ray, e, k);
+    ray.tdepth--;
+    if (ray.voxel == medium) {
+      internal++;
+      if (internal > 10) {
+        ray.dir = old_dir;
+        ray.voxel = 0;
+      }
+    }
+    medium = ray.voxel;
+    w.t = initial_t(ray.dir, w.cur, ray.pos);
+    const f3 step = sign3(ray.dir);
+    const float q = ((comp(w.cur, axis) + comp(step, axis)) - comp(ray.pos, axis)) /
+                        comp(ray.dir, axis) - (w.len - ray.len);
+    set_comp(w.t, axis, q);
+#if VRT_CERT_CONTINUATION
+    if (medium == 0u && cert_continuation(c, ray, w, axis, color)) {
+      settled = true;
+      return h;
+    }
+#endif
+  }
+  return h;
 }
 
 // The whole pixel by certified walks, when it can be certified: a primary miss, or a non-glass
@@ -1786,8 +1912,14 @@ __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       ray = stack[--sp];
       k.c[VRT_CNT_SECONDARY_RAYS]++;
 #if VRT_CERT_SECONDARY
-      if (CSH && CSEC && cert_secondary(c, ray, color)) {
-        h.found = false;  // settled: a miss or a hit without secondary rays
+      if constexpr (CSH && CSEC) {
+        bool settled;
+        h = march_cert(c, ray, color, settled, k, steps, flags);
+        if (settled) {
+          h.found = false;  // a miss or a hit without secondary rays
+          continue;
+        }
+        shade<STATS, TEX, VRT_CERT_EXACT_SHADOWS>(c, ray, h, color, k, steps, flags);
         continue;
       }
 #endif

@@ -146,16 +146,14 @@ static cres_t cwalk(v3 P, v3 D, float U, int shadow, const int* cell0, double e0
       first = 0;
     }
     if (G >= 2) {
-      float slim = 1e30f;
+      /* per axis: box face of axis b minus that axis's crossing bound (the kernel's rule) */
+      float uj = U + 2.0f;
       for (int b = 0; b < 3; b++) {
         float face = (float)(s[b] > 0 ? cell[b] + G : cell[b] + 1 - G) - (float)s[b] * MARGIN;
         float l = (face - p[b]) * rcp[b];
-        if (l < slim) slim = l;
+        float lb = (float)(l - gam[b]);
+        if (lb < uj) uj = lb;
       }
-      double gmx = gam[0] > gam[1] ? gam[0] : gam[1];
-      if (gam[2] > gmx) gmx = gam[2];
-      if (slim > U + 2.0f) slim = U + 2.0f;
-      float uj = (float)(slim - gmx);
       if (uj > s1) {
         for (int b = 0; b < 3; b++) {
           float x = p[b] + uj * d[b];

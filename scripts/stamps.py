@@ -108,7 +108,14 @@ def main():
         print(cfg, json.dumps(r))
         if args.save:
             os.makedirs(args.save, exist_ok=True)
-            np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st)
+            extra = {}
+            if hasattr(lib, "vrt_debug_stamps2"):  # {time after the certified attempt, exact lanes}
+                lib.vrt_debug_stamps2.restype = C.c_int
+                lib.vrt_debug_stamps2.argtypes = [C.c_void_p, C.c_uint64]
+                st2 = np.zeros((waves, 2), dtype=np.uint64)
+                assert lib.vrt_debug_stamps2(st2.ctypes.data, st2.size) == 0
+                extra["stamps2"] = st2
+            np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st, **extra)
     return report
 
 

@@ -1163,8 +1163,11 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
       const float lx = (float(cx + 1 - ux) + float(sx) * fg - P.x) * rcp.x;
       const float ly = (float(cy + 1 - uy) + float(sy) * fg - P.y) * rcp.y;
       const float lz = (float(cz + 1 - uz) + float(sz) * fg - P.z) * rcp.z;
-      const float slim = __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, U + 2.0f));
-      const float uj = slim - __builtin_fmaxf(gam.x, __builtin_fmaxf(gam.y, gam.z));
+      // per axis: the exact walk crosses the box face of axis b within gam_b of l_b, so its steps
+      // up to min_b (l_b - gam_b) sample box cells (a common max(gam) would let one nearly
+      // parallel axis, |1/d_b| huge, stop every jump: ~90 us cell-by-cell walks at C3)
+      const float uj = __builtin_fminf(__builtin_fminf(lx - gam.x, ly - gam.y),
+                                       __builtin_fminf(lz - gam.z, U + 2.0f));
       if (uj > s1) {
         const float x = P.x + uj * D.x, y = P.y + uj * D.y, z = P.z + uj * D.z;
         cx = sx > 0 ? int(__builtin_floorf(x)) : int(__builtin_ceilf(x)) - 1;
@@ -1807,6 +1810,8 @@ __device__ __forceinline__ int pixel_row(int wave, uint32_t lane) {
 // {HW_ID, XCC_ID}, indexed by the linear wave id. Never part of the product library.
 constexpr int kMaxStampWaves = 1 << 18;
 __device__ unsigned long long g_stamps[kMaxStampWaves][3];
+// {time after the certified attempt (all lanes reconverged), lanes that took the exact path}
+__device__ unsigned long long g_stamps2[kMaxStampWaves][2];
 __device__ __forceinline__ uint32_t hw_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -1823,8 +1828,11 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // a single array would serialise ~300K same-address atomics per 1080p frame at the memory side.
 constexpr int kCntReplicas = 256;
 
+// Waves per SIMD the register budget is sized for: 7 -> 72 VGPRs. With certified walks inside the
+// bounce stacks, 64 VGPRs (8 waves) spill in the glass waves that bound a frame: 7 is 2-4 % faster
+// on C1-C4 (profiles/r01_v56_ab_occupancy.log), 6 (80 VGPRs) no better.
 #ifndef VRT_MIN_WAVES
-#define VRT_MIN_WAVES 8
+#define VRT_MIN_WAVES 7
 #endif
 
 // Per-launch constants of the walk context
@@ -1986,7 +1994,16 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
     if (CERT < 2 || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
 #else
-    if (CERT < 2 || !cert_pixel(c, ray, a.max_refl, a.max_transp, color))
+    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, a.max_refl, a.max_transp, color);
+#ifdef VRT_STAMPS
+    const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
+    if (lane_id() == 0 && wave_lin < kMaxStampWaves) {
+      g_stamps2[wave_lin][0] = t_cert;
+      g_stamps2[wave_lin][1] = n_exact;
+    }
+#endif
+    if (need_exact)
 #endif
 #endif
     {
@@ -2600,6 +2617,11 @@ int vrt_debug_cert_diag(uint64_t* out) {
 int vrt_debug_stamps(uint64_t* out, uint64_t count) {
   if (!out || count > 3ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps), count * 8) == hipSuccess ? VRT_OK
+                                                                                     : VRT_ERR_DEVICE;
+}
+int vrt_debug_stamps2(uint64_t* out, uint64_t count) {
+  if (!out || count > 2ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps2), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
 #endif

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 6
+#define VRT_ABI_VERSION 7
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -161,6 +161,16 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode);
 /* ABI v6: 1 when the next stats-free colour-only frame tries certified walks for whole pixels,
  * else 0. */
 int vrt_certified(const vrt_ctx* ctx);
+
+/* ABI v7: heavy-first tile order for stats-free colour-only launches with certified pixels
+ * (vrt_certified() == 1; DESIGN.md §6 "Tile order"): on = 1 (default), off = 0. Each launch
+ * records which of its 16x16 tiles ran a glass bounce stack; the next launch of the same band
+ * (width, rows, row0, row_step) on the same stream dispatches those tiles first, so the frame's
+ * longest waves start first. Device state per band and stream: 3 x tiles words, up to 8 bands x
+ * streams, allocated and zeroed on the launch stream at first use (recycling one synchronises the
+ * device). Launches on a stream that is being captured into a graph use dispatch order. Every
+ * tile is rendered exactly once in any case: images are identical with and without it. */
+int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
  * pairs, out = n float3. Synchronous. */

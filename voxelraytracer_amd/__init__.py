@@ -226,6 +226,10 @@ class Renderer:
         """Whether the next stats-free colour-only frame uses certified walks."""
         return self._lib.vrt_certified(self._h) == 1
 
+    def set_tile_order(self, on: bool):
+        """Heavy-first tile order for stats-free launches (default on; images are identical)."""
+        self._check(self._lib.vrt_set_tile_order(self._h, 1 if on else 0), "vrt_set_tile_order")
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 

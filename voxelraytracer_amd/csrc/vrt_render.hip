@@ -48,6 +48,11 @@ struct KArgs {
   // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
   // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
   int32_t cert;
+  // tile dispatch order (stats-free launches, vrt_set_tile_order; tile_order_begin): nullptr =
+  // dispatch order. tiles_x: tiles per row; tiles: tiles of the launch; ord_r / ord_w: the flag
+  // sets read and written by this launch (grid 2 x tiles: heavy tiles first)
+  uint32_t* order;
+  uint32_t tiles_x, tiles, ord_r, ord_w;
 };
 
 // ------------------------------------------------------------------ GLSL vector semantics --
@@ -1773,36 +1778,59 @@ static_assert(VRT_WG_WAVES == 1 || VRT_WG_WAVES == 2 || VRT_WG_WAVES == 4, "1, 2
 constexpr int kWgThreads = 64 * VRT_WG_WAVES;
 constexpr int kTileW = VRT_WG_WAVES >= 2 ? 16 : 8;
 constexpr int kTileH = VRT_WG_WAVES == 4 ? 16 : 8;
-// XCD-aware tile order: the dispatcher hands workgroup L (linear, row-major over the grid) to XCD
-// L % 8, so neighbouring tiles land on different XCDs and every XCD's L2 ends up holding the whole
+// XCD-aware tile order: the dispatcher hands workgroup L (linear over the 1-D grid) to XCD L % 8,
+// so neighbouring tiles land on different XCDs and every XCD's L2 ends up holding the whole
 // visible volume. With VRT_XCD_CHUNK = C > 0, XCD x renders runs of C consecutive tiles instead
 // (tile T = ((L/8)/C*8 + L%8)*C + (L/8)%C: a bijection on the first floor(G/8C)*8C workgroups;
 // the remainder keeps L). 0 = dispatch order.
 #ifndef VRT_XCD_CHUNK
 #define VRT_XCD_CHUNK 0
 #endif
+__device__ __forceinline__ uint32_t dispatch_tile(uint32_t L, uint32_t tiles) {
 #if VRT_XCD_CHUNK > 0
-__device__ __forceinline__ uint32_t tile_id() {
-  const uint32_t L = blockIdx.y * gridDim.x + blockIdx.x;
   constexpr uint32_t C = VRT_XCD_CHUNK;
-  const uint32_t full = (gridDim.x * gridDim.y) / (8u * C) * (8u * C);
+  const uint32_t full = tiles / (8u * C) * (8u * C);
   if (L < full) {
     const uint32_t pos = L >> 3;
     return ((pos / C) * 8u + (L & 7u)) * C + pos % C;
   }
+#endif
+  (void)tiles;
   return L;
 }
-__device__ __forceinline__ int tile_x() { return int(tile_id() % gridDim.x); }
-__device__ __forceinline__ int tile_y() { return int(tile_id() / gridDim.x); }
-#else
-__device__ __forceinline__ int tile_x() { return int(blockIdx.x); }
-__device__ __forceinline__ int tile_y() { return int(blockIdx.y); }
-#endif
-__device__ __forceinline__ int pixel_x(int wave, uint32_t lane) {
-  return tile_x() * kTileW + (wave & 1) * 8 + int(lane & 7u);
+
+// Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, the glass pixels'
+// bounce stacks; dispatched in row order, those start wherever the glass is in the image. Each
+// stats-free launch therefore records which of its tiles ran a bounce stack, and the next launch
+// of the same band (same stream) dispatches those first. The order buffer of a band holds a
+// per-tile wave counter and two per-tile flag sets: launch e reads set e % 2 (complete: written by
+// launch e - 1) and writes set (e + 1) % 2. The grid is two passes over the tiles in row order:
+// slot L < tiles renders tile L iff its flag is set, slot tiles + L renders it iff it is clear.
+// Both test the same immutable word, so every tile is rendered exactly once whatever the buffer
+// holds (a fresh zeroed buffer: no heavy tiles).
+constexpr uint32_t kOrdHdr = 0;  // the per-tile wave counters, then the two flag sets
+// the tile workgroup L renders, or ~0u (nothing to do)
+__device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L) {
+  const uint32_t* flags = a.order + kOrdHdr + a.tiles + a.ord_r * a.tiles;
+  const bool first = L < a.tiles;
+  const uint32_t j = first ? L : L - a.tiles;
+  return (flags[j] != 0u) == first ? j : ~0u;
 }
-__device__ __forceinline__ int pixel_row(int wave, uint32_t lane) {
-  return tile_y() * kTileH + (wave >> 1) * 8 + int(lane >> 3);
+// after the trace: the tile's last wave files it for the next launch
+__device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool heavy_wave) {
+  uint32_t* cnt = a.order + kOrdHdr + tile;
+  const uint32_t add = heavy_wave ? 0x10001u : 1u;
+  const uint32_t old = atomicAdd(cnt, add);
+  if ((old & 0xFFFFu) != uint32_t(VRT_WG_WAVES) - 1u) return;
+  *cnt = 0u;
+  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] = ((old + add) >> 16) != 0u ? 1u : 0u;
+}
+
+__device__ __forceinline__ int pixel_x(uint32_t tx, int wave, uint32_t lane) {
+  return int(tx) * kTileW + (wave & 1) * 8 + int(lane & 7u);
+}
+__device__ __forceinline__ int pixel_row(uint32_t ty, int wave, uint32_t lane) {
+  return int(ty) * kTileH + (wave >> 1) * 8 + int(lane >> 3);
 }
 
 #ifdef VRT_STAMPS
@@ -1885,8 +1913,9 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
 // spawn none never touch it. CSH: shadow bits by certified walks from the exact hit points where
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
+// Returns whether the pixel ran a bounce stack.
 template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
-__device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
+__device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
   Ray stack[kMaxStack];
@@ -1933,7 +1962,9 @@ __device__ __forceinline__ void exact_pixel(const KArgs& a, const Ctx& c, Ray ra
 #endif
       h = trace_with_shadow<STATS, TEX, false, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
     }
+    return true;
   }
+  return false;
 }
 
 // output of one pixel: float RGBA, or the fused reference post-pass (RGB8 ray-trace store,
@@ -1964,12 +1995,22 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   // every wave (~1.8 KB/wave of scratch writes, most of the excess WRITE_SIZE over the frame).
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
 #ifdef VRT_STAMPS
-  const uint32_t wave_lin = (blockIdx.y * gridDim.x + blockIdx.x) * VRT_WG_WAVES + wave;
+  const uint32_t wave_lin = blockIdx.x * VRT_WG_WAVES + wave;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  const int px = pixel_x(wave, lane_id());
-  const int li = pixel_row(wave, lane_id());
+  uint32_t tile = dispatch_tile(blockIdx.x, a.tiles);
+  if constexpr (!STATS) {
+    if (a.order) {
+      tile = ordered_tile(a, blockIdx.x);
+      if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
+    }
+  }
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  const int px = pixel_x(tx, wave, lane_id());
+  const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
+  bool stack = false;  // this lane ran a bounce stack (tile order)
 
   Counters k;
 #pragma unroll
@@ -2012,10 +2053,11 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       // prefer them over the certified-only waves beside them
       if (CERT == 2) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
 #endif
-      exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+      stack = exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
+                                                            hit_len);
     }
     const uint32_t l2 = lane_id();
-    const size_t o = size_t(pixel_row(wave, l2)) * size_t(a.pitch) + size_t(pixel_x(wave, l2));
+    const size_t o = size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2));
     if (STATS && hits) {
       vrt_hit hr;
       hr.voxel_index = hit_vidx;
@@ -2037,9 +2079,14 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     }
   }
 #endif
+  if constexpr (!STATS) {
+    if (a.order) {
+      const bool heavy = __ballot(stack) != 0ull;
+      if (lane_id() == 0) order_record(a, tile, heavy);
+    }
+  }
   if (STATS && counters) {
-    unsigned long long* slot =
-        counters + size_t((blockIdx.y * gridDim.x + blockIdx.x) % kCntReplicas) * VRT_CNT_COUNT;
+    unsigned long long* slot = counters + size_t(blockIdx.x % kCntReplicas) * VRT_CNT_COUNT;
 #pragma unroll
     for (int q = 0; q < VRT_CNT_COUNT; ++q) {
       unsigned long long v = k.c[q];
@@ -2240,6 +2287,9 @@ __global__ void __launch_bounds__(256) fwd_pack_kernel(const uint8_t* __restrict
 
 // ---------------------------------------------------------------------------- C-ABI context --
 
+#ifndef VRT_TILE_ORDER_DEFAULT
+#define VRT_TILE_ORDER_DEFAULT 1
+#endif
 struct vrt_ctx {
   int device = 0;
   uint8_t* d_vox = nullptr;       // canonical N^3
@@ -2250,6 +2300,7 @@ struct vrt_ctx {
   int32_t layout_req = 0;         // vrt_set_skip_layout: 0 auto, 1 single centred volume, 8 octants
   int32_t cert_req = 0;           // vrt_set_certified: 0 automatic, 1 always, -1 never
   bool cert_auto = true;          // the automatic choice for the resident volume (volume_finish)
+  bool has_glass = true;          // the resident volume has glass (bounce stacks; tile order)
   unsigned long long* d_vstats = nullptr;  // glass and non-empty voxel counts of the last upload
   float4* d_out = nullptr;
   vrt_hit* d_hit = nullptr;
@@ -2266,6 +2317,17 @@ struct vrt_ctx {
   int32_t atlas_size = 0;
   const uint8_t* atlas_src = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // heavy-first tile order (vrt_set_tile_order): one order buffer per band geometry and stream
+  struct OrderSlot {
+    int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d = nullptr;
+    uint64_t epoch = 0, tick = 0;
+  };
+  static constexpr int kOrderSlots = 8;
+  OrderSlot order[kOrderSlots];
+  uint64_t order_tick = 0;
+  bool tile_order = VRT_TILE_ORDER_DEFAULT;
   std::string err;
 };
 
@@ -2362,10 +2424,13 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.cur = nullptr;
   a.raw = nullptr;
   a.cert = !VRT_CERT || ctx->octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || ctx->cert_auto ? 2 : 1);
+  a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
+  a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
+  a.order = nullptr;
+  a.ord_r = a.ord_w = 0;
   return a;
 }
 
-// Render kernel, then (when counting) fold the replicas into `cnt` (accumulate) and re-zero them.
 void free_history(vrt_ctx* ctx) {
   for (uint32_t** b : {&ctx->d_hist[0], &ctx->d_hist[1], &ctx->d_raw}) {
     if (*b) (void)hipFree(*b);
@@ -2374,10 +2439,70 @@ void free_history(vrt_ctx* ctx) {
   ctx->hist_w = ctx->hist_h = 0;
 }
 
-void launch(const vrt_ctx* ctx, const vrt::KArgs& a, float4* out, vrt_hit* hit,
-            unsigned long long* cnt, hipStream_t s) {
-  dim3 grid((a.width + vrt::kTileW - 1) / vrt::kTileW, (a.rows + vrt::kTileH - 1) / vrt::kTileH);
+// The order buffer of this launch's band and stream (heavy-first tile order, render_kernel):
+// found, or allocated zeroed (no heavy tiles yet) on the launch stream. Not while the stream is
+// being captured into a graph (a replayed node would reuse one buffer set): dispatch order then.
+// Recycling one of the kOrderSlots buffers (more bands x streams than that) synchronises the device.
+void tile_order_begin(vrt_ctx* ctx, vrt::KArgs& a, hipStream_t s) {
+  // only where it pays: glass in the volume (no bounce stacks otherwise: the first pass would be
+  // tiles empty workgroups, C2/C4 +4 %) and certified pixels (glass-heavy volumes, where most
+  // tiles are heavy, keep dispatch order: C1 +8 %)
+  if (!ctx->tile_order || a.tiles == 0 || a.textured || a.cert != 2 || !ctx->has_glass) return;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
+  vrt_ctx::OrderSlot* slot = nullptr;
+  for (auto& o : ctx->order)
+    if (o.d && o.width == a.width && o.rows == a.rows && o.row0 == a.row0 && o.row_step == a.row_step &&
+        o.stream == s)
+      slot = &o;
+  if (!slot) {
+    slot = &ctx->order[0];
+    for (auto& o : ctx->order)
+      if (!o.d || o.tick < slot->tick) slot = &o;
+    if (slot->d) {
+      if (hipDeviceSynchronize() != hipSuccess) return;
+      (void)hipFree(slot->d);
+      slot->d = nullptr;
+    }
+    const size_t words = vrt::kOrdHdr + 3u * size_t(a.tiles);
+    if (hipMalloc(&slot->d, words * sizeof(uint32_t)) != hipSuccess) {
+      slot->d = nullptr;
+      return;
+    }
+    if (hipMemsetAsync(slot->d, 0, words * sizeof(uint32_t), s) != hipSuccess) {
+      (void)hipFree(slot->d);
+      slot->d = nullptr;
+      return;
+    }
+    slot->width = a.width;
+    slot->rows = a.rows;
+    slot->row0 = a.row0;
+    slot->row_step = a.row_step;
+    slot->stream = s;
+    slot->epoch = 0;
+  }
+  slot->tick = ++ctx->order_tick;
+  a.order = slot->d;
+  a.ord_r = uint32_t(slot->epoch & 1u);
+  a.ord_w = uint32_t((slot->epoch + 1u) & 1u);
+  slot->epoch++;
+}
+
+void free_tile_order(vrt_ctx* ctx) {
+  for (auto& o : ctx->order) {
+    if (o.d) (void)hipFree(o.d);
+    o = vrt_ctx::OrderSlot();
+  }
+}
+
+// Render kernel (1-D grid of tiles; with a tile order, two passes: heavy tiles, then the rest),
+// then (when counting)
+// fold the replicas into `cnt` (accumulate) and re-zero them.
+void launch(vrt_ctx* ctx, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
+            hipStream_t s) {
   const bool stats = hit || cnt;
+  if (!stats) tile_order_begin(ctx, a, s);
+  const dim3 grid(a.order ? 2u * a.tiles : a.tiles);
   // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
   // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
   // ~5 %), exact walks only (0)
@@ -2466,6 +2591,7 @@ int volume_finish(vrt_ctx* ctx, hipStream_t s) {
   unsigned long long vs[2] = {0, 0};
   VRT_HIP(ctx, hipMemcpy(vs, ctx->d_vstats, sizeof(vs), hipMemcpyDeviceToHost));
   ctx->cert_auto = vs[0] * 8 <= vs[1];
+  ctx->has_glass = vs[0] > 0;
   ctx->err.clear();
   return VRT_OK;
 }
@@ -2509,6 +2635,7 @@ void vrt_destroy(vrt_ctx* c) {
   if (c->d_atlas) (void)hipFree(c->d_atlas);
   if (c->d_vstats) (void)hipFree(c->d_vstats);
   free_history(c);
+  free_tile_order(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -2581,6 +2708,14 @@ int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
   if (octants != 0 && octants != 1 && octants != 8)
     return fail(ctx, VRT_ERR_INVALID, "skip layout must be 0 (auto), 1 or 8");
   ctx->layout_req = octants;
+  return VRT_OK;
+}
+
+int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
+  ctx->tile_order = on != 0;
+  ctx->err.clear();
   return VRT_OK;
 }
 

@@ -51,6 +51,9 @@ def main():
         out = torch.empty((h, w, 4), dtype=torch.float32, device=dev)
         with vrt.Renderer(0) as ren:
             ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
+            # stamps are indexed by workgroup: the heavy-first tile order's two-pass grid leaves
+            # slots without stamps (their tile is rendered by the other pass), so time dispatch order
+            ren.set_tile_order(False)
             for _ in range(5):   # warm; the stamps of the last launch are kept
                 ren.render_rows_async(cam, params, 0, h, 1, out.data_ptr(), 0, 0, stream.cuda_stream)
             torch.cuda.synchronize()
@@ -92,6 +95,9 @@ def main():
             sel = (full_rows >= b0 // 8) & (full_rows < (b0 + brows) // 8)
             with vrt.Renderer(0) as ren:
                 ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
+            # stamps are indexed by workgroup: the heavy-first tile order's two-pass grid leaves
+            # slots without stamps (their tile is rendered by the other pass), so time dispatch order
+            ren.set_tile_order(False)
                 for _ in range(3):
                     ren.render_rows_async(cam, params, b0, brows, 1, out.data_ptr(), 0, 0,
                                           stream.cuda_stream)

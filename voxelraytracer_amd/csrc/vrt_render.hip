@@ -1551,7 +1551,12 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h) {
 // planes. In an air medium every event is a hit (:353), and a non-glass hit spawns no rays
 // (:440-448). true (colour updated as TraceWithShadow's, :395-423): a miss, or a non-glass hit
 // whose shadow certifies. false (colour untouched): the exact march goes on.
-__device__ __forceinline__ bool cert_air_segment(const Ctx& c, const Ray& ray, int cx, int cy, int cz,
+#ifdef VRT_AIR_SEGMENT_NOINLINE  // A/B experiment
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+bool cert_air_segment(const Ctx& c, const Ray& ray, int cx, int cy, int cz,
                                                  const f3 ed, f3& color) {
   const f3 D = ray.dir;
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
@@ -1620,7 +1625,12 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
 // segments — the whole ray from its exact origin, or the rest after an in-volume refraction into
 // air — settled by certified walks where they can be (settled: colour updated, no secondary
 // rays); the exact march (as march()) otherwise.
-__device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k, uint32_t& steps,
+#ifdef VRT_MARCH_CERT_NOINLINE  // A/B experiment
+__device__ __noinline__
+#else
+__device__
+#endif
+Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k, uint32_t& steps,
                           uint32_t& flags) {
   Hit h;
   h.found = false;

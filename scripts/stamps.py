@@ -95,9 +95,7 @@ def main():
             sel = (full_rows >= b0 // 8) & (full_rows < (b0 + brows) // 8)
             with vrt.Renderer(0) as ren:
                 ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
-            # stamps are indexed by workgroup: the heavy-first tile order's two-pass grid leaves
-            # slots without stamps (their tile is rendered by the other pass), so time dispatch order
-            ren.set_tile_order(False)
+                ren.set_tile_order(False)
                 for _ in range(3):
                     ren.render_rows_async(cam, params, b0, brows, 1, out.data_ptr(), 0, 0,
                                           stream.cuda_stream)
@@ -121,6 +119,12 @@ def main():
                 st2 = np.zeros((waves, 2), dtype=np.uint64)
                 assert lib.vrt_debug_stamps2(st2.ctypes.data, st2.size) == 0
                 extra["stamps2"] = st2
+            if hasattr(lib, "vrt_debug_stamps3"):  # {after the exact primary trace, after the stacks}
+                lib.vrt_debug_stamps3.restype = C.c_int
+                lib.vrt_debug_stamps3.argtypes = [C.c_void_p, C.c_uint64]
+                st3 = np.zeros((waves, 2), dtype=np.uint64)
+                assert lib.vrt_debug_stamps3(st3.ctypes.data, st3.size) == 0
+                extra["stamps3"] = st3
             np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st, **extra)
     return report
 

@@ -1048,6 +1048,12 @@ constexpr int kMaxStack = 17;
 #ifndef VRT_CERT_CONTINUATION
 #define VRT_CERT_CONTINUATION 1
 #endif
+// Tile order: waves that took the exact path in nearly every lane last launch skip the certified
+// attempt. Off: C3 0.0740 vs 0.0730 ms per frame (profiles/r01_v73_skip_cert.log) — the glass
+// waves' certified attempts cost less than the exact walks the other lanes then run
+#ifndef VRT_SKIP_CERT
+#define VRT_SKIP_CERT 0
+#endif
 #ifndef VRT_FALLBACK_PRIO
 #define VRT_FALLBACK_PRIO 0
 #endif
@@ -1819,21 +1825,28 @@ __device__ __forceinline__ uint32_t dispatch_tile(uint32_t L, uint32_t tiles) {
 // Both test the same immutable word, so every tile is rendered exactly once whatever the buffer
 // holds (a fresh zeroed buffer: no heavy tiles).
 constexpr uint32_t kOrdHdr = 0;  // the per-tile wave counters, then the two flag sets
-// the tile workgroup L renders, or ~0u (nothing to do)
-__device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L) {
+// The tile workgroup L renders, or ~0u (nothing to do); flag: the tile's word of the last launch,
+// bit 0 heavy (ran a bounce stack), bit 1 + w: wave w took the exact path in nearly every lane
+// (it then skips the certified attempt, whose work those lanes would throw away)
+__device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L, uint32_t& flag) {
   const uint32_t* flags = a.order + kOrdHdr + a.tiles + a.ord_r * a.tiles;
   const bool first = L < a.tiles;
   const uint32_t j = first ? L : L - a.tiles;
-  return (flags[j] != 0u) == first ? j : ~0u;
+  flag = flags[j];
+  return ((flag & 1u) != 0u) == first ? j : ~0u;
 }
 // after the trace: the tile's last wave files it for the next launch
-__device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool heavy_wave) {
+// (counter: bits 0-7 waves done, 8-15 heavy waves, 16 + w wave w mostly exact)
+__device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool heavy_wave, int wave,
+                                             bool mostly_exact) {
   uint32_t* cnt = a.order + kOrdHdr + tile;
-  const uint32_t add = heavy_wave ? 0x10001u : 1u;
+  const uint32_t add = 1u | (heavy_wave ? 0x100u : 0u) | (mostly_exact ? 0x10000u << wave : 0u);
   const uint32_t old = atomicAdd(cnt, add);
-  if ((old & 0xFFFFu) != uint32_t(VRT_WG_WAVES) - 1u) return;
+  if ((old & 0xFFu) != uint32_t(VRT_WG_WAVES) - 1u) return;
   *cnt = 0u;
-  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] = ((old + add) >> 16) != 0u ? 1u : 0u;
+  const uint32_t all = old + add;
+  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] =
+      ((all & 0xFF00u) != 0u ? 1u : 0u) | ((all >> 16) & 0xFu) << 1;
 }
 
 __device__ __forceinline__ int pixel_x(uint32_t tx, int wave, uint32_t lane) {
@@ -1850,6 +1863,7 @@ constexpr int kMaxStampWaves = 1 << 18;
 __device__ unsigned long long g_stamps[kMaxStampWaves][3];
 // {time after the certified attempt (all lanes reconverged), lanes that took the exact path}
 __device__ unsigned long long g_stamps2[kMaxStampWaves][2];
+
 __device__ __forceinline__ uint32_t hw_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -1918,6 +1932,12 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
   return ray;
 }
 
+#ifdef VRT_STAMPS
+// Diagnostic build only: per wave {time after the exact primary trace, after the bounce stacks}
+constexpr int kMaxStampWaves3 = 1 << 18;
+__device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
+#endif
+
 // fragment main (voxel.glsl:425-452) with exact walks. The primary ray (stack[0] of the
 // reference) stays in registers; the scratch stack only ever holds secondary rays, so pixels that
 // spawn none never touch it. CSH: shadow bits by certified walks from the exact hit points where
@@ -1932,6 +1952,14 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
   const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
+#ifdef VRT_STAMPS
+  const uint32_t st_wave = blockIdx.x * VRT_WG_WAVES + (threadIdx.x >> 6);
+  {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (lane_id() == uint32_t(__builtin_amdgcn_readfirstlane(int(lane_id()))) && st_wave < kMaxStampWaves3)
+      g_stamps3[st_wave][0] = t;
+  }
+#endif
   hit_vidx = h0.found ? h0.vidx : -1;
   hit_len = h0.found ? h0.len : 0.0f;
 #ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
@@ -1972,6 +2000,13 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
 #endif
       h = trace_with_shadow<STATS, TEX, false, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
     }
+#ifdef VRT_STAMPS
+    {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (lane_id() == uint32_t(__builtin_amdgcn_readfirstlane(int(lane_id()))) && st_wave < kMaxStampWaves3)
+        g_stamps3[st_wave][1] = t;
+    }
+#endif
     return true;
   }
   return false;
@@ -2009,10 +2044,18 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   uint32_t tile = dispatch_tile(blockIdx.x, a.tiles);
+  bool skip_cert = false;  // tile order: this wave was nearly all exact last launch
   if constexpr (!STATS) {
     if (a.order) {
-      tile = ordered_tile(a, blockIdx.x);
+      uint32_t flag;
+      tile = ordered_tile(a, blockIdx.x, flag);
       if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
+#if VRT_SKIP_CERT
+      skip_cert = ((flag >> (1 + wave)) & 1u) != 0u;
+#endif
+#ifdef VRT_HEAVY_PRIO  // A/B experiment: heavy tiles' waves at raised priority from the start
+      if (blockIdx.x < a.tiles) __builtin_amdgcn_s_setprio(VRT_HEAVY_PRIO);
+#endif
     }
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
@@ -2020,7 +2063,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const int px = pixel_x(tx, wave, lane_id());
   const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
-  bool stack = false;  // this lane ran a bounce stack (tile order)
+  bool stack = false;       // this lane ran a bounce stack (tile order)
+  bool exact_lane = false;  // this lane took the exact path (tile order)
 
   Counters k;
 #pragma unroll
@@ -2045,7 +2089,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
     if (CERT < 2 || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
 #else
-    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, a.max_refl, a.max_transp, color);
+    const bool need_exact = CERT < 2 || skip_cert || !cert_pixel(c, ray, a.max_refl, a.max_transp, color);
+    exact_lane = need_exact;
 #ifdef VRT_STAMPS
     const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
     const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
@@ -2092,7 +2137,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   if constexpr (!STATS) {
     if (a.order) {
       const bool heavy = __ballot(stack) != 0ull;
-      if (lane_id() == 0) order_record(a, tile, heavy);
+      const bool mostly_exact = VRT_SKIP_CERT && __builtin_popcountll(__ballot(exact_lane)) >= 56;
+      if (lane_id() == 0) order_record(a, tile, heavy, wave, mostly_exact);
     }
   }
   if (STATS && counters) {
@@ -2767,6 +2813,11 @@ int vrt_debug_stamps(uint64_t* out, uint64_t count) {
 int vrt_debug_stamps2(uint64_t* out, uint64_t count) {
   if (!out || count > 2ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps2), count * 8) == hipSuccess ? VRT_OK
+                                                                                     : VRT_ERR_DEVICE;
+}
+int vrt_debug_stamps3(uint64_t* out, uint64_t count) {
+  if (!out || count > 2ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps3), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
 #endif

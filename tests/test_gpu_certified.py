@@ -150,3 +150,25 @@ def test_certified_modes(renderer):
             renderer.set_certified(2)
     finally:
         renderer.set_certified(1)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_certified_glass_slabs_continuations(renderer, seed):
+    """Bounce stacks through glass slabs and rods: refraction rays cross the glass and leave it by
+    in-volume refraction (the certified march continuation, with the refracted axis' plane offset),
+    at lattice-aligned cameras and views along lattice diagonals; thick slabs give total internal
+    reflection."""
+    n = [32, 64, 32, 64][seed]
+    vox = np.zeros((n, n, n), np.uint8)
+    vox[:, : n // 8, :] = 1                                      # floor
+    t = [1, 2, 3, 5][seed]
+    vox[n // 3: n // 3 + t, n // 8: n // 2, n // 4: 3 * n // 4] = 2   # upright slab, thickness t
+    vox[n // 4: 3 * n // 4, n // 2: n // 2 + t, n // 2] = 2            # a rod along x
+    vox[2 * n // 3, n // 8: n // 3, n // 5: n // 5 + t] = 3            # an opaque post
+    if seed % 2:
+        vox[n // 2: n // 2 + 4, n // 3: n // 3 + 4, n // 2: n // 2 + 4] = 2   # a glass block
+    vox = vox.reshape(-1)
+    for pos, rot in LATTICE[:6]:
+        check_same(renderer, vox, n, 64, 48, 4, 4, pos=pos, rot=rot)
+    check_same(renderer, vox, n, 64, 48, 4, 4, pos=(0.5, 2.0, -6.0), rot=(-15.0, 20.0, 0.0),
+               refraction_noise=0.02, time=1.5)

@@ -1054,6 +1054,18 @@ constexpr int kMaxStack = 17;
 #ifndef VRT_SKIP_CERT
 #define VRT_SKIP_CERT 0
 #endif
+// Packed bounce-stack entries (9 words, scratch 1008 -> 880 B/lane): neutral on C1-C4
+// (profiles/r01_v75_ab_packed_stack.log), off
+#ifndef VRT_PACKED_STACK
+#define VRT_PACKED_STACK 0
+#endif
+#if VRT_PACKED_STACK
+#define VRT_STACK_PUSH(r) pack_ray(r)
+#define VRT_STACK_POP(p) unpack_ray(p)
+#else
+#define VRT_STACK_PUSH(r) (r)
+#define VRT_STACK_POP(p) (p)
+#endif
 #ifndef VRT_FALLBACK_PRIO
 #define VRT_FALLBACK_PRIO 0
 #endif
@@ -1932,6 +1944,34 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
   return ray;
 }
 
+// A bounce-stack entry in scratch: a Ray with its medium byte and both depths in one word (9
+// words instead of 11 per push and pop)
+struct StackRay {
+  f3 pos, dir;
+  float len, energy;
+  uint32_t packed;  // voxel (8 bits) | rdepth (signed 12) << 8 | tdepth (signed 12) << 20
+};
+__device__ __forceinline__ StackRay pack_ray(const Ray& r) {
+  StackRay p;
+  p.pos = r.pos;
+  p.dir = r.dir;
+  p.len = r.len;
+  p.energy = r.energy;
+  p.packed = (r.voxel & 0xFFu) | (uint32_t(r.rdepth) & 0xFFFu) << 8 | (uint32_t(r.tdepth) & 0xFFFu) << 20;
+  return p;
+}
+__device__ __forceinline__ Ray unpack_ray(const StackRay& p) {
+  Ray r;
+  r.pos = p.pos;
+  r.dir = p.dir;
+  r.len = p.len;
+  r.energy = p.energy;
+  r.voxel = p.packed & 0xFFu;
+  r.rdepth = int32_t(p.packed << 12) >> 20;
+  r.tdepth = int32_t(p.packed) >> 20;
+  return r;
+}
+
 #ifdef VRT_STAMPS
 // Diagnostic build only: per wave {time after the exact primary trace, after the bounce stacks}
 constexpr int kMaxStampWaves3 = 1 << 18;
@@ -1948,7 +1988,11 @@ template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
+#if VRT_PACKED_STACK
+  StackRay stack[kMaxStack];
+#else
   Ray stack[kMaxStack];
+#endif
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
   const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
@@ -1975,16 +2019,16 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       const uint32_t m = mat_id(h.voxel);
       if (h.found) {
         if (mat_reflective(m) && ray.rdepth < a.max_refl) {
-          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
+          if (sp < cap) stack[sp++] = VRT_STACK_PUSH(reflection_ray(c, ray, h));
           else flags |= VRT_HIT_FLAG_STACK_FULL;
         }
         if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
-          if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
+          if (sp < cap) stack[sp++] = VRT_STACK_PUSH(refraction_ray<TEX>(c, ray, h, k));
           else flags |= VRT_HIT_FLAG_STACK_FULL;
         }
       }
       if (sp == 0) break;
-      ray = stack[--sp];
+      ray = VRT_STACK_POP(stack[--sp]);
       k.c[VRT_CNT_SECONDARY_RAYS]++;
 #if VRT_CERT_SECONDARY
       if constexpr (CSH && CSEC) {

@@ -27,10 +27,11 @@ build/bin/vrt_headless: examples/headless_app.cpp include/vrt.h $(LIBDIR)/libvrt
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ examples/headless_app.cpp -L$(LIBDIR) -lvrt \
 	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 
-# experiment variants for scripts/ab.py: make variant NAME=w5 DEFS="-DVRT_MIN_WAVES=5"
+# experiment / diagnostic variants for scripts/ab.py, stamps.py, cert_diag.py (never the product
+# library): make variant NAME=w6 DEFS="-DVRT_MIN_WAVES=6", NAME=stamps DEFS=-DVRT_STAMPS
 variant: $(SRC) include/vrt.h
 	mkdir -p build/variants
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/libvrt_$(NAME).so $(SRC) -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) $(HIPFLAGS) -DVRT_DIAGNOSTIC_BUILD $(DEFS) -shared -o build/variants/libvrt_$(NAME).so $(SRC) -Wl,-rpath,/opt/rocm/lib
 
 asm: $(SRC) include/vrt.h
 	mkdir -p build/asm

@@ -54,7 +54,10 @@ def parse():
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the oracle CPU baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (0: all the host grants, see host_cores)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-timing check of the timed frame against the exact instance")
     ap.add_argument("--output", default="rgba8", choices=["rgba8", "f32"],
                     help="rgba8: the reference's stored frame (RGB8 store + temporal filter fused "
                          "into the kernel); f32: the float RGBA frame of vrt_render")
@@ -77,9 +80,39 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores():
+    """CPU counts of this host as seen by this process: the affinity mask, lscpu's logical CPUs,
+    the cgroup CPU quota (cpu.max) and OMP_NUM_THREADS; the baseline runs on the smallest of the
+    ones that are set (on the GPU box the affinity mask lists the whole machine while the job's
+    share is its cgroup quota)."""
+    import subprocess
+
+    aff = len(os.sched_getaffinity(0))
+    try:
+        out = subprocess.run(["lscpu", "-p=CPU"], capture_output=True, text=True, timeout=10).stdout
+        lscpu = sum(1 for l in out.splitlines() if l and not l.startswith("#"))
+    except Exception:
+        lscpu = None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    use = min(x for x in (aff, quota, omp) if x)
+    return dict(threads=use, affinity_cpus=aff, lscpu_cpus=lscpu, cgroup_cpu_quota=quota,
+                omp_num_threads=omp)
+
+
 def cpu_baseline(cam, vox, n, params, budget_s, threads):
-    """The oracle (scalar C restatement, `port`) on host cores over a bounded sample of the same
-    frame: whole frames if they fit the budget, else every k-th row band."""
+    """The oracle (scalar C restatement of voxel.glsl, `port`) on host cores over a bounded sample
+    of the same frame: whole frames if they fit the budget, else every k-th row band. It replays
+    every DDA step of the reference's walk (the GPU's certified walks skip most of them), so the
+    ratio mixes algorithm and hardware. Also returns the last whole oracle frame (float RGBA, or
+    None), the checker of the GPU frame in main()."""
     import oracle
 
     h = cam.height
@@ -89,10 +122,11 @@ def cpu_baseline(cam, vox, n, params, budget_s, threads):
     est_frame = probe * 16
     rays = 0
     frames = 0
+    frame = None
     t0 = time.perf_counter()
     if est_frame * 1.5 <= budget_s:
         while True:
-            _, _, c = oracle.render(cam, vox, n, params, threads=threads)
+            frame, _, c = oracle.render(cam, vox, n, params, threads=threads)
             rays += c["primary_rays"] + c["secondary_rays"] + c["shadow_rays"]
             frames += 1
             if time.perf_counter() - t0 + est_frame > budget_s:
@@ -106,7 +140,18 @@ def cpu_baseline(cam, vox, n, params, budget_s, threads):
         sample = f"every {step}th row of one frame ({h // step} rows)"
     dt = time.perf_counter() - t0
     return dict(value=rays / dt / 1e6, unit="Mrays/s", cores=threads, kind="port",
-                sample=f"oracle/vrt_oracle.c -O3, {threads} threads, {sample}, {dt:.1f} s")
+                sample=f"oracle/vrt_oracle.c -O3 (exact walks), {threads} threads, {sample}, "
+                       f"{dt:.1f} s"), frame
+
+
+def lib_sha256():
+    """SHA-256 of the loaded product library (profiles are stamped with it)."""
+    import hashlib
+
+    from voxelraytracer_amd import abi
+
+    with open(abi.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def main():
@@ -187,12 +232,19 @@ def main():
     tiler = FrameTiler(w, frame_h, render_band, dev,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts)
 
-    # One counted band per rank (outside the timed region): rays and algorithmic bytes per frame.
+    # One counted launch per part (outside the timed region, the exact STATS instance): rays and
+    # algorithmic bytes per frame and per launch.
     cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device=dev)
-    launch(tiler.row0, tiler.rows, tiler.step, tiler.bands[0], tiler.bands[-1], cnt.data_ptr())
-    torch.cuda.synchronize(dev)
-    for band in tiler.bands:
-        band.zero_()
+    part_bytes = []
+    own = None
+    for (row0, rows, step) in tiler.specs:
+        pc = torch.zeros_like(cnt)
+        scratch = torch.zeros((rows, w, 4), dtype=torch.uint8 if rgba8 else torch.float32, device=dev)
+        launch(row0, rows, step, scratch, scratch, pc.data_ptr())
+        torch.cuda.synchronize(dev)
+        pcd = vrt.counters_dict(pc.cpu().tolist())
+        part_bytes.append(vrt.algorithmic_bytes(pcd, 8 if rgba8 else 16))
+        cnt += pc
     own = vrt.counters_dict(cnt.cpu().tolist())
     if world > 1:
         dist.all_reduce(cnt)
@@ -237,32 +289,98 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, frame_ms_max = t.tolist()
 
+    # Check of the timed path (after all timing): one more frame through the same FrameTiler
+    # (parts on their streams, pitched in place, tile order seeded by the frames before it,
+    # certified walks) against the exact STATS instance (exact walks, counters on) rendering the
+    # same rows from a copy of the same history: the stored bytes (or float frame) must be equal.
+    verify = None
+    prev_full = None
+    if not args.no_verify:
+        nb = len(tiler.bands)
+        last = tiler.bands[(tiler.k - 1) % nb]
+        prev_parts = [tiler._part_buffers(s_, last, last)[0].clone() for s_ in range(parts)]
+        if world == 1 and tiler.frame_buf is not None:
+            prev_full = tiler.frame_buf.clone()
+        tiler.frame()
+        tiler.finish()
+        torch.cuda.synchronize(dev)
+        newest = tiler.bands[(tiler.k - 1) % nb]
+        bad = 0
+        total = 0
+        vc = torch.zeros_like(cnt)
+        for s_, (row0, rows, step) in enumerate(tiler.specs):
+            got = tiler._part_buffers(s_, newest, newest)[0].contiguous()
+            ref = torch.zeros_like(got)
+            prev_c = prev_parts[s_].contiguous()
+            launch(row0, rows, step, ref, prev_c, vc.data_ptr())   # counters on: STATS instance
+            torch.cuda.synchronize(dev)
+            bad += int((got != ref).sum().item())
+            total += got.numel()
+        verify = {"verified": bad == 0, "mismatched_elements": bad, "elements": total,
+                  "against": "exact walks (STATS instance, counters on) on a copy of the same "
+                             "history, every part of this rank"}
+        ok = torch.tensor([1 if bad == 0 else 0], device=dev)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        verify["verified_all_ranks"] = bool(ok.item())
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel: the algorithmic bytes of THIS rank's band per launch
-        # over its mean launch time (HIP events on the stream the kernel is launched on)
+        # Roofline of the dominant kernel, per launch (as rocprofv3 reports it): this rank's
+        # algorithmic bytes of one part launch over the mean launch duration. The algorithmic
+        # bytes are the reference's: 1 B per DDA step of its walk + 2 B per refraction probe + the
+        # pixel bytes; the certified walks read only a few texels per pixel, so this
+        # is a reference-normalised rate, not a bandwidth. What binds the kernel is VALU issue and
+        # dependency latency (valu_issue below); the measured HBM traffic is hbm_frac.
         own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
-        achieved = own_bytes / (frame_gpu_ms * 1e-3) / 1e9
-        traffic = None
+        bytes_per_launch = float(np.mean(part_bytes))
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        lib_hash = lib_sha256()
+        traffic = traffic_frame = hbm_frac = None
         valu = None
+        prof_note = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{args.output}.json")
         if os.path.exists(pmc) and world == 1 and args.shading == "color":
             with open(pmc) as f:
                 pj = json.load(f)
-            traffic = pj.get("hbm_bytes_per_launch")
-            if pj.get("valu_insts_per_launch"):
-                # VALU-issue bound of the same frame: wave64 VALU ops take 2 cycles on a SIMD32;
-                # 1024 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
-                floor_ms = pj["valu_insts_per_launch"] * 2 / (1024 * 2.4e9) * 1e3
-                valu = {"insts_per_frame": pj["valu_insts_per_launch"],
-                        "issue_bound_ms": round(floor_ms, 4),
-                        "frac": round(floor_ms / frame_gpu_ms, 4),
-                        "source": os.path.relpath(pmc, ROOT)}
+            if pj.get("lib_sha256") != lib_hash:
+                prof_note = (f"{os.path.relpath(pmc, ROOT)} was measured on another build "
+                             f"({str(pj.get('lib_sha256'))[:12]} != {lib_hash[:12]}): not used")
+            elif pj.get("parts") != parts:
+                prof_note = f"{os.path.relpath(pmc, ROOT)} has parts={pj.get('parts')}: not used"
+            else:
+                traffic = int(pj["hbm_bytes_per_launch"])
+                traffic_frame = traffic * parts
+                hbm_frac = round(traffic_frame / (frame_gpu_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)
+                if pj.get("valu_insts_per_launch"):
+                    # VALU-issue bound of the same frame: a wave64 VALU op takes 2 cycles on a
+                    # SIMD32; 1024 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+                    insts = pj["valu_insts_per_launch"] * parts
+                    floor_ms = insts * 2 / (1024 * 2.4e9) * 1e3
+                    valu = {"insts_per_frame": int(insts), "issue_bound_ms": round(floor_ms, 4),
+                            "frac": round(floor_ms / frame_gpu_ms, 4),
+                            "source": os.path.relpath(pmc, ROOT)}
+                prof_note = pj.get("source")
         cpu = None
+        oracle_check = None
         if world == 1 and args.cpu_seconds > 0:
+            cores = host_cores()
+            threads = args.cpu_threads or cores["threads"]
             cam1 = vrt.make_camera(w, h)
-            cpu = cpu_baseline(cam1, vox_host, n, params, args.cpu_seconds, args.cpu_threads)
+            cpu, frame_o = cpu_baseline(cam1, vox_host, n, params, args.cpu_seconds, threads)
+            cpu.update({k: v for k, v in cores.items() if k != "threads"})
+            if frame_o is not None and verify is not None and rgba8 and prev_full is not None:
+                # the oracle's frame through the oracle's RGB8 store + temporal filter against the
+                # same history: the timed path's stored bytes must be within 1 LSB (colour within
+                # 1e-4 may straddle a rounding boundary of x*255)
+                import oracle
+
+                _, cur_o = oracle.temporal(frame_o, prev_full.cpu().numpy(), args.alpha)
+                got = tiler.frame_buf.cpu().numpy().astype(np.int16)
+                d = np.abs(got - cur_o.astype(np.int16))
+                oracle_check = {"max_lsb": int(d.max()), "bytes_off_by_one": int((d == 1).sum()),
+                                "bytes": int(d.size), "ok": bool(d.max() <= 1)}
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
             "value": round(value, 3),
@@ -276,6 +394,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
+            "verified": None if verify is None else verify["verified_all_ranks"],
             "config": {
                 "workload": f"{args.config}: {desc}",
                 "scene": scene,
@@ -297,22 +416,34 @@ def main():
                 "algorithmic_bytes_per_frame": bytes_per_frame,
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": "valu-issue/latency",
                 "achieved": round(achieved, 2),
+                "achieved_is": ("reference-normalised algorithmic bytes (1 B per DDA step of the "
+                                "reference walk + 2 B per refraction probe + pixel bytes) of one "
+                                "render_kernel launch / its mean duration; not a bandwidth"),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_is": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_per_frame": traffic_frame,
+                "hbm_frac": hbm_frac,
+                "hbm_frac_is": "measured HBM bytes per frame / GPU time per frame / 8 TB/s",
+                "bytes_per_launch": int(bytes_per_launch),
                 "bytes_per_frame": own_bytes,
+                "launch_ms": round(launch_ms, 4),
+                "launches_per_frame": parts,
                 "kernel_ms": round(frame_gpu_ms, 4),
                 "kernel_ms_is": (f"GPU time per frame of this rank: {parts} concurrent "
                                  "render_kernel launches (interleaved row parts on separate "
                                  "streams), HIP events around the K timed frames"),
-                "launches_per_frame": parts,
-                "launch_ms": round(launch_ms, 4),
                 "kernel_ms_max_over_ranks": round(frame_ms_max, 4),
                 "valu_issue": valu,
+                "lib_sha256": lib_hash[:16],
+                "profile": prof_note,
             },
+            "verify": verify,
+            "oracle_check": oracle_check,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,52 @@
+#!/bin/bash
+# One gpurun call built from named steps (each under its own time limit; the call stops at the
+# first step that ends in a fault, abort or timeout):
+#   bash scripts/gpu_session.sh TAG step [step ...]
+# steps: tests | smoke | bench[:CFG] | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
+#        sq[:CFG] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
+TAG=$1; shift
+cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
+  echo "== $name rc=$rc"; grep -v amdgpu.ids "$OUT/$name.log" | tail -n ${TAILN:-6}
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  [ $rc -eq 0 ] || [ -n "$KEEP_GOING" ] || exit $rc
+}
+libs() { echo base; ls build/variants/*.so 2>/dev/null; }
+pmc() {  # pmc <name> <cfg> <counters...>
+  local name=$1 cfg=$2; shift 2
+  for lib in $(libs); do
+    local ln=$(basename $lib .so)
+    if [ $lib = base ]; then unset VRT_LIB; else export VRT_LIB=$ROOT/$lib; fi
+    run ${name}_${ln}_$cfg 120 rocprofv3 --pmc "$@" -d "$OUT/${name}_${ln}_$cfg" -o run --output-format csv -- \
+      python3 "$ROOT/bench.py" --config "$cfg" --steps 5 --warmup 1 --cpu-seconds 0 --parts 1 --no-verify
+  done
+  unset VRT_LIB
+}
+for st in "$@"; do
+  arg=${st#*:}; [ "$arg" = "$st" ] && arg=""
+  case ${st%%:*} in
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench_${arg:-C3} 300 python bench.py --config ${arg:-C3} ;;
+    ab) run ab 600 python -u scripts/ab.py --rounds 8 --configs ${arg:-C1,C2,C3,C4} ;;
+    benchvar)
+      for lib in $(libs); do
+        ln=$(basename $lib .so)
+        if [ $lib = base ]; then unset VRT_LIB; else export VRT_LIB=$ROOT/$lib; fi
+        for cfg in ${arg//,/ }; do
+          run bench_${ln}_$cfg 200 python bench.py --config $cfg --cpu-seconds 0 --no-verify
+        done
+      done; unset VRT_LIB ;;
+    write) pmc write ${arg:-C3} WRITE_SIZE ;;
+    fetch) pmc fetch ${arg:-C3} FETCH_SIZE ;;
+    sq) pmc sq ${arg:-C3} SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD ;;
+    trace) run trace_${arg:-C3} 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${arg:-C3}" -o run --output-format csv -- \
+             python3 "$ROOT/bench.py" --config ${arg:-C3} --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    py) run py_$(echo $arg | tr -c 'a-zA-Z0-9' '_' | cut -c1-40) 600 python -u $arg ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+exit 0

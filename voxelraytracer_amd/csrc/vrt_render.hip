@@ -21,6 +21,12 @@
 
 #include "vrt.h"
 
+// Diagnostic instrumentation (per-wave timestamps, certified-walk outcome counts; images and
+// counters unchanged) exists only in `make variant` builds, never in the product library.
+#if (defined(VRT_STAMPS) || defined(VRT_CERT_DIAG)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_STAMPS / VRT_CERT_DIAG are diagnostic builds: use make variant"
+#endif
+
 namespace vrt {
 
 // ------------------------------------------------------------------------ kernel arguments --
@@ -28,6 +34,7 @@ namespace vrt {
 struct KArgs {
   float inv_pv[16];
   float sun[3];
+  float sky_sy;      // max(u_SunDir.y, 0): the skybox's sun height factor (voxel.glsl:391), uniform
   float sun_n[3];    // normalize(u_SunDir), GLSL normalize semantics (host: same IEEE ops)
   float sun_rcp[3];  // RN(1 / sun_n): the shadow walk's per-axis reciprocals (uniform)
   float time, ray_noise, refl_noise, refr_noise, max_len;
@@ -177,33 +184,12 @@ struct Counters {
   uint32_t c[VRT_CNT_COUNT];
 };
 
-// Crossed-axis operands of a skip step from a per-lane LDS table (one ds_read_b128) instead of
-// three 3-way register selects.
-#ifndef VRT_LDS_AXIS
-#define VRT_LDS_AXIS 1
-#endif
-// The LDS entry address selected from three per-lane addresses (2 VALU, 2 more
-// VGPRs) instead of index + shift-add (3 VALU).
-#ifndef VRT_AX_ADDR_SEL
-#define VRT_AX_ADDR_SEL 1
-#endif
-// Table layout: axis-major (entry a of work-item t at [a * threads + t]) keeps a wave's 16-byte
-// reads on distinct banks whatever axis each lane picks; lane-major ([3t + a], 48-byte lane
-// stride) collides whenever neighbouring lanes pick different axes.
-#ifndef VRT_AX_AXIS_MAJOR
-#define VRT_AX_AXIS_MAJOR 0
-#endif
-#ifndef VRT_WG_WAVES
-#define VRT_WG_WAVES 4
-#endif
-#ifndef VRT_CMP_T
-#define VRT_CMP_T 0
-#endif
-#ifndef VRT_LEN0_SPLIT
-#define VRT_LEN0_SPLIT 0
-#endif
-constexpr int kAxStride = VRT_AX_AXIS_MAJOR ? 64 * VRT_WG_WAVES : 1;  // float4s between axes
-constexpr int kAxLane = VRT_AX_AXIS_MAJOR ? 1 : 3;                      // float4s between lanes
+// Crossed-axis operands of a skip step come from a per-lane LDS table (one ds_read_b128 at an
+// address selected from the lane's three entry addresses: 2 VALU) instead of three 3-way register
+// selects. Lane-major layout: entry a of work-item t at [3t + a] (an axis-major table measured
+// neutral, profiles/r01_v37_ab_axis_major_len0_cmpt.log).
+constexpr int kAxStride = 1;  // float4s between axes
+constexpr int kAxLane = 3;    // float4s between lanes
 
 struct Ctx {
   const uint16_t* __restrict__ vox;  // padded (N+1)^3 layout, voxel | G << 8, one per octant (see pack kernels)
@@ -212,11 +198,10 @@ struct Ctx {
   uint32_t p;  // N + 1
   float fn;
   float max_len;
-  f3 sun, sun_n, sun_rcp;
+  f3 sun_n, sun_rcp;
+  float sky_sy;
   float time, refl_noise, refr_noise;
-#if VRT_LDS_AXIS
   float4* ax;  // this lane's 3-entry axis table in LDS: {pos, dir, rcp, sign} per axis
-#endif
   const uint32_t* atlas;  // textured instances only (TEX)
   uint32_t atlas_mask;   // atlas_size - 1 (power of two)
   float atlas_fs, atlas_fts;  // (float)u_AtlasSize, (float)u_AtlasTextureSize
@@ -355,15 +340,6 @@ __device__ __forceinline__ uint32_t axis_index(unsigned long long mey, unsigned 
   asm("v_cndmask_b32_e64 %0, 0, 1, %1\n\tv_cndmask_b32_e64 %0, %0, 2, %2" : "=&v"(r) : "s"(mey), "s"(mez));
   return r;
 }
-
-#ifdef VRT_DIAG_WAVE
-// diagnostic builds only: true on the lowest active lane (one count per wave and event)
-__device__ __forceinline__ bool diag_leader() {
-  uint32_t l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return (__builtin_amdgcn_ballot_w64(true) & ((1ull << l) - 1ull)) == 0ull;
-}
-#endif
 
 // m's lane bit ? if_set : if_clear, as one v_cndmask on an SGPR lane mask
 __device__ __forceinline__ float sel_mask(unsigned long long m, float if_set, float if_clear) {
@@ -536,15 +512,9 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 // inside the volume — no event, no TestCube — and needs only the exact DDA state update; the
 // sample, its address and the load are skipped. Every float op that defines the walk's state is
 // still executed, in the reference's order, so the walk is bit-identical.
-#ifndef VRT_DIST_CAP
-#define VRT_DIST_CAP 64
-#endif
-constexpr uint32_t kDistCap = VRT_DIST_CAP;
+constexpr uint32_t kDistCap = 64;  // (profiles/r01_v32_ab_distance_cap.log: 128/255 add nothing)
 static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
-#ifndef VRT_FWD_CAP
-#define VRT_FWD_CAP 64
-#endif
-constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F; G = F - 1 is stored in 8 bits
+constexpr uint32_t kFwdCap = 64;  // cap of F; G = F - 1 is stored in 8 bits (r01_v36_ab_fwd_cap.log)
 static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
@@ -561,23 +531,12 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   // skip-box face in travel direction: B = (v + c0) + sgn * (D - margin); c0 = 0 / 1 for d > 0 / < 0
   const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
   const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
-  // the selects read dir/rcp as VGPRs (the lane mask takes the one scalar operand a VOP3 may
-  // read): materialise shadow rays' uniform sun constants once, not per step
-#if VRT_LDS_AXIS
+  // the crossed axis' operands per step from this lane's LDS table
   c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
   c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
   c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
-#if VRT_AX_ADDR_SEL
   uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
   asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));  // three VGPRs, not re-derived
-#endif
-#else
-  f3 dv = dir, rv = rcp;
-  if (SHADOW) {
-    asm volatile("" : "+v"(dv.x), "+v"(dv.y), "+v"(dv.z));
-    asm volatile("" : "+v"(rv.x), "+v"(rv.y), "+v"(rv.z));
-  }
-#endif
   const bool skip_ok = SHADOW || medium == 0u;
   // this ray's octant volume (its skip distances look along the ray's direction); uniform for
   // shadow rays. Every octant volume holds the same voxel bytes.
@@ -628,48 +587,22 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const f3 tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
       len += tmin;
       const float s = LEN0Z ? len : len - len0;
-#if VRT_CMP_T
-      // t.a - tmin == 0 <=> t.a == tmin (finite t, gradual underflow): the masks no longer wait
-      // for the subtractions
-      const bool ey = t.y == tmin, ez = t.z == tmin;
-#else
       const bool ey = tp.y == 0.0f, ez = tp.z == 0.0f;
-#endif
-#if !defined(VRT_DIAG_SAMPLED) && !defined(VRT_DIAG_WAVE)
       if (STATS) ties = add_if_both(ties, ey, ez);  // intersectionAxis[3] (counter/flag only)
-#elif defined(VRT_DIAG_WAVE) && VRT_DIAG_WAVE == 1  // diagnostic: TIE3 counts wave-level steps
-      ties += diag_leader() ? 1u : 0u;
-#endif
       // t update for the crossed axis (voxel.glsl:296/381)
       // crossed axis: z if ez (index 2, and 3 clamped), else y if ey, else x. Selected with the
       // compare masks kept in SGPRs (the compiler re-derives !ez with another v_cmp otherwise).
       const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
       const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
-#if VRT_LDS_AXIS && VRT_AX_ADDR_SEL
       // the crossed axis' entry address straight from the masks: two v_cndmask, no index math
       const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
-#elif VRT_LDS_AXIS
-      const uint32_t ai = axis_index(mey, mez);
-      const float4 ae = c.ax[ai * kAxStride];
-      const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
-#else
-      const float pa = sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x));
-      const float da = sel_mask(mez, dv.z, sel_mask(mey, dv.y, dv.x));
-      const float ra = sel_mask(mez, rv.z, sel_mask(mey, rv.y, rv.x));
-      const float sa = __builtin_copysignf(1.0f, da);
-#endif
       const float ca = pa + s * da;  // == cur on that axis: the same two ops
       const float num = (ca + sa) - pa;
       const float q = div_rn(num, da, ra) - s;
       t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
       asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
       if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
-#ifdef VRT_DIAG_SAMPLED  // diagnostic build: the TIE3 counter counts sampled fast-path steps
-        ++ties;
-#elif defined(VRT_DIAG_WAVE) && VRT_DIAG_WAVE == 2  // diagnostic: wave-level sampled branches
-        ties += diag_leader() ? 1u : 0u;
-#endif
         const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
         const bool ex = tp.x == 0.0f;
         const f3 smp = mk(cur.x + (ex ? hs.x : 0.0f), cur.y + (ey ? hs.y : 0.0f),
@@ -738,8 +671,8 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
                                         uint32_t& v) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    return skip_walk<false, STATS, LEN0Z && VRT_LEN0_SPLIT>(c, pos, dir, rcp, len0, medium, w, axis,
-                                                            vidx, v);
+    // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
+    return skip_walk<false, STATS, false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -839,9 +772,6 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 template <bool STATS>
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
-#ifdef VRT_ABLATE_SHADOW  // timing-only ablation build (scripts/ab.py); wrong images
-  if (ray.len >= 0.0f) return false;
-#endif
   WalkState w;
   walk_init(w, ray);
   const int r = walk_shadow<STATS>(c, ray.pos, ray.len, w);
@@ -941,7 +871,7 @@ __device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3
   const f3 u = normalize3(ray.dir);
   const float sun = 10.0f * gpow(dot3(c.sun_n, u), 400.0f);
   const float grad = (u.y + 1.0f) * 0.5f;
-  const float sy = gmax(c.sun.y, 0.0f);
+  const float sy = c.sky_sy;  // gmax(u_SunDir.y, 0), precomputed (a wave-uniform constant)
   const f3 sk = mk(gmax(0.0f, sun) * sy, gmax(grad * 0.75f, sun) * sy, gmax(grad, 0.0f) * sy);
   const float a1 = 1.0f - ray.energy;
   const f3 s1 = mk(mixf(sk.x, color.x, a1), mixf(sk.y, color.y, a1), mixf(sk.z, color.z, a1));
@@ -1024,54 +954,9 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 // exact walk, and textured shading reads the hit point.
 constexpr int kMaxStack = 17;
 
-#ifndef VRT_CERT
-#define VRT_CERT 1
-#endif
-// wave priority (s_setprio 0..3) of certified-instance waves that take the exact path, and of any
-// wave entering a glass pixel's bounce stack; 0 = leave the default
-// glass pixels' bounce stacks by certified walks too (cert_tree, out of line). Correct (the GPU
-// tests pass with it) and 85 % of C3's glass pixels certify, but the call site alone makes the
-// whole kernel ~3x slower (C2 0.40 vs 0.148 ms, profiles/r01_v46_ab_cert_trees.log): off
-#ifndef VRT_CERT_TREES
-#define VRT_CERT_TREES 0
-#endif
-// Certified shadow walks from exact hit points on the certified instance's exact path (fallback
-// pixels and bounce stacks)
-#ifndef VRT_CERT_EXACT_SHADOWS
-#define VRT_CERT_EXACT_SHADOWS 1
-#endif
-// ... and certified walks for the bounce stacks' secondary rays in air
-#ifndef VRT_CERT_SECONDARY
-#define VRT_CERT_SECONDARY 1
-#endif
-// ... and for the rest of a march after an in-volume refraction into air
-#ifndef VRT_CERT_CONTINUATION
-#define VRT_CERT_CONTINUATION 1
-#endif
-// Tile order: waves that took the exact path in nearly every lane last launch skip the certified
-// attempt. Off: C3 0.0740 vs 0.0730 ms per frame (profiles/r01_v73_skip_cert.log) — the glass
-// waves' certified attempts cost less than the exact walks the other lanes then run
-#ifndef VRT_SKIP_CERT
-#define VRT_SKIP_CERT 0
-#endif
-// Packed bounce-stack entries (9 words, scratch 1008 -> 880 B/lane): neutral on C1-C4
-// (profiles/r01_v75_ab_packed_stack.log), off
-#ifndef VRT_PACKED_STACK
-#define VRT_PACKED_STACK 0
-#endif
-#if VRT_PACKED_STACK
-#define VRT_STACK_PUSH(r) pack_ray(r)
-#define VRT_STACK_POP(p) unpack_ray(p)
-#else
-#define VRT_STACK_PUSH(r) (r)
-#define VRT_STACK_POP(p) (p)
-#endif
-#ifndef VRT_FALLBACK_PRIO
-#define VRT_FALLBACK_PRIO 0
-#endif
-#ifndef VRT_STACK_PRIO
-#define VRT_STACK_PRIO 3
-#endif
+// Bounce stacks run at raised wave priority (s_setprio): they are a frame's longest waves
+// (-2 % at C3, profiles/r01_v45_ab_wave_priority.log).
+constexpr int kStackPrio = 3;
 #ifdef VRT_CERT_DIAG  // diagnostic build only (scripts/cert_diag.py): outcome counts per pixel
 __device__ unsigned long long g_cert_diag[16];
 #define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
@@ -1360,13 +1245,8 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
     const uint32_t n = uint32_t(c.n);
     if (uint32_t(ax) >= n || uint32_t(ay) >= n || uint32_t(az) >= n) { CERT_DIAG(7); return false; }
     if (cert_event<true>(cell_texel(c, ax, ay, az, 0u) & kVoxMask, 0u)) { CERT_DIAG(7); return false; }
-#ifdef VRT_ABLATE_SHADOWCERT  // timing-only ablation build: no shadow walk, wrong images
-    CertResult s;
-    s.res = CERT_MISS;
-#else
     const CertResult s = cert_walk<true>(c, hh.point, S, c.sun_rcp, c.max_len - hh.len, ax, ay, az,
                                          h.eu, ed, hh.len, 0u);
-#endif
     if (s.res == CERT_UNSURE) { CERT_DIAG(8); return false; }
     CERT_DIAG(9);
     brightness = s.res == CERT_HIT ? kAmbient : lit;
@@ -1453,89 +1333,6 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
   return h;
 }
 
-struct CertSpawn {
-  Ray ray;
-  int cx, cy, cz;
-  float e0;
-  f3 ed;
-};
-
-// The bounce stack of a glass primary hit (voxel.glsl:436-451) by certified walks: every
-// secondary ray starts at an exact hit point known to its bound, so each start is checked like a
-// shadow origin (cert_start) and its uncertainty carried into the walk. Out of line: only glass
-// pixels call it, and the main walk's registers stay free of it. false: some step could differ
-// from the exact path (the pixel then takes it; colour untouched).
-__device__ __noinline__ bool cert_tree(const Ctx& c, const Ray& ray0, const CertResult& h0,
-                                       int max_refl, int max_transp, f3& color_out) {
-  f3 color = color_out;
-  Ray ray = ray0;
-  CertResult h = h0;
-  Hit hh = cert_hit_record(ray, h);
-  if (!cert_shade_hit(c, ray, h, hh, color)) return false;
-  CertSpawn stack[kMaxStack];
-  const int cap = max_refl + max_transp + 1;
-  int sp = 0;
-  for (;;) {
-    if (h.res == CERT_HIT) {
-      const uint32_t m = mat_id(h.byte);
-      if (mat_reflective(m) && ray.rdepth < max_refl && sp < cap) {
-        if (!(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))) return false;
-        CertSpawn& e = stack[sp];
-        e.ray = reflection_ray(c, ray, hh);
-        cell_before(h, ray.dir, e.cx, e.cy, e.cz);
-        const f3 rn = mk(__builtin_amdgcn_rcpf(e.ray.dir.x), __builtin_amdgcn_rcpf(e.ray.dir.y),
-                         __builtin_amdgcn_rcpf(e.ray.dir.z));
-        if (!fast_path_ok(e.ray.dir) ||
-            !cert_start(hh.point, ray.dir, e.ray.dir, rn, h.axis, h.eu, e.cx, e.cy, e.cz, e.ed))
-          return false;
-        e.e0 = h.eu;
-        sp++;
-      }
-      if (mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f &&
-          sp < cap) {
-        // probes at the hit point +- normal/2 (:219-220): robust positions only (cert_start)
-        const float eta = mat_refr(get_voxel(c, hh.point + hh.normal * 0.5f)) /
-                          mat_refr(get_voxel(c, hh.point - hh.normal * 0.5f));
-        const f3 rd = refract3(normalize3(ray.dir), hh.normal, eta);
-        const bool tir = rd.x == 0.0f && rd.y == 0.0f && rd.z == 0.0f;
-        if (tir ? !(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))
-                : !(c.refr_noise == 0.0f && zero_noise_exact(rd)))
-          return false;
-        Counters kk;
-#pragma unroll
-        for (int q = 0; q < VRT_CNT_COUNT; ++q) kk.c[q] = 0;
-        CertSpawn& e = stack[sp];
-        e.ray = refraction_ray<false>(c, ray, hh, kk);
-        e.cx = h.cx;  // into the glass cell, or (total internal reflection) back before it
-        e.cy = h.cy;
-        e.cz = h.cz;
-        if ((comp(e.ray.dir, h.axis) > 0.0f) != (comp(ray.dir, h.axis) > 0.0f))
-          cell_before(h, ray.dir, e.cx, e.cy, e.cz);
-        const f3 rn = mk(__builtin_amdgcn_rcpf(e.ray.dir.x), __builtin_amdgcn_rcpf(e.ray.dir.y),
-                         __builtin_amdgcn_rcpf(e.ray.dir.z));
-        if (!fast_path_ok(e.ray.dir) ||
-            !cert_start(hh.point, ray.dir, e.ray.dir, rn, h.axis, h.eu, e.cx, e.cy, e.cz, e.ed))
-          return false;
-        e.e0 = h.eu;
-        sp++;
-      }
-    }
-    if (sp == 0) break;
-    --sp;
-    ray = stack[sp].ray;
-    h = cert_march(c, ray, stack[sp].cx, stack[sp].cy, stack[sp].cz, stack[sp].e0, stack[sp].ed);
-    if (h.res == CERT_UNSURE) return false;
-    if (h.res == CERT_HIT) {
-      hh = cert_hit_record(ray, h);
-      if (!cert_shade_hit(c, ray, h, hh, color)) return false;
-    } else {
-      apply_sky_color(c, ray, color);
-    }
-  }
-  color_out = color;
-  return true;
-}
-
 // The exact walk's start cell from P along D (voxel.glsl:306-309: first planes d < 0 ? ceil(p - 1)
 // : floor(p + 1)); false when it lies outside the volume or a plane disagrees with the cell's.
 __device__ __forceinline__ bool exact_start_cell(const Ctx& c, const f3 P, const f3 D, int& cx, int& cy,
@@ -1569,12 +1366,7 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h) {
 // planes. In an air medium every event is a hit (:353), and a non-glass hit spawns no rays
 // (:440-448). true (colour updated as TraceWithShadow's, :395-423): a miss, or a non-glass hit
 // whose shadow certifies. false (colour untouched): the exact march goes on.
-#ifdef VRT_AIR_SEGMENT_NOINLINE  // A/B experiment
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-bool cert_air_segment(const Ctx& c, const Ray& ray, int cx, int cy, int cz,
+__device__ __forceinline__ bool cert_air_segment(const Ctx& c, const Ray& ray, int cx, int cy, int cz,
                                                  const f3 ed, f3& color) {
   const f3 D = ray.dir;
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
@@ -1643,13 +1435,9 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
 // segments — the whole ray from its exact origin, or the rest after an in-volume refraction into
 // air — settled by certified walks where they can be (settled: colour updated, no secondary
 // rays); the exact march (as march()) otherwise.
-#ifdef VRT_MARCH_CERT_NOINLINE  // A/B experiment
-__device__ __noinline__
-#else
-__device__
-#endif
-Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k, uint32_t& steps,
-                          uint32_t& flags) {
+// (Out of line it costs C2-C4 +45 %, profiles/r01_v69_ab_noinline_w6.log.)
+__device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k,
+                          uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
   h.vidx = -1;
@@ -1706,38 +1494,33 @@ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k, ui
     const float q = ((comp(w.cur, axis) + comp(step, axis)) - comp(ray.pos, axis)) /
                         comp(ray.dir, axis) - (w.len - ray.len);
     set_comp(w.t, axis, q);
-#if VRT_CERT_CONTINUATION
     if (medium == 0u && cert_continuation(c, ray, w, axis, color)) {
       settled = true;
       return h;
     }
-#endif
   }
   return h;
 }
 
 // The whole pixel by certified walks, when it can be certified: a primary miss, or a non-glass
-// primary hit with its shadow. false (colour untouched) when any walk or any derived value could
-// differ from the exact path's, or the hit is glass (its secondary rays start at the exact hit
-// point): the pixel then takes the exact path.
-__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, int max_refl, int max_transp,
-                                           f3& color_out) {
+// primary hit with its shadow. The pixel's colour starts black (voxel.glsl:428); color_out is
+// written only when the pixel certifies. false when any walk or any derived value could differ
+// from the exact path's, or the hit is glass (its secondary rays start at the exact hit point):
+// the pixel then takes the exact path.
+__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out) {
   const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
   int cx, cy, cz;
   if (!exact_start_cell(c, P, D, cx, cy, cz)) { CERT_DIAG(0); return false; }
   // hardware reciprocals (<= 1 ulp): the certified walk only needs its own error bounded
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
-#ifdef VRT_ABLATE_WALKS  // timing-only ablation build: no walks at all (sky), wrong images
-  if (P.x > -1e30f) { apply_sky_color(c, ray0, color_out); return true; }
-#endif
   CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f,
                                   mk(0.0f, 0.0f, 0.0f), 0.0f, 0u);
 #ifdef VRT_CERT_DIAG
   cert_diag_iters(10, h.iters);
 #endif
   if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }
-  f3 color = color_out;
+  f3 color = mk(0.0f, 0.0f, 0.0f);
   if (h.res == CERT_MISS) {
     CERT_DIAG(2);
     apply_sky_color(c, ray0, color);
@@ -1745,13 +1528,8 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, int ma
     return true;
   }
   if (mat_id(h.byte) == 2u) {  // only glass spawns secondary rays (:440-448)
-#if VRT_CERT_TREES
-    if (cert_tree(c, ray0, h, max_refl, max_transp, color)) {
-      CERT_DIAG(11);
-      color_out = color;
-      return true;
-    }
-#endif
+    // (certifying the glass pixels' bounce stacks too was correct but slower: the call site alone
+    // made the kernel 3x slower out of line, and inline C3 lost 20-45 %, profiles/r01_v46_*, r01_v48_*)
     CERT_DIAG(3);
     return false;
   }
@@ -1759,7 +1537,6 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, int ma
   color_out = color;
   return true;
 }
-
 
 // ---- RGB8 framebuffer store + temporal filter (oracle/vrt_oracle.c oracle_temporal) ----------
 // GL float -> UNORM8 store into the RGB8 FBO attachments (FrameBuffer.cpp:8): clamp to [0,1]
@@ -1797,35 +1574,13 @@ __device__ __forceinline__ uint32_t lane_id() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
-// Waves per workgroup (1, 2 or 4): each wave renders an 8x8 pixel tile; a workgroup covers
-// 8x8, 16x8 or 16x16 pixels (wave = threadIdx.x >> 6, uniform).
-#ifndef VRT_WG_WAVES
-#define VRT_WG_WAVES 4
-#endif
-static_assert(VRT_WG_WAVES == 1 || VRT_WG_WAVES == 2 || VRT_WG_WAVES == 4, "1, 2 or 4 waves");
-constexpr int kWgThreads = 64 * VRT_WG_WAVES;
-constexpr int kTileW = VRT_WG_WAVES >= 2 ? 16 : 8;
-constexpr int kTileH = VRT_WG_WAVES == 4 ? 16 : 8;
-// XCD-aware tile order: the dispatcher hands workgroup L (linear over the 1-D grid) to XCD L % 8,
-// so neighbouring tiles land on different XCDs and every XCD's L2 ends up holding the whole
-// visible volume. With VRT_XCD_CHUNK = C > 0, XCD x renders runs of C consecutive tiles instead
-// (tile T = ((L/8)/C*8 + L%8)*C + (L/8)%C: a bijection on the first floor(G/8C)*8C workgroups;
-// the remainder keeps L). 0 = dispatch order.
-#ifndef VRT_XCD_CHUNK
-#define VRT_XCD_CHUNK 0
-#endif
-__device__ __forceinline__ uint32_t dispatch_tile(uint32_t L, uint32_t tiles) {
-#if VRT_XCD_CHUNK > 0
-  constexpr uint32_t C = VRT_XCD_CHUNK;
-  const uint32_t full = tiles / (8u * C) * (8u * C);
-  if (L < full) {
-    const uint32_t pos = L >> 3;
-    return ((pos / C) * 8u + (L & 7u)) * C + pos % C;
-  }
-#endif
-  (void)tiles;
-  return L;
-}
+// Four waves per workgroup, each rendering an 8x8 pixel tile: a workgroup covers 16x16 pixels
+// (wave = threadIdx.x >> 6, uniform). Tiles are dispatched in row order (an XCD-aware order that
+// keeps runs of tiles on one XCD's L2 was neutral or worse, profiles/r01_v29_ab_xcd_tile_swizzle_negative.log).
+constexpr int kWgWaves = 4;
+constexpr int kWgThreads = 64 * kWgWaves;
+constexpr int kTileW = 16;
+constexpr int kTileH = 16;
 
 // Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, the glass pixels'
 // bounce stacks; dispatched in row order, those start wherever the glass is in the image. Each
@@ -1837,28 +1592,24 @@ __device__ __forceinline__ uint32_t dispatch_tile(uint32_t L, uint32_t tiles) {
 // Both test the same immutable word, so every tile is rendered exactly once whatever the buffer
 // holds (a fresh zeroed buffer: no heavy tiles).
 constexpr uint32_t kOrdHdr = 0;  // the per-tile wave counters, then the two flag sets
-// The tile workgroup L renders, or ~0u (nothing to do); flag: the tile's word of the last launch,
-// bit 0 heavy (ran a bounce stack), bit 1 + w: wave w took the exact path in nearly every lane
-// (it then skips the certified attempt, whose work those lanes would throw away)
-__device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L, uint32_t& flag) {
+// The tile workgroup L renders, or ~0u (nothing to do); a tile's flag word of the last launch is 1
+// when it ran a bounce stack (heavy)
+__device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L) {
   const uint32_t* flags = a.order + kOrdHdr + a.tiles + a.ord_r * a.tiles;
   const bool first = L < a.tiles;
   const uint32_t j = first ? L : L - a.tiles;
-  flag = flags[j];
-  return ((flag & 1u) != 0u) == first ? j : ~0u;
+  return ((flags[j] & 1u) != 0u) == first ? j : ~0u;
 }
 // after the trace: the tile's last wave files it for the next launch
-// (counter: bits 0-7 waves done, 8-15 heavy waves, 16 + w wave w mostly exact)
-__device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool heavy_wave, int wave,
-                                             bool mostly_exact) {
+// (counter: bits 0-7 waves done, 8-15 heavy waves)
+__device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool heavy_wave) {
   uint32_t* cnt = a.order + kOrdHdr + tile;
-  const uint32_t add = 1u | (heavy_wave ? 0x100u : 0u) | (mostly_exact ? 0x10000u << wave : 0u);
+  const uint32_t add = 1u | (heavy_wave ? 0x100u : 0u);
   const uint32_t old = atomicAdd(cnt, add);
-  if ((old & 0xFFu) != uint32_t(VRT_WG_WAVES) - 1u) return;
+  if ((old & 0xFFu) != uint32_t(kWgWaves) - 1u) return;
   *cnt = 0u;
   const uint32_t all = old + add;
-  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] =
-      ((all & 0xFF00u) != 0u ? 1u : 0u) | ((all >> 16) & 0xFu) << 1;
+  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] = (all & 0xFF00u) != 0u ? 1u : 0u;
 }
 
 __device__ __forceinline__ int pixel_x(uint32_t tx, int wave, uint32_t lane) {
@@ -1895,7 +1646,7 @@ constexpr int kCntReplicas = 256;
 // Waves per SIMD the register budget is sized for: 7 -> 72 VGPRs. With certified walks inside the
 // bounce stacks, 64 VGPRs (8 waves) spill in the glass waves that bound a frame: 7 is 2-4 % faster
 // on C1-C4 (profiles/r01_v56_ab_occupancy.log), 6 (80 VGPRs) no better.
-#ifndef VRT_MIN_WAVES
+#ifndef VRT_MIN_WAVES  // occupancy A/B builds (make variant); images identical at any value
 #define VRT_MIN_WAVES 7
 #endif
 
@@ -1907,7 +1658,7 @@ __device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t*
   c.p = uint32_t(a.n) + 1u;
   c.fn = a.fn;
   c.max_len = a.max_len;
-  c.sun = mk(a.sun[0], a.sun[1], a.sun[2]);
+  c.sky_sy = a.sky_sy;
   c.sun_n = mk(a.sun_n[0], a.sun_n[1], a.sun_n[2]);
   c.sun_rcp = mk(a.sun_rcp[0], a.sun_rcp[1], a.sun_rcp[2]);
   c.time = a.time;
@@ -1944,34 +1695,6 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
   return ray;
 }
 
-// A bounce-stack entry in scratch: a Ray with its medium byte and both depths in one word (9
-// words instead of 11 per push and pop)
-struct StackRay {
-  f3 pos, dir;
-  float len, energy;
-  uint32_t packed;  // voxel (8 bits) | rdepth (signed 12) << 8 | tdepth (signed 12) << 20
-};
-__device__ __forceinline__ StackRay pack_ray(const Ray& r) {
-  StackRay p;
-  p.pos = r.pos;
-  p.dir = r.dir;
-  p.len = r.len;
-  p.energy = r.energy;
-  p.packed = (r.voxel & 0xFFu) | (uint32_t(r.rdepth) & 0xFFFu) << 8 | (uint32_t(r.tdepth) & 0xFFFu) << 20;
-  return p;
-}
-__device__ __forceinline__ Ray unpack_ray(const StackRay& p) {
-  Ray r;
-  r.pos = p.pos;
-  r.dir = p.dir;
-  r.len = p.len;
-  r.energy = p.energy;
-  r.voxel = p.packed & 0xFFu;
-  r.rdepth = int32_t(p.packed << 12) >> 20;
-  r.tdepth = int32_t(p.packed) >> 20;
-  return r;
-}
-
 #ifdef VRT_STAMPS
 // Diagnostic build only: per wave {time after the exact primary trace, after the bounce stacks}
 constexpr int kMaxStampWaves3 = 1 << 18;
@@ -1988,16 +1711,12 @@ template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
-#if VRT_PACKED_STACK
-  StackRay stack[kMaxStack];
-#else
   Ray stack[kMaxStack];
-#endif
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
 #ifdef VRT_STAMPS
-  const uint32_t st_wave = blockIdx.x * VRT_WG_WAVES + (threadIdx.x >> 6);
+  const uint32_t st_wave = blockIdx.x * kWgWaves + (threadIdx.x >> 6);
   {
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     if (lane_id() == uint32_t(__builtin_amdgcn_readfirstlane(int(lane_id()))) && st_wave < kMaxStampWaves3)
@@ -2006,31 +1725,24 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
 #endif
   hit_vidx = h0.found ? h0.vidx : -1;
   hit_len = h0.found ? h0.len : 0.0f;
-#ifdef VRT_ABLATE_SECONDARY  // timing-only ablation build (scripts/ab.py); wrong images
-  if (false) {
-#else
   if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)
-#endif
-#if VRT_STACK_PRIO
-    __builtin_amdgcn_s_setprio(VRT_STACK_PRIO);  // bounce stacks: the longest waves of a frame
-#endif
+    __builtin_amdgcn_s_setprio(kStackPrio);  // bounce stacks: the longest waves of a frame
     Hit h = h0;
     for (;;) {
       const uint32_t m = mat_id(h.voxel);
       if (h.found) {
         if (mat_reflective(m) && ray.rdepth < a.max_refl) {
-          if (sp < cap) stack[sp++] = VRT_STACK_PUSH(reflection_ray(c, ray, h));
+          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
           else flags |= VRT_HIT_FLAG_STACK_FULL;
         }
         if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
-          if (sp < cap) stack[sp++] = VRT_STACK_PUSH(refraction_ray<TEX>(c, ray, h, k));
+          if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
           else flags |= VRT_HIT_FLAG_STACK_FULL;
         }
       }
       if (sp == 0) break;
-      ray = VRT_STACK_POP(stack[--sp]);
+      ray = stack[--sp];
       k.c[VRT_CNT_SECONDARY_RAYS]++;
-#if VRT_CERT_SECONDARY
       if constexpr (CSH && CSEC) {
         bool settled;
         h = march_cert(c, ray, color, settled, k, steps, flags);
@@ -2038,11 +1750,10 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
           h.found = false;  // a miss or a hit without secondary rays
           continue;
         }
-        shade<STATS, TEX, VRT_CERT_EXACT_SHADOWS>(c, ray, h, color, k, steps, flags);
+        shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
         continue;
       }
-#endif
-      h = trace_with_shadow<STATS, TEX, false, CSH && VRT_CERT_EXACT_SHADOWS>(c, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH>(c, ray, color, k, steps, flags);
     }
 #ifdef VRT_STAMPS
     {
@@ -2074,6 +1785,8 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // STATS: this instance writes hit records and/or counters. Without it the per-lane counters,
 // step/flag/tie tracking are dead code (~20 VGPRs and a VALU per DDA step freed); the rendering
 // arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
+// CERT (stats-free colour-only instances): 0 exact walks only, 1 certified walks for the exact
+// path's shadow and air-medium secondary rays, 2 also whole pixels first.
 template <bool STATS, bool TEX, int CERT = 0>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
@@ -2084,22 +1797,14 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   // every wave (~1.8 KB/wave of scratch writes, most of the excess WRITE_SIZE over the frame).
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
 #ifdef VRT_STAMPS
-  const uint32_t wave_lin = blockIdx.x * VRT_WG_WAVES + wave;
+  const uint32_t wave_lin = blockIdx.x * kWgWaves + wave;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  uint32_t tile = dispatch_tile(blockIdx.x, a.tiles);
-  bool skip_cert = false;  // tile order: this wave was nearly all exact last launch
+  uint32_t tile = blockIdx.x;
   if constexpr (!STATS) {
     if (a.order) {
-      uint32_t flag;
-      tile = ordered_tile(a, blockIdx.x, flag);
+      tile = ordered_tile(a, blockIdx.x);
       if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
-#if VRT_SKIP_CERT
-      skip_cert = ((flag >> (1 + wave)) & 1u) != 0u;
-#endif
-#ifdef VRT_HEAVY_PRIO  // A/B experiment: heavy tiles' waves at raised priority from the start
-      if (blockIdx.x < a.tiles) __builtin_amdgcn_s_setprio(VRT_HEAVY_PRIO);
-#endif
     }
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
@@ -2107,8 +1812,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const int px = pixel_x(tx, wave, lane_id());
   const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
-  bool stack = false;       // this lane ran a bounce stack (tile order)
-  bool exact_lane = false;  // this lane took the exact path (tile order)
+  bool stack = false;  // this lane ran a bounce stack (tile order)
 
   Counters k;
 #pragma unroll
@@ -2117,24 +1821,22 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   if (valid) {
     Ctx c;
     init_ctx(c, a, vox);
-#if VRT_LDS_AXIS
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * kAxLane];
-#endif
     const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
-    f3 color = mk(0.0f, 0.0f, 0.0f);
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
     uint32_t steps = 0, flags = 0;
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
-#if VRT_CERT
-    // stats-free colour-only frames: certified primary + shadow walks, the exact path for the rest
-#ifdef VRT_ABLATE_FALLBACK  // timing-only ablation build (scripts/ab.py): no exact path, wrong images
-    if (CERT < 2 || (cert_pixel(c, ray, a.max_refl, a.max_transp, color), false))
-#else
-    const bool need_exact = CERT < 2 || skip_cert || !cert_pixel(c, ray, a.max_refl, a.max_transp, color);
-    exact_lane = need_exact;
+    // stats-free colour-only frames: certified primary + shadow walks, the exact path for the
+    // rest. cert_pixel starts from its own black colour and writes the result only on success,
+    // so no colour value is live (and spilled, 1 KB per wave) across its early exits: C3
+    // WRITE_SIZE 41 -> 17 MB per frame at equal speed (profiles/r02_s03). Parking the certified
+    // colour in LDS, or storing certified pixels before the exact path and re-deriving the
+    // primary ray there, was 4-6 % slower.
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, color);
 #ifdef VRT_STAMPS
     const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
     const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
@@ -2143,15 +1845,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       g_stamps2[wave_lin][1] = n_exact;
     }
 #endif
-    if (need_exact)
-#endif
-#endif
-    {
-#if VRT_FALLBACK_PRIO
-      // the frame's longest waves are the ones with exact work left: let the SIMD's arbiter
-      // prefer them over the certified-only waves beside them
-      if (CERT == 2) __builtin_amdgcn_s_setprio(VRT_FALLBACK_PRIO);
-#endif
+    if (need_exact) {
+      color = mk(0.0f, 0.0f, 0.0f);
       stack = exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
                                                             hit_len);
     }
@@ -2181,8 +1876,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   if constexpr (!STATS) {
     if (a.order) {
       const bool heavy = __ballot(stack) != 0ull;
-      const bool mostly_exact = VRT_SKIP_CERT && __builtin_popcountll(__ballot(exact_lane)) >= 56;
-      if (lane_id() == 0) order_record(a, tile, heavy, wave, mostly_exact);
+      if (lane_id() == 0) order_record(a, tile, heavy);
     }
   }
   if (STATS && counters) {
@@ -2387,9 +2081,6 @@ __global__ void __launch_bounds__(256) fwd_pack_kernel(const uint8_t* __restrict
 
 // ---------------------------------------------------------------------------- C-ABI context --
 
-#ifndef VRT_TILE_ORDER_DEFAULT
-#define VRT_TILE_ORDER_DEFAULT 1
-#endif
 struct vrt_ctx {
   int device = 0;
   uint8_t* d_vox = nullptr;       // canonical N^3
@@ -2427,7 +2118,7 @@ struct vrt_ctx {
   static constexpr int kOrderSlots = 8;
   OrderSlot order[kOrderSlots];
   uint64_t order_tick = 0;
-  bool tile_order = VRT_TILE_ORDER_DEFAULT;
+  bool tile_order = true;
   std::string err;
 };
 
@@ -2490,6 +2181,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   vrt::KArgs a;
   std::memcpy(a.inv_pv, cam->inv_pv, sizeof(a.inv_pv));
   std::memcpy(a.sun, p->sun_dir, sizeof(a.sun));
+  a.sky_sy = std::fmax(p->sun_dir[1], 0.0f);  // GLSL max(x, 0) with fmaxf's NaN rule, as gmax
   // normalize(u_SunDir) exactly as the kernel's normalize3 (IEEE single ops, no contraction)
   const float sx = p->sun_dir[0], sy = p->sun_dir[1], sz = p->sun_dir[2];
   const float inv = 1.0f / std::sqrt(sx * sx + sy * sy + sz * sz);
@@ -2523,7 +2215,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params
   a.prev = nullptr;
   a.cur = nullptr;
   a.raw = nullptr;
-  a.cert = !VRT_CERT || ctx->octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || ctx->cert_auto ? 2 : 1);
+  a.cert = ctx->octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || ctx->cert_auto ? 2 : 1);
   a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
   a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
   a.order = nullptr;
@@ -2828,7 +2520,7 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
 
 int vrt_certified(const vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
-  return VRT_CERT && ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto) ? 1 : 0;
+  return ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto) ? 1 : 0;
 }
 
 int vrt_volume_octants(const vrt_ctx* ctx) {

@@ -347,16 +347,16 @@ def main():
             if pj.get("lib_sha256") != lib_hash:
                 prof_note = (f"{os.path.relpath(pmc, ROOT)} was measured on another build "
                              f"({str(pj.get('lib_sha256'))[:12]} != {lib_hash[:12]}): not used")
-            elif pj.get("parts") != parts:
-                prof_note = f"{os.path.relpath(pmc, ROOT)} has parts={pj.get('parts')}: not used"
             else:
-                traffic = int(pj["hbm_bytes_per_launch"])
-                traffic_frame = traffic * parts
+                # the PMC passes run one launch per frame (--parts 1); a frame of `parts`
+                # interleaved launches moves the same bytes, split over its launches
+                traffic_frame = int(pj["hbm_bytes_per_launch"]) * int(pj.get("parts", 1))
+                traffic = traffic_frame // parts
                 hbm_frac = round(traffic_frame / (frame_gpu_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)
                 if pj.get("valu_insts_per_launch"):
                     # VALU-issue bound of the same frame: a wave64 VALU op takes 2 cycles on a
                     # SIMD32; 1024 SIMDs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
-                    insts = pj["valu_insts_per_launch"] * parts
+                    insts = pj["valu_insts_per_launch"] * int(pj.get("parts", 1))
                     floor_ms = insts * 2 / (1024 * 2.4e9) * 1e3
                     valu = {"insts_per_frame": int(insts), "issue_bound_ms": round(floor_ms, 4),
                             "frac": round(floor_ms / frame_gpu_ms, 4),
@@ -425,7 +425,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "traffic_is": "measured HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_is": ("measured HBM bytes per launch: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a "
+                               "one-launch frame (profile stamped with this library's hash) / parts"),
                 "traffic_per_frame": traffic_frame,
                 "hbm_frac": hbm_frac,
                 "hbm_frac_is": "measured HBM bytes per frame / GPU time per frame / 8 TB/s",

@@ -5,6 +5,7 @@
 TAG=${1:-run}; CFG=${2:-C3}
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
+sha256sum voxelraytracer_amd/_lib/libvrt.so | cut -d" " -f1 > "$OUT/lib.sha256"
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
@@ -13,7 +14,7 @@ step() {  # step <name> <timeout> <cmd...>
   ok $rc || exit $rc
 }
 if [ -z "$SKIP_TESTS" ]; then
-  step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench 300 python bench.py --config "$CFG"

@@ -7,7 +7,7 @@ vectors and cannot run here, so these pin REGRESSIONS of the re
 kernel, not the reference's own output. Each fixture holds its inputs (scene id, N, seed, camera
 matrix, params) and outputs (RGBA float32, primary hit records, counters) plus the SHA-256 of the
 volume bytes, which pins the scene builders (main.cpp:218-288).
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [fixture names]
 """
 import hashlib
 import json
@@ -37,22 +37,38 @@ FIXTURES = [
     ("textured_terrain16_64", "terrain", 16, 64, 64, 4, 2, dict(atlas=(32, 16, 5))),
     ("textured_glass_cube16_48", "glass_cube", 16, 48, 48, 4, 4,
      dict(atlas=(32, 16, 6), reflection_noise=0.05, time=2.0)),
+    # textured mode with the reference's own textures (tests/golden/atlas/atlas_ref128.npz, made
+    # by make_atlas_ref.py from res/textures/*128.png): glass alpha is 0 or 255, so both sides of
+    # GetColor(hit).a != 1 (voxel.glsl:445) and energy *= 1 - a (:239-240) occur
+    ("textured_ref_refraction32_96x64", "refraction", 32, 96, 64, 4, 4, dict(atlas="ref")),
+    ("textured_ref_glass_cube16_64", "glass_cube", 16, 64, 64, 4, 4,
+     dict(atlas="ref", reflection_noise=0.05, time=2.0)),
 ]
+
+
+def ref_atlas():
+    z = np.load(os.path.join(HERE, "atlas", "atlas_ref128.npz"), allow_pickle=False)
+    return z["atlas"]
 
 PARAM_KEYS = ("time", "ray_noise", "reflection_noise", "refraction_noise", "max_ray_length",
               "max_reflections", "max_transparencies", "color_only", "atlas_size",
               "atlas_texture_size")
 
 
-def main():
+def main(only=()):
     for name, scene, n, w, h, R, T, extra in FIXTURES:
+        if only and name not in only:
+            continue
         extra = dict(extra)
         pose = {k: extra.pop(k) for k in ("pos", "rot") if k in extra}
         cam = vrt.make_camera(w, h, **pose)
         atlas_spec = extra.pop("atlas", None)
         p = vrt.default_params(R, T, **extra)
         atlas = np.zeros((0, 0, 4), np.uint8)
-        if atlas_spec:
+        if atlas_spec == "ref":
+            atlas, ts = ref_atlas(), 128
+            p = vrt.textured_params(p, atlas, ts)
+        elif atlas_spec:
             size, ts, seed = atlas_spec
             atlas = vrt.make_atlas(size, ts, seed)
             p = vrt.textured_params(p, atlas, ts)
@@ -77,4 +93,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))   # optional fixture names: regenerate only those

@@ -35,6 +35,23 @@ def load(path):
     return z, meta, cam, p, vox
 
 
+def test_reference_atlas_fixture():
+    """tests/golden/atlas/atlas_ref128.npz holds the reference's decoded textures
+    (main.cpp:187-193): 256x256 RGBA8, opaque stone/dirt/grass, glass alpha exactly {0, 255}."""
+    z = np.load(os.path.join(HERE, "golden", "atlas", "atlas_ref128.npz"), allow_pickle=False)
+    a = z["atlas"]
+    meta = json.loads(str(z["meta"]))
+    assert a.shape == (256, 256, 4) and a.dtype == np.uint8
+    assert set(meta["png_sha256"]) == {f"{k}128.png" for k in vrt.ATLAS_SLOTS}
+    for name, (tx, ty) in vrt.ATLAS_SLOTS.items():
+        rs, cs = vrt.atlas_slot_rows(256, 128, tx, ty)
+        alpha = np.unique(a[rs, cs, 3])
+        if name == "glass":
+            assert alpha.tolist() == [0, 255]
+        else:
+            assert alpha.tolist() == [255]
+
+
 def test_fixtures_present():
     assert len(FILES) >= 6
 

@@ -156,6 +156,28 @@ def test_parity_textured_full_size_refraction(renderer):
     compare(rgba_g, hits_g, st, rgba_o, hits_o, cnt_o)
 
 
+def ref_atlas():
+    """The reference's own textures (res/textures/*128.png, main.cpp:187-193) decoded into the
+    ABI atlas layout: tests/golden/atlas/atlas_ref128.npz (tests/golden/make_atlas_ref.py)."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "atlas", "atlas_ref128.npz")
+    return np.load(path, allow_pickle=False)["atlas"]
+
+
+@pytest.mark.parametrize("scene,R,T", [("refraction", 4, 4), ("glass_cube", 1, 2)])
+def test_parity_textured_full_size_reference_atlas(renderer, scene, R, T):
+    """Full 1920x1080 frames at 128^3 in textured mode with the reference's own atlas, whose glass
+    alpha is 0 or 255: both sides of GetColor(hit).a != 1 (voxel.glsl:445) and of
+    energy *= 1 - a (:239-240) occur."""
+    vox = vrt.build_scene(scene, 128)
+    renderer.upload_volume(vox, 128)
+    cam = vrt.make_camera(1920, 1080)
+    p = vrt.textured_params(vrt.default_params(R, T), ref_atlas())
+    rgba_g, hits_g, st = renderer.render(cam, p)
+    rgba_o, hits_o, cnt_o = oracle.render(cam, vox, 128, p, threads=THREADS)
+    compare(rgba_g, hits_g, st, rgba_o, hits_o, cnt_o)
+    assert cnt_o["secondary_rays"] > 0
+
+
 def test_atlas_upload_and_switching(renderer):
     """The context keeps the atlas: an explicit upload serves a params block without a pointer;
     a different pointer re-uploads; colour-only renders are unaffected."""

@@ -58,6 +58,11 @@ def parse():
                     help="threads of the CPU baseline (0: all the host grants, see host_cores)")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the post-timing check of the timed frame against the exact instance")
+    ap.add_argument("--verify-frames", type=int, default=1,
+                    help="consecutive frames of the timed path checked after the timed region")
+    ap.add_argument("--oracle-check", action="store_true",
+                    help="also check the verified frames against the oracle when the CPU baseline "
+                         "leg is off (renders one oracle frame on the host cores)")
     ap.add_argument("--output", default="rgba8", choices=["rgba8", "f32"],
                     help="rgba8: the reference's stored frame (RGB8 store + temporal filter fused "
                          "into the kernel); f32: the float RGBA frame of vrt_render")
@@ -289,34 +294,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, frame_ms_max = t.tolist()
 
-    # Check of the timed path (after all timing): one more frame through the same FrameTiler
-    # (parts on their streams, pitched in place, tile order seeded by the frames before it,
-    # certified walks) against the exact STATS instance (exact walks, counters on) rendering the
-    # same rows from a copy of the same history: the stored bytes (or float frame) must be equal.
+    # Check of the timed path (after all timing): the next `verify_frames` frames through the same
+    # FrameTiler (parts on their streams, pitched in place, tile order seeded by the frames before
+    # them, certified walks), each against the exact STATS instance (exact walks, counters on)
+    # rendering the same rows from a copy of the same history: the stored bytes (or float frame)
+    # must be equal. Single rank: the frames and their histories are kept for the oracle check.
     verify = None
-    prev_full = None
+    pairs = []   # (history before, frame after) of each verified frame, host copies
     if not args.no_verify:
         nb = len(tiler.bands)
-        last = tiler.bands[(tiler.k - 1) % nb]
-        prev_parts = [tiler._part_buffers(s_, last, last)[0].clone() for s_ in range(parts)]
-        if world == 1 and tiler.frame_buf is not None:
-            prev_full = tiler.frame_buf.clone()
-        tiler.frame()
-        tiler.finish()
-        torch.cuda.synchronize(dev)
-        newest = tiler.bands[(tiler.k - 1) % nb]
         bad = 0
         total = 0
         vc = torch.zeros_like(cnt)
-        for s_, (row0, rows, step) in enumerate(tiler.specs):
-            got = tiler._part_buffers(s_, newest, newest)[0].contiguous()
-            ref = torch.zeros_like(got)
-            prev_c = prev_parts[s_].contiguous()
-            launch(row0, rows, step, ref, prev_c, vc.data_ptr())   # counters on: STATS instance
+        for _ in range(max(1, args.verify_frames)):
+            last = tiler.bands[(tiler.k - 1) % nb]
+            prev_parts = [tiler._part_buffers(s_, last, last)[0].clone() for s_ in range(parts)]
+            prev_full = tiler.frame_buf.clone() if world == 1 and tiler.frame_buf is not None else None
+            tiler.frame()
+            tiler.finish()
             torch.cuda.synchronize(dev)
-            bad += int((got != ref).sum().item())
-            total += got.numel()
-        verify = {"verified": bad == 0, "mismatched_elements": bad, "elements": total,
+            newest = tiler.bands[(tiler.k - 1) % nb]
+            for s_, (row0, rows, step) in enumerate(tiler.specs):
+                got = tiler._part_buffers(s_, newest, newest)[0].contiguous()
+                ref = torch.zeros_like(got)
+                prev_c = prev_parts[s_].contiguous()
+                launch(row0, rows, step, ref, prev_c, vc.data_ptr())   # counters on: STATS instance
+                torch.cuda.synchronize(dev)
+                bad += int((got != ref).sum().item())
+                total += got.numel()
+            if prev_full is not None:
+                pairs.append((prev_full.cpu().numpy(), tiler.frame_buf.cpu().numpy()))
+        verify = {"verified": bad == 0, "frames": max(1, args.verify_frames),
+                  "mismatched_elements": bad, "elements": total,
                   "against": "exact walks (STATS instance, counters on) on a copy of the same "
                              "history, every part of this rank"}
         ok = torch.tensor([1 if bad == 0 else 0], device=dev)
@@ -364,23 +373,31 @@ def main():
                 prof_note = pj.get("source")
         cpu = None
         oracle_check = None
+        frame_o = None
+        cores = host_cores() if world == 1 else None
+        cam1 = vrt.make_camera(w, h)
         if world == 1 and args.cpu_seconds > 0:
-            cores = host_cores()
             threads = args.cpu_threads or cores["threads"]
-            cam1 = vrt.make_camera(w, h)
             cpu, frame_o = cpu_baseline(cam1, vox_host, n, params, args.cpu_seconds, threads)
             cpu.update({k: v for k, v in cores.items() if k != "threads"})
-            if frame_o is not None and verify is not None and rgba8 and prev_full is not None:
-                # the oracle's frame through the oracle's RGB8 store + temporal filter against the
-                # same history: the timed path's stored bytes must be within 1 LSB (colour within
-                # 1e-4 may straddle a rounding boundary of x*255)
-                import oracle
+        if frame_o is None and args.oracle_check and pairs:
+            import oracle
 
-                _, cur_o = oracle.temporal(frame_o, prev_full.cpu().numpy(), args.alpha)
-                got = tiler.frame_buf.cpu().numpy().astype(np.int16)
-                d = np.abs(got - cur_o.astype(np.int16))
-                oracle_check = {"max_lsb": int(d.max()), "bytes_off_by_one": int((d == 1).sum()),
-                                "bytes": int(d.size), "ok": bool(d.max() <= 1)}
+            frame_o, _, _ = oracle.render(cam1, vox_host, n, params,
+                                          threads=args.cpu_threads or cores["threads"])
+        if frame_o is not None and pairs and rgba8:
+            # the oracle's frame through the oracle's RGB8 store + temporal filter against the
+            # same history, frame by frame: the timed path's stored bytes must be within 1 LSB
+            # (colour within 1e-4 may straddle a rounding boundary of x*255)
+            import oracle
+
+            worst, off1, nbytes = 0, 0, 0
+            for prev_np, got_np in pairs:
+                _, cur_o = oracle.temporal(frame_o, prev_np, args.alpha)
+                d = np.abs(got_np.astype(np.int16) - cur_o.astype(np.int16))
+                worst, off1, nbytes = max(worst, int(d.max())), off1 + int((d == 1).sum()), nbytes + d.size
+            oracle_check = {"frames": len(pairs), "max_lsb": worst, "bytes_off_by_one": off1,
+                            "bytes": nbytes, "ok": worst <= 1}
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
             "value": round(value, 3),

@@ -10,7 +10,9 @@
 //     (:397-404) when --day-night is given, noise uniforms (:156-158)
 //   - RGB8 store + temporal filter + FBO swap (:363-393) -> vrt_render_frame
 //   - "Clear framebuffer" (key F, :417-421) -> vrt_history_reset, via --reset-at K
-//   - the GUI's FPS label from GL_TIME_ELAPSED (:350-360) -> vrt_stats.kernel_ms
+//   - the GUI's FPS label from GL_TIME_ELAPSED (:350-360) -> vrt_stats.kernel_ms (timing only:
+//     the fast kernel instance; --counters also counts rays, which runs the exact instance)
+//   - more than one GPU (--device-mask): vrt_create's mask, the frame split into row bands
 //   - Utils::Screenshot of the last frame (key F1, :424-428) -> a binary PPM (--ppm), and the raw
 //     RGBA8 frame (--raw, row 0 = bottom) for tests
 // Build: make app (-> build/vrt_headless). Usage: build/vrt_headless --help
@@ -35,7 +37,9 @@ struct Options {
   std::string atlas_raw;       // textured mode: raw RGBA8 atlas file (size^2 * 4 bytes)
   int atlas_size = 256, atlas_tile = 128;
   std::string ppm, raw;
-  bool quiet = false;
+  bool quiet = false, counters = false;
+  uint32_t device_mask = 1;  // bit i = HIP device i
+  int warmup = 0;            // frames excluded from the reported mean
 };
 
 void usage() {
@@ -44,7 +48,7 @@ void usage() {
       "             [--bounces R T] [--alpha A] [--ray-noise x] [--reflection-noise x]\n"
       "             [--refraction-noise x] [--day-night SECONDS_PER_FRAME] [--reset-at K]\n"
       "             [--atlas-raw FILE --atlas-size S --atlas-tile T] [--ppm FILE] [--raw FILE]\n"
-      "             [--quiet]");
+      "             [--device-mask M] [--counters] [--warmup K] [--quiet]");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -77,6 +81,9 @@ bool parse(int argc, char** argv, Options& o) {
     else if (a == "--ppm") o.ppm = next("--ppm");
     else if (a == "--raw") o.raw = next("--raw");
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--counters") o.counters = true;
+    else if (a == "--device-mask") o.device_mask = uint32_t(std::strtoul(next(a.c_str()), nullptr, 0));
+    else if (a == "--warmup") o.warmup = std::atoi(next("--warmup"));
     else if (a == "--help" || a == "-h") return false;
     else {
       std::fprintf(stderr, "unknown option %s\n", a.c_str());
@@ -130,7 +137,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   vrt_ctx* rt = nullptr;
-  if (vrt_create(0, &rt) != VRT_OK) {
+  if (vrt_create(o.device_mask, &rt) != VRT_OK) {
     std::fprintf(stderr, "vrt_create failed: %s\n", vrt_last_error(rt));
     return 1;
   }
@@ -171,30 +178,39 @@ int main(int argc, char** argv) {
   float time_of_day = 0.9f * day_time;  // "Make day" (main.cpp:577)
   std::vector<uint8_t> frame(size_t(o.width) * o.height * 4);
   double ms_sum = 0.0;
+  int timed = 0;
   for (int f = 0; f < o.frames && status == 0; ++f) {
     if (f == o.reset_at) vrt_history_reset(rt);  // key F
     p.time = float(f + 1);                       // static i; i++ (main.cpp:343-345)
     vrt_sun_dir(time_of_day, day_time, p.sun_dir);
     vrt_stats st;
+    std::memset(&st, 0, sizeof(st));
+    st.request = o.counters ? VRT_STATS_COUNTERS : 0u;
     if (vrt_render_frame(rt, &cam, &p, o.alpha, frame.data(), &st) != VRT_OK) {
       std::fprintf(stderr, "vrt_render_frame: %s\n", vrt_last_error(rt));
       status = 1;
       break;
     }
-    ms_sum += st.kernel_ms;
+    if (f >= o.warmup) {
+      ms_sum += st.kernel_ms;
+      ++timed;
+    }
     const uint64_t rays = st.counters[VRT_CNT_PRIMARY_RAYS] + st.counters[VRT_CNT_SECONDARY_RAYS] +
                           st.counters[VRT_CNT_SHADOW_RAYS];
-    if (!o.quiet)
-      std::printf("frame %d  %.3f ms  fps %.0f  rays %llu  %.0f Mrays/s\n", f, st.kernel_ms,
+    if (!o.quiet && o.counters)
+      std::printf("frame %d  %.4f ms  fps %.0f  rays %llu  %.0f Mrays/s\n", f, st.kernel_ms,
                   1000.0 / st.kernel_ms, (unsigned long long)rays, rays / (st.kernel_ms * 1e3));
+    else if (!o.quiet)
+      std::printf("frame %d  %.4f ms  fps %.0f\n", f, st.kernel_ms, 1000.0 / st.kernel_ms);
     if (o.frame_seconds > 0.0f) {  // Update(): day/night cycle (main.cpp:397-404)
       time_of_day += o.frame_seconds;
       while (time_of_day > day_time) time_of_day -= day_time;
     }
   }
-  if (status == 0 && !o.quiet)
-    std::printf("%d frames, mean %.3f ms (kernel + counters, synchronous API)\n", o.frames,
-                ms_sum / o.frames);
+  if (status == 0 && timed > 0)
+    std::printf("timed %d frames (after %d warm-up) on %d device(s): mean %.4f ms GPU time per frame%s\n",
+                timed, o.warmup, vrt_device_count(rt), ms_sum / timed,
+                o.counters ? " (exact instance, counting)" : "");
   if (status == 0 && !o.raw.empty() && !write_file(o.raw, frame.data(), frame.size())) status = 1;
   if (status == 0 && !o.ppm.empty() && !write_ppm(o.ppm, frame, o.width, o.height)) status = 1;
   vrt_destroy(rt);

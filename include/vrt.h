@@ -14,6 +14,10 @@
  *   - Not thread-safe per context: one context per host thread (as the GL context was).
  *   - Volumes are N^3 bytes, x fastest: idx = x + y*N + z*N*N   (main.cpp:227).
  *   - Images are W*H RGBA float, row 0 = bottom row (GL window convention).
+ *   - A context spans one or more GPUs (vrt_create's device mask). Whole-frame entry points
+ *     (vrt_render, vrt_render_frame, vrt_render_frame_device) split the frame into cyclic row
+ *     bands, one per device, each rendered as two interleaved row parts on two context-owned
+ *     streams; the *_async band entry points run on the context's first (root) device.
  */
 #ifndef VRT_H
 #define VRT_H
@@ -24,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 7
+#define VRT_ABI_VERSION 8
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -97,32 +101,51 @@ enum {
   VRT_CNT_COUNT
 };
 
+/* Statistics of a synchronous render. kernel_ms is always filled: the GPU time of the frame's
+ * launches (hipEvents, the max over the context's devices), like the reference's GL_TIME_ELAPSED
+ * query (main.cpp:350-360). Counters are filled only when requested (request |=
+ * VRT_STATS_COUNTERS): counting runs the exact-walk instance, ~3x slower than the uncounted
+ * frame, so timing alone never asks for it. */
+#define VRT_STATS_COUNTERS 1u
 typedef struct {
-  uint64_t counters[VRT_CNT_COUNT];
-  float kernel_ms;            /* hipEvent time of the render (kernel + counter reduction) */
-  float reserved[3];
+  uint64_t counters[VRT_CNT_COUNT];  /* out (when requested) */
+  float kernel_ms;                   /* out */
+  uint32_t request;                  /* in: VRT_STATS_* bits */
+  float reserved[2];
 } vrt_stats;
 
 /* ---- context / device ---------------------------------------------------------------------- */
 
-/* Create a context on HIP device `device` (ordinal). */
-int vrt_create(int device, vrt_ctx** out);
+/* Create a context on the HIP devices of `device_mask` (bit i = device ordinal i):
+ * one device renders whole frames; k devices split every whole frame into k cyclic row bands
+ * (device j of the mask renders rows j, j+k, ...; the volume is replicated on every device:
+ * RCCL broadcast from the first device, RCCL communicators over the mask's devices). */
+int vrt_create(uint32_t device_mask, vrt_ctx** out);
+/* Same over an explicit device list; a device may repeat (rehearses a k-device split on fewer
+ * GPUs: the bands and the gather then use device-to-device copies instead of RCCL). */
+int vrt_create_devices(const int32_t* devices, int32_t count, vrt_ctx** out);
+/* Devices of the context (k), and the ordinal of its i-th device (-1 if out of range). */
+int vrt_device_count(const vrt_ctx* ctx);
+int vrt_device_ordinal(const vrt_ctx* ctx, int32_t i);
 void vrt_destroy(vrt_ctx* ctx);
 const char* vrt_last_error(const vrt_ctx* ctx);  /* never NULL; "" when no error */
 int vrt_abi_version(void);
 
-/* Copy the volume to device memory (replaces glTexImage3D, main.cpp:315-318). The caller keeps
- * ownership of `vol->voxels`. N must be a power of two in [2, 1024]. */
+/* Copy the volume to device memory (replaces glTexImage3D, main.cpp:315-318): host -> the first
+ * device, then a broadcast to the others. The caller keeps ownership of `vol->voxels`. N must be
+ * a power of two in [2, 1024]. */
 int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol);
 
-/* Same from a DEVICE buffer of N^3 bytes on this context's GPU (e.g. after an RCCL broadcast of
- * the volume to every GPU of the node), ordered on `hip_stream`; returns after the copy. */
+/* Same from a DEVICE buffer of N^3 bytes on the context's first GPU (e.g. after an RCCL broadcast
+ * of the volume to every GPU of the node by the caller), ordered on `hip_stream`; the context's
+ * other devices receive it by broadcast; returns after the copy. */
 int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream);
 
 /* Build the _TERRAIN / _GLASS_CUBE / _REFRACTION volume of main.cpp:218-288 directly on the device
  * (bytes identical to vrt_build_scene; only the n*n terrain heightfield is computed on the host)
  * and make it the context's volume, ordered on `hip_stream`; returns after the build. N must be
- * a power of two in [8, 1024]. Replaces the host build + glTexImage3D upload (main.cpp:315-318). */
+ * a power of two in [8, 1024]. Replaces the host build + glTexImage3D upload (main.cpp:315-318).
+ * Every device of the context builds its own replica (no transfer). */
 int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed, void* hip_stream);
 
 /* Device pointer of the resident volume (N^3 bytes, canonical layout), e.g. for a broadcast.
@@ -169,7 +192,10 @@ int vrt_certified(const vrt_ctx* ctx);
  * longest waves start first. Device state per band and stream: 3 x tiles words, up to 8 bands x
  * streams, allocated and zeroed on the launch stream at first use (recycling one synchronises the
  * device). Launches on a stream that is being captured into a graph use dispatch order. Every
- * tile is rendered exactly once in any case: images are identical with and without it. */
+ * tile is rendered exactly once in any case: images are identical with and without it.
+ * ABI v8: the state is a pool allocated by vrt_create (8 slots of bands up to 65536 tiles, i.e.
+ * 4096 x 4096 pixels; larger bands use dispatch order); reusing a slot on another stream waits
+ * for its last launch on the device (hipStreamWaitEvent), never on the host. */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
@@ -179,7 +205,8 @@ int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_
 
 /* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats
  * (alpha = 1, voxel.glsl:451) to the HOST buffer out_rgba. out_hit (W*H records) and stats may
- * be NULL. */
+ * be NULL. Hit records or counters run the exact-walk instance; otherwise the fast instance on
+ * the context's streams. Each device copies its band straight into the host rows. */
 int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
                float* out_rgba, vrt_hit* out_hit, vrt_stats* stats);
 
@@ -188,7 +215,8 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
  * d_out_rgba / d_out_hit holds frame row row0 + i*row_step. d_out_hit and d_counters
  * (VRT_CNT_COUNT uint64, ACCUMULATED into; the caller zeroes them) may be NULL. Counting uses a
  * per-context replica buffer: at most one counted render per context in flight at a time.
- * No host sync, no allocation: capturable in a hipGraph. */
+ * No host sync, no allocation: capturable in a hipGraph (the tile order is skipped while the
+ * stream is being captured). Runs on the context's first device. */
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
                           int32_t row0, int32_t rows, int32_t row_step,
                           float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
@@ -244,12 +272,24 @@ int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
                                            uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
                                            uint64_t* d_counters, void* hip_stream);
 
-/* Synchronous frame loop of main.cpp:323-393 with the two history FBOs and the ray-trace FBO kept
- * in the context: render, filter against the last filtered frame, copy the new filtered frame to
- * the HOST buffer out_rgba8 (W*H*4 bytes), then swap (PostRender). The history starts black and
- * restarts black when the image size changes. stats may be NULL. */
+/* Synchronous frame loop of main.cpp:323-393 with the history and the ray-trace FBO kept in the
+ * context: render, filter against the last filtered frame, copy the new filtered frame to the
+ * HOST buffer out_rgba8 (W*H*4 bytes). The history starts black and restarts black when the image
+ * size changes. stats may be NULL. Each device renders its row band as two interleaved parts on
+ * its two context-owned streams (one launch's tail overlaps the other's) and filters it in
+ * place; the bands are copied straight into the host rows (no device-side gather). */
 int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params, float alpha,
                      uint8_t* out_rgba8, vrt_stats* stats);
+
+/* ABI v8: the same frame assembled on the first device: the new filtered frame (W*H RGBA8 words,
+ * row 0 = bottom) is written to the DEVICE buffer d_out_rgba8 on the context's first GPU, ordered
+ * after prior work on hip_stream and before later work on it (e.g. a texture upload for display).
+ * With several devices the bands are gathered to the first one over xGMI by ncclGather
+ * (rccl.h) and placed into their rows by strided copies; one device copies its frame. Returns
+ * after the launches (asynchronous); stats (kernel_ms only) may be NULL and then no host sync
+ * happens. */
+int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
+                            float alpha, uint32_t* d_out_rgba8, void* hip_stream, vrt_stats* stats);
 
 /* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history. */
 int vrt_history_reset(vrt_ctx* ctx);
@@ -276,6 +316,14 @@ void vrt_sun_dir(float time_of_day, float day_time, float out[3]);
 
 /* Default params for the bench configs (noise 0, max_ray_length 100, colour-only, time 1). */
 void vrt_params_default(vrt_params* out);
+
+/* ABI v8: the row plan of a whole frame of `height` rows over k devices with `parts` interleaved
+ * parts each (host arithmetic, no GPU): for band j (device j) and part p, the frame rows
+ * row0 + i*row_step (i < rows) that the part renders, written to band-buffer row
+ * band_row0 + i*parts. out[(j*parts + p)*4 + 0..3] = {row0, rows, row_step, band_row0}; a band
+ * holds ceil((height - j) / k) rows, band row r = frame row j + r*k. Returns the largest band's
+ * rows. Used by the whole-frame entry points; exported for tests. */
+int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out);
 
 #ifdef __cplusplus
 }

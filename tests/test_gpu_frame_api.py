@@ -1,0 +1,128 @@
+"""GPU: the whole-frame entry points of the C-ABI (ABI v8) — the drop-in's fast path.
+
+vrt_render_frame (main.cpp:323-393 as one call) now renders each device band as two interleaved
+row parts on two context-owned streams with the fast (certified, uncounted) instance; timing
+alone (vrt_stats.kernel_ms) no longer selects the exact-walk instance, counting does
+(VRT_STATS_COUNTERS). Checked here:
+  - frames are bit-identical to the exact instance's, over consecutive frames with alpha < 1;
+  - a context over a device list splits the frame into cyclic row bands (vrt_create_devices with
+    a repeated ordinal rehearses a k-device split on one GPU): identical frames, float frames and
+    hit records;
+  - vrt_render_frame_device assembles the same frame on the first device;
+  - the C++ host (examples/headless_app.cpp) gets the bench's per-frame GPU time through the ABI.
+The RCCL paths (ncclBroadcast of the volume, ncclGather of the bands) need two distinct GPUs and
+are not exercised on the one-GPU test box."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import voxelraytracer_amd as vrt
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APP = os.path.join(ROOT, "build", "bin", "vrt_headless")
+
+
+def sequence(dev, scene, n, w, h, R, T, alphas, counters=False, **kw):
+    with vrt.Renderer(dev) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        cam = vrt.make_camera(w, h)
+        out = []
+        for i, a in enumerate(alphas):
+            p = vrt.default_params(R, T, time=float(i + 1), **kw)
+            f, st = r.render_frame(cam, p, a, counters=counters)
+            out.append(f)
+            if not counters:
+                assert st["kernel_ms"] > 0 and st["pixels"] == 0
+            else:
+                assert st["pixels"] == w * h
+        return out
+
+
+CASES = [("refraction", 128, 480, 270, 4, 4, {}), ("glass_cube", 64, 320, 180, 1, 2, {}),
+         ("terrain", 64, 256, 144, 4, 2, dict(ray_noise=0.02))]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_frame_fast_path_equals_exact_instance(built, case):
+    scene, n, w, h, R, T, kw = case
+    alphas = [1.0, 0.5, 0.5, 0.3]
+    fast = sequence(0, scene, n, w, h, R, T, alphas, **kw)
+    exact = sequence(0, scene, n, w, h, R, T, alphas, counters=True, **kw)
+    for k, (a, b) in enumerate(zip(fast, exact)):
+        assert np.array_equal(a, b), f"frame {k}"
+
+
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]], ids=["k2", "k3"])
+def test_device_list_splits_frames_into_bands(built, devs):
+    scene, n, w, h, R, T = "refraction", 64, 200, 121, 4, 4   # 121 rows: unequal bands
+    alphas = [1.0, 0.5, 0.5]
+    one = sequence(0, scene, n, w, h, R, T, alphas)
+    many = sequence(devs, scene, n, w, h, R, T, alphas)
+    for k, (a, b) in enumerate(zip(one, many)):
+        assert np.array_equal(a, b), f"frame {k}"
+    with vrt.Renderer(devs) as r, vrt.Renderer(0) as r1:
+        assert r.device_count() == len(devs)
+        vox = vrt.build_scene(scene, n)
+        r.upload_volume(vox, n)
+        r1.upload_volume(vox, n)
+        cam = vrt.make_camera(w, h)
+        p = vrt.default_params(R, T)
+        for hits, counters in ((True, True), (False, False)):
+            a, ha, sa = r.render(cam, p, want_hits=hits, counters=counters)
+            b, hb, sb = r1.render(cam, p, want_hits=hits, counters=counters)
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+            if hits:
+                assert np.array_equal(ha, hb)
+            if counters:
+                assert {k: v for k, v in sa.items() if k != "kernel_ms"} == \
+                       {k: v for k, v in sb.items() if k != "kernel_ms"}
+
+
+@pytest.mark.parametrize("devs", [0, [0, 0]], ids=["k1", "k2"])
+def test_frame_device_output(built, devs):
+    scene, n, w, h, R, T = "refraction", 128, 320, 181, 4, 4
+    ref = sequence(0, scene, n, w, h, R, T, [1.0, 0.5])
+    with vrt.Renderer(devs) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        cam = vrt.make_camera(w, h)
+        s = torch.cuda.Stream()
+        outs = []
+        for i, a in enumerate([1.0, 0.5]):
+            d = torch.full((h, w, 4), 7, dtype=torch.uint8, device="cuda")
+            s.wait_stream(torch.cuda.current_stream())
+            ms = r.render_frame_device(cam, vrt.default_params(R, T, time=float(i + 1)), a,
+                                       d.data_ptr(), s.cuda_stream, timing=(i == 1))
+            torch.cuda.current_stream().wait_stream(s)
+            outs.append(d.cpu().numpy())
+        assert ms is not None and ms > 0
+    for k, (a, b) in enumerate(zip(outs, ref)):
+        assert np.array_equal(a, b), f"frame {k}"
+
+
+def test_headless_app_gets_the_bench_frame_time(built):
+    """vrt_headless (C++ over the C-ABI, vrt_render_frame) at C3: its per-frame GPU time is within
+    10 % of bench.py's per-frame GPU time of the same workload (both uncounted, certified, two
+    parts); the C++ host inherits HIP's default hardware-queue count."""
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    r = subprocess.run([APP, "--scene", "refraction", "--n", "128", "--size", "1920x1080",
+                        "--bounces", "4", "4", "--frames", "400", "--warmup", "200", "--quiet"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr
+    app_ms = float(re.search(r"mean ([0-9.]+) ms", r.stdout).group(1))
+    b = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C3",
+                        "--steps", "200", "--warmup", "200", "--cpu-seconds", "0", "--no-verify"],
+                       capture_output=True, text=True, timeout=240)
+    assert b.returncode == 0, b.stderr[-2000:]
+    out = json.loads([l for l in b.stdout.splitlines() if l.startswith("{")][-1])
+    bench_ms = out["roofline"]["kernel_ms"]
+    print(f"vrt_headless {app_ms:.4f} ms/frame, bench {bench_ms:.4f} ms/frame")
+    assert app_ms <= 1.10 * bench_ms, (app_ms, bench_ms)

@@ -104,7 +104,7 @@ def test_frame_loop_history_and_reset(renderer):
     renderer.render_temporal_rows_async(cam, p, 1.0, 0, h, 1, zeros.data_ptr(), d_raw.data_ptr())
     torch.cuda.synchronize()
     raw = d_raw.cpu().numpy()             # the frame's quantised colour (deterministic)
-    f1, st = renderer.render_frame(cam, p, 0.5)
+    f1, st = renderer.render_frame(cam, p, 0.5, counters=True)
     assert np.array_equal(f1, oracle.temporal_from_raw(raw, np.zeros_like(raw), 0.5))
     f2, _ = renderer.render_frame(cam, p, 0.5)
     assert np.array_equal(f2, oracle.temporal_from_raw(raw, f1, 0.5))

@@ -159,17 +159,37 @@ def total_rays(c: dict) -> int:
     return c["primary_rays"] + c["secondary_rays"] + c["shadow_rays"]
 
 
-class Renderer:
-    """One vrt_ctx on one HIP device (replaces the GL context + FrameBuffer of the reference)."""
+def band_plan(height: int, k: int, parts: int = 2):
+    """The library's whole-frame row plan (vrt_band_plan): ({(band j, part p): (row0, rows,
+    row_step, band_row0)}, rows of the largest band). Band j holds frame rows j, j+k, ..."""
+    out = np.zeros(k * parts * 4, np.int32)
+    cap = lib().vrt_band_plan(height, k, parts, out.ctypes.data)
+    if cap < 0:
+        raise VrtError(cap, "vrt_band_plan")
+    o = out.reshape(k, parts, 4)
+    return {(j, p): tuple(int(v) for v in o[j, p]) for j in range(k) for p in range(parts)}, cap
 
-    def __init__(self, device: int = 0):
+
+class Renderer:
+    """One vrt_ctx (replaces the GL context + FrameBuffer of the reference). `device` is a HIP
+    device ordinal, or a sequence of ordinals: whole frames are then split into row bands across
+    them (vrt_create's device mask; a repeated ordinal rehearses the split on one GPU)."""
+
+    def __init__(self, device=0):
         self._lib = lib()
         h = C.c_void_p()
-        rc = self._lib.vrt_create(device, C.byref(h))
+        if isinstance(device, int):
+            rc = self._lib.vrt_create(1 << device, C.byref(h))
+        else:
+            devs = (C.c_int32 * len(device))(*device)
+            rc = self._lib.vrt_create_devices(devs, len(device), C.byref(h))
         if rc != 0:
             raise VrtError(rc, f"vrt_create(device={device}) failed (no GPU?)")
         self._h = h
         self.n = None
+
+    def device_count(self) -> int:
+        return self._lib.vrt_device_count(self._h)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -233,12 +253,15 @@ class Renderer:
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 
-    def render(self, cam: Camera, params: Params, want_hits: bool = True):
-        """Synchronous frame: returns (rgba[H,W,4] float32, hits[H,W] structured or None, stats)."""
+    def render(self, cam: Camera, params: Params, want_hits: bool = True, counters: bool = True):
+        """Synchronous frame: returns (rgba[H,W,4] float32, hits[H,W] structured or None, stats).
+        Hit records or counters run the exact-walk instance; with neither, the fast instance
+        renders and stats holds kernel_ms only."""
         w, h = cam.width, cam.height
         rgba = np.empty((h, w, 4), dtype=np.float32)
         hits = np.empty((h, w), dtype=HIT_DTYPE) if want_hits else None
         st = abi.Stats()
+        st.request = abi.VRT_STATS_COUNTERS if counters else 0
         self._check(
             self._lib.vrt_render(self._h, C.byref(cam), C.byref(params), rgba.ctypes.data,
                                  hits.ctypes.data if want_hits else None, C.byref(st)),
@@ -291,16 +314,30 @@ class Renderer:
             "vrt_render_temporal_rows_async",
         )
 
-    def render_frame(self, cam: Camera, params: Params, alpha: float = 1.0):
+    def render_frame(self, cam: Camera, params: Params, alpha: float = 1.0, counters: bool = False):
         """main.cpp's frame loop with the history in the context (vrt_render_frame): returns the
-        new filtered frame as rgba8[H,W,4] uint8 and the stats."""
+        new filtered frame as rgba8[H,W,4] uint8 and the stats (counters only when asked: they
+        run the exact-walk instance)."""
         out = np.empty((cam.height, cam.width, 4), dtype=np.uint8)
         st = abi.Stats()
+        st.request = abi.VRT_STATS_COUNTERS if counters else 0
         self._check(self._lib.vrt_render_frame(self._h, C.byref(cam), C.byref(params), alpha,
                                                out.ctypes.data, C.byref(st)), "vrt_render_frame")
         stats = counters_dict(st.counters)
         stats["kernel_ms"] = float(st.kernel_ms)
         return out, stats
+
+    def render_frame_device(self, cam: Camera, params: Params, alpha: float, d_out: int,
+                            stream: int = 0, timing: bool = False):
+        """vrt_render_frame_device: the filtered frame assembled on the first device into d_out
+        (W*H RGBA8 words, e.g. a torch uint32/uint8 tensor's data_ptr()), ordered on `stream`.
+        timing=True waits for the frame and returns kernel_ms."""
+        st = abi.Stats() if timing else None
+        self._check(self._lib.vrt_render_frame_device(self._h, C.byref(cam), C.byref(params), alpha,
+                                                      d_out, stream or None,
+                                                      C.byref(st) if st is not None else None),
+                    "vrt_render_frame_device")
+        return float(st.kernel_ms) if st is not None else None
 
     def history_reset(self):
         """Key F (main.cpp:417-421): the last ray-traced frame becomes the temporal history."""

@@ -77,11 +77,15 @@ class Hit(C.Structure):
     ]
 
 
+VRT_STATS_COUNTERS = 1   # vrt_stats.request: count (runs the exact-walk instance)
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("counters", C.c_uint64 * VRT_CNT_COUNT),
         ("kernel_ms", C.c_float),
-        ("reserved", C.c_float * 3),
+        ("request", C.c_uint32),
+        ("reserved", C.c_float * 2),
     ]
 
 
@@ -91,7 +95,11 @@ HIT_DTYPE = [("voxel_index", "<i4"), ("ray_length", "<f4"), ("steps", "<u4"), ("
 # name -> (restype, argtypes): every function include/vrt.h declares
 SIGNATURES = {
     "vrt_abi_version": (C.c_int, []),
-    "vrt_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "vrt_create": (C.c_int, [C.c_uint32, C.POINTER(C.c_void_p)]),
+    "vrt_create_devices": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "vrt_device_count": (C.c_int, [C.c_void_p]),
+    "vrt_device_ordinal": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_band_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     "vrt_destroy": (None, [C.c_void_p]),
     "vrt_last_error": (C.c_char_p, [C.c_void_p]),
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),
@@ -142,6 +150,11 @@ SIGNATURES = {
     "vrt_render_frame": (
         C.c_int,
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p, C.POINTER(Stats)],
+    ),
+    "vrt_render_frame_device": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p, C.c_void_p,
+         C.POINTER(Stats)],
     ),
     "vrt_history_reset": (C.c_int, [C.c_void_p]),
     "vrt_upload_atlas": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),

@@ -1,0 +1,979 @@
+// vrt_context.cpp — the C-ABI context of include/vrt.h around the kernels of vrt_render.hip.
+//
+// A context spans the devices of its mask. Every device holds a "shard": a
+// replica of the volume in the kernel's packed layout, two context-owned part streams, its row
+// band's history / ray-trace / float buffers, counters and the tile-order pool. Whole-frame entry
+// points split the frame into cyclic row bands (device j renders rows j, j+k, ...; sky and
+// geometry rows balance across devices) and each band into two interleaved row parts, one per
+// part stream, so one launch's last dispatch round overlaps the other's (DESIGN.md §6 "Tail
+// hiding"). The reference's single GL draw (main.cpp:323-361) becomes 2k concurrent launches.
+// The only exchange is the output: host outputs are written by each device straight into its
+// host rows (k PCIe links in parallel, no device hop); the device-output frame is gathered to
+// the first device with ncclGather over xGMI (rccl.h:745). The volume reaches the other devices
+// by ncclBroadcast from the first one.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vrt.h"
+#include "vrt_internal.h"
+
+namespace {
+
+constexpr int kParts = 2;              // interleaved row parts per device band
+constexpr int kOrderSlots = 8;         // tile-order buffers per device (band geometry x stream)
+constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 4096 x 4096 pixels
+
+struct OrderSlot {
+  int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
+  hipStream_t stream = nullptr;
+  uint32_t* d = nullptr;       // 3 x kOrderMaxTiles words inside the shard's pool
+  hipEvent_t done = nullptr;   // recorded after every launch that used the slot
+  bool used = false;
+  uint64_t epoch = 0, tick = 0;
+};
+
+struct Shard {
+  int device = 0;
+  // volume: canonical N^3, distance scratch, the kernel's packed octant volumes
+  uint8_t* d_vox = nullptr;
+  uint8_t* d_tmp = nullptr;
+  uint16_t* d_vox_pad = nullptr;
+  int32_t n = 0, octants = 0;
+  bool cert_auto = true;   // automatic certified-pixel choice for the resident volume
+  bool has_glass = true;   // the resident volume has glass (bounce stacks; tile order)
+  unsigned long long* d_vstats = nullptr;  // glass and non-empty voxel counts
+  // counters
+  unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of a synchronous render
+  unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
+  // streams and events of whole-frame renders
+  hipStream_t part[kParts] = {nullptr, nullptr};
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;  // timing, on part[0]
+  hipEvent_t ev_join = nullptr;                      // part[1] done
+  // this device's row band of the whole-frame buffers (band_cap rows x width)
+  uint32_t* d_hist = nullptr;  // filtered frame = temporal history, filtered in place
+  uint32_t* d_raw = nullptr;   // quantised ray-trace frame (the rayTrace FBO; key F)
+  size_t hist_pixels = 0;
+  float4* d_out = nullptr;     // vrt_render's float band
+  vrt_hit* d_hit = nullptr;
+  size_t out_pixels = 0;
+  // textured mode's atlas (RGBA8 words)
+  uint32_t* d_atlas = nullptr;
+  int32_t atlas_size = 0;
+  // heavy-first tile order
+  uint32_t* d_order_pool = nullptr;
+  OrderSlot order[kOrderSlots];
+  uint64_t order_tick = 0;
+};
+
+}  // namespace
+
+struct vrt_ctx {
+  std::vector<Shard> sh;
+  bool distinct = true;                 // devices pairwise distinct: RCCL communicators exist
+  std::vector<ncclComm_t> comms;
+  int32_t layout_req = 0;               // vrt_set_skip_layout
+  int32_t cert_req = 0;                 // vrt_set_certified
+  bool tile_order = true;               // vrt_set_tile_order
+  const uint8_t* atlas_src = nullptr;   // host buffer of the last atlas upload
+  int32_t hist_w = 0, hist_h = 0;       // image size of the resident whole-frame history
+  uint32_t* d_gather = nullptr;         // first device: k x band_cap x width words (ncclGather)
+  size_t gather_pixels = 0;
+  hipEvent_t ev_gathered = nullptr;     // first device: the last device-output frame is assembled
+  bool gather_pending = false;
+  std::string err;
+};
+
+namespace {
+
+int fail(vrt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(vrt_ctx* c, hipError_t e, const char* what) {
+  return fail(c, VRT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int nccl_fail(vrt_ctx* c, ncclResult_t r, const char* what) {
+  return fail(c, VRT_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+#define VRT_HIP(ctx, call)                                   \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
+  } while (0)
+
+#define VRT_NCCL(ctx, call)                                    \
+  do {                                                         \
+    ncclResult_t r_ = (call);                                  \
+    if (r_ != ncclSuccess) return nccl_fail((ctx), r_, #call); \
+  } while (0)
+
+// The caller's current device is restored when an entry point returns (entry points switch
+// between the context's devices).
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() { (void)hipGetDevice(&dev); }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
+int32_t band_rows(int32_t height, int32_t k, int32_t j) { return j < height ? (height - j + k - 1) / k : 0; }
+int32_t band_cap(int32_t height, int32_t k) { return (height + k - 1) / k; }
+
+// Part p of band j: frame rows (j + p k) + i (k P), band rows p + i P.
+struct PartRows {
+  int32_t row0, rows, row_step, band_row0;
+};
+PartRows part_rows(int32_t height, int32_t k, int32_t parts, int32_t j, int32_t p) {
+  const int32_t hb = band_rows(height, k, j);
+  return PartRows{j + p * k, hb > p ? (hb - p + parts - 1) / parts : 0, k * parts, p};
+}
+
+void shard_free(Shard& s) {
+  (void)hipSetDevice(s.device);
+  for (void* p : {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats, (void*)s.d_cnt,
+                  (void*)s.d_cnt_rep, (void*)s.d_hist, (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
+                  (void*)s.d_atlas, (void*)s.d_order_pool})
+    if (p) (void)hipFree(p);
+  for (auto& o : s.order)
+    if (o.done) (void)hipEventDestroy(o.done);
+  for (hipEvent_t e : {s.ev_start, s.ev_stop, s.ev_join})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t st : s.part)
+    if (st) (void)hipStreamDestroy(st);
+  s = Shard();
+}
+
+hipError_t shard_init(Shard& s, int device) {
+  s.device = device;
+  hipError_t e = hipSetDevice(device);
+  const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
+  const size_t pool_words = size_t(kOrderSlots) * 3u * kOrderMaxTiles;
+  for (int p = 0; p < kParts && e == hipSuccess; ++p) e = hipStreamCreateWithFlags(&s.part[p], hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&s.ev_start);
+  if (e == hipSuccess) e = hipEventCreate(&s.ev_stop);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&s.d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT);
+  if (e == hipSuccess) e = hipMalloc(&s.d_cnt_rep, rep_bytes);
+  if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
+  if (e == hipSuccess) e = hipMalloc(&s.d_order_pool, pool_words * sizeof(uint32_t));
+  for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) {
+    s.order[i].d = s.d_order_pool + size_t(i) * 3u * kOrderMaxTiles;
+    e = hipEventCreateWithFlags(&s.order[i].done, hipEventDisableTiming);
+  }
+  return e;
+}
+
+int upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t size) {
+  if (!rgba || size < 1 || size > 8192 || (size & (size - 1)) != 0)
+    return fail(ctx, VRT_ERR_INVALID, "atlas edge must be a power of two in [1, 8192]");
+  const size_t bytes = size_t(size) * size * 4;
+  for (Shard& s : ctx->sh) {
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    if (s.atlas_size != size) {
+      if (s.d_atlas) (void)hipFree(s.d_atlas);
+      s.d_atlas = nullptr;
+      s.atlas_size = 0;
+      if (hipMalloc(&s.d_atlas, bytes) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc atlas");
+    }
+    VRT_HIP(ctx, hipMemcpy(s.d_atlas, rgba, bytes, hipMemcpyHostToDevice));
+    s.atlas_size = size;
+  }
+  ctx->atlas_src = rgba;
+  return VRT_OK;
+}
+
+int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) {
+  if (!cam || !p) return fail(ctx, VRT_ERR_INVALID, "null camera or params");
+  if (!ctx->sh[0].d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
+  if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
+    return fail(ctx, VRT_ERR_INVALID, "bad image size");
+  if (!p->color_only) {  // textured mode: the context's atlas (uploaded here when it changes)
+    if (p->atlas_rgba && (p->atlas_rgba != ctx->atlas_src || p->atlas_size != ctx->sh[0].atlas_size)) {
+      const int st = upload_atlas(ctx, p->atlas_rgba, p->atlas_size);
+      if (st != VRT_OK) return st;
+    }
+    if (!ctx->sh[0].d_atlas || p->atlas_size != ctx->sh[0].atlas_size)
+      return fail(ctx, VRT_ERR_INVALID, "textured mode needs an atlas of atlas_size (vrt_upload_atlas)");
+    if (p->atlas_texture_size <= 0) return fail(ctx, VRT_ERR_INVALID, "atlas_texture_size must be > 0");
+  }
+  if (p->max_reflections < 0 || p->max_transparencies < 0 ||
+      p->max_reflections + p->max_transparencies + 1 > vrt::kMaxStack)
+    return fail(ctx, VRT_ERR_UNSUPPORTED, "max_reflections + max_transparencies must be <= 16");
+  return VRT_OK;
+}
+
+vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, const vrt_params* p,
+                     int32_t row0, int32_t rows, int32_t row_step) {
+  vrt::KArgs a;
+  std::memcpy(a.inv_pv, cam->inv_pv, sizeof(a.inv_pv));
+  std::memcpy(a.sun, p->sun_dir, sizeof(a.sun));
+  a.sky_sy = std::fmax(p->sun_dir[1], 0.0f);  // GLSL max(x, 0) with fmaxf's NaN rule, as gmax
+  // normalize(u_SunDir) exactly as the kernel's normalize3 (IEEE single ops, no contraction)
+  const float sx = p->sun_dir[0], sy = p->sun_dir[1], sz = p->sun_dir[2];
+  const float inv = 1.0f / std::sqrt(sx * sx + sy * sy + sz * sz);
+  a.sun_n[0] = sx * inv;
+  a.sun_n[1] = sy * inv;
+  a.sun_n[2] = sz * inv;
+  for (int i = 0; i < 3; ++i) a.sun_rcp[i] = 1.0f / a.sun_n[i];
+  a.time = p->time;
+  a.ray_noise = p->ray_noise;
+  a.refl_noise = p->reflection_noise;
+  a.refr_noise = p->refraction_noise;
+  a.max_len = p->max_ray_length;
+  a.n = s.n;
+  a.fn = float(s.n);
+  a.width = cam->width;
+  a.height = cam->height;
+  a.row0 = row0;
+  a.rows = rows;
+  a.row_step = row_step;
+  a.pitch = cam->width;
+  a.ostride = s.octants == 8 ? uint32_t(uint64_t(s.n + 1) * (s.n + 1) * (s.n + 1) * sizeof(uint16_t)) : 0u;
+  a.max_refl = p->max_reflections;
+  a.max_transp = p->max_transparencies;
+  a.textured = p->color_only ? 0 : 1;
+  a.atlas_size = p->color_only ? 1 : p->atlas_size;
+  a.atlas_tex_size = p->atlas_texture_size;
+  a.atlas = s.d_atlas;
+  a.alpha = 1.0f;
+  a.prev = nullptr;
+  a.cur = nullptr;
+  a.raw = nullptr;
+  a.cert = s.octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || s.cert_auto ? 2 : 1);
+  a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
+  a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
+  a.order = nullptr;
+  a.ord_r = a.ord_w = 0;
+  return a;
+}
+
+// The tile-order slot of this launch's band and stream, from the shard's pool (no allocation, no
+// host sync). Reusing the least recently used slot for another band / stream waits on the device
+// for that slot's last launch, then zeroes it on this stream (no heavy tiles yet). Not while the
+// stream is being captured into a graph (a replayed node would reuse one flag set): dispatch order.
+OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
+  // only where it pays: glass in the volume (no bounce stacks otherwise: the first pass would be
+  // `tiles` empty workgroups, C2/C4 +4 %) and certified pixels (glass-heavy volumes, where most
+  // tiles are heavy, keep dispatch order: C1 +8 %)
+  if (!ctx->tile_order || a.tiles == 0 || a.tiles > kOrderMaxTiles || a.textured || a.cert != 2 ||
+      !s.has_glass)
+    return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+  OrderSlot* slot = nullptr;
+  for (auto& o : s.order)
+    if (o.used && o.width == a.width && o.rows == a.rows && o.row0 == a.row0 && o.row_step == a.row_step &&
+        o.stream == st)
+      slot = &o;
+  if (!slot) {
+    slot = &s.order[0];
+    for (auto& o : s.order)
+      if (!o.used || (slot->used && o.tick < slot->tick)) slot = &o;
+    if (slot->used && hipStreamWaitEvent(st, slot->done, 0) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(slot->d, 0, size_t(3) * a.tiles * sizeof(uint32_t), st) != hipSuccess) return nullptr;
+    slot->width = a.width;
+    slot->rows = a.rows;
+    slot->row0 = a.row0;
+    slot->row_step = a.row_step;
+    slot->stream = st;
+    slot->epoch = 0;
+    slot->used = true;
+  }
+  slot->tick = ++s.order_tick;
+  a.order = slot->d;
+  a.ord_r = uint32_t(slot->epoch & 1u);
+  a.ord_w = uint32_t((slot->epoch + 1u) & 1u);
+  slot->epoch++;
+  return slot;
+}
+
+// One band launch on `st` (heavy-first tile order for uncounted launches), then, when counting,
+// the fold of the counter replicas into `cnt` (accumulating).
+void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
+            hipStream_t st) {
+  const bool stats = hit || cnt;
+  OrderSlot* slot = stats ? nullptr : tile_order_begin(ctx, s, a, st);
+  vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st);
+  if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
+  if (slot) (void)hipEventRecord(slot->done, st);
+}
+
+int volume_alloc(vrt_ctx* ctx, Shard& s, int32_t n) {
+  if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
+    return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
+  VRT_HIP(ctx, hipSetDevice(s.device));
+  // octant layout while 8 padded u16 volumes stay addressable by a 32-bit byte offset
+  const bool fits = uint64_t(n + 1) * (n + 1) * (n + 1) * 2 * 8 <= (uint64_t(1) << 32);
+  const int32_t octants = fits && ctx->layout_req != 1 ? 8 : 1;
+  if (s.d_vox && (s.n != n || s.octants != octants)) {
+    (void)hipFree(s.d_vox);
+    (void)hipFree(s.d_tmp);
+    (void)hipFree(s.d_vox_pad);
+    s.d_vox = s.d_tmp = nullptr;
+    s.d_vox_pad = nullptr;
+  }
+  if (!s.d_vox) {
+    const size_t bytes = size_t(n) * n * n, pbytes = size_t(n + 1) * (n + 1) * (n + 1) * 2 * size_t(octants);
+    if (hipMalloc(&s.d_vox, bytes) != hipSuccess ||
+        hipMalloc(&s.d_tmp, (octants == 8 ? 3 : 2) * bytes) != hipSuccess ||
+        hipMalloc(&s.d_vox_pad, pbytes) != hipSuccess) {
+      if (s.d_vox) (void)hipFree(s.d_vox);
+      if (s.d_tmp) (void)hipFree(s.d_tmp);
+      if (s.d_vox_pad) (void)hipFree(s.d_vox_pad);
+      s.d_vox = s.d_tmp = nullptr;
+      s.d_vox_pad = nullptr;
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume buffers");
+    }
+  }
+  s.n = n;
+  s.octants = octants;
+  return VRT_OK;
+}
+
+int volume_alloc_all(vrt_ctx* ctx, int32_t n) {
+  for (Shard& s : ctx->sh) {
+    const int st = volume_alloc(ctx, s, n);
+    if (st != VRT_OK) return st;
+  }
+  return VRT_OK;
+}
+
+// Distance passes + packing + glass share on every device (canonical bytes already resident on
+// each, ordered on part[0]), then wait (upload is not a hot call).
+int volume_finish_all(vrt_ctx* ctx) {
+  for (Shard& s : ctx->sh) {
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    const uint64_t vol = uint64_t(s.n) * s.n * s.n;
+    vrt::launch_volume_passes(s.d_vox, s.d_tmp, s.d_vox_pad, uint32_t(s.n), s.octants, s.part[0]);
+    // certified walks cannot settle glass pixels (their secondary rays start at the exact hit
+    // point) and a glass pixel pays the certified primary walk before the exact path: the
+    // automatic mode turns them off when glass makes up more than 1/8 of the non-empty voxels
+    if (!s.d_vstats) VRT_HIP(ctx, hipMalloc(&s.d_vstats, 2 * sizeof(unsigned long long)));
+    VRT_HIP(ctx, hipMemsetAsync(s.d_vstats, 0, 2 * sizeof(unsigned long long), s.part[0]));
+    vrt::launch_glass_share(s.d_vox, vol, s.d_vstats, s.part[0]);
+    VRT_HIP(ctx, hipGetLastError());
+  }
+  for (Shard& s : ctx->sh) {
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    unsigned long long vs[2] = {0, 0};
+    VRT_HIP(ctx, hipMemcpyAsync(vs, s.d_vstats, sizeof(vs), hipMemcpyDeviceToHost, s.part[0]));
+    VRT_HIP(ctx, hipStreamSynchronize(s.part[0]));
+    s.cert_auto = vs[0] * 8 <= vs[1];
+    s.has_glass = vs[0] > 0;
+  }
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+// The first device's canonical volume (resident, ordered on its part[0]) to every other device:
+// ncclBroadcast over xGMI, or device-to-device copies when a device repeats.
+int broadcast_volume(vrt_ctx* ctx) {
+  const size_t k = ctx->sh.size();
+  if (k == 1) return VRT_OK;
+  Shard& root = ctx->sh[0];
+  const size_t bytes = size_t(root.n) * root.n * root.n;
+  if (ctx->distinct) {
+    VRT_NCCL(ctx, ncclGroupStart());
+    for (size_t j = 0; j < k; ++j) {
+      Shard& s = ctx->sh[j];
+      (void)hipSetDevice(s.device);
+      const ncclResult_t r = ncclBroadcast(root.d_vox, s.d_vox, bytes, ncclUint8, 0, ctx->comms[j], s.part[0]);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(ctx, r, "ncclBroadcast(volume)");
+      }
+    }
+    VRT_NCCL(ctx, ncclGroupEnd());
+    return VRT_OK;
+  }
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  VRT_HIP(ctx, hipEventRecord(root.ev_join, root.part[0]));
+  for (size_t j = 1; j < k; ++j) {
+    Shard& s = ctx->sh[j];
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], root.ev_join, 0));
+    VRT_HIP(ctx, hipMemcpyPeerAsync(s.d_vox, s.device, root.d_vox, root.device, bytes, s.part[0]));
+  }
+  return VRT_OK;
+}
+
+// Whole-frame band buffers of every device for a W x H frame (history black on (re)creation).
+int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
+  if (w == ctx->hist_w && h == ctx->hist_h) return VRT_OK;
+  const int32_t k = int32_t(ctx->sh.size());
+  const size_t pixels = size_t(band_cap(h, k)) * size_t(w);
+  for (Shard& s : ctx->sh) {
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    VRT_HIP(ctx, hipDeviceSynchronize());  // nothing may still read the old buffers
+    if (pixels > s.hist_pixels) {
+      for (uint32_t** b : {&s.d_hist, &s.d_raw}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+      }
+      s.hist_pixels = 0;
+      if (hipMalloc(&s.d_hist, pixels * 4) != hipSuccess || hipMalloc(&s.d_raw, pixels * 4) != hipSuccess)
+        return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
+      s.hist_pixels = pixels;
+    }
+    VRT_HIP(ctx, hipMemset(s.d_hist, 0, pixels * 4));
+    VRT_HIP(ctx, hipMemset(s.d_raw, 0, pixels * 4));
+  }
+  ctx->hist_w = w;
+  ctx->hist_h = h;
+  ctx->gather_pending = false;
+  return VRT_OK;
+}
+
+// Launch one whole frame on every device: band j as kParts interleaved parts on the part streams
+// (or, when counting or writing hit records, one exact-instance launch on part[0]), bracketed by
+// ev_start / ev_stop on part[0] with part[1] joined. rgba8: the temporal path into d_hist (in
+// place) + d_raw; else the float band into d_out (+ d_hit).
+int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, bool rgba8,
+                 bool hits, bool counting) {
+  const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
+  for (int32_t j = 0; j < k; ++j) {
+    Shard& s = ctx->sh[j];
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    if (ctx->gather_pending && j > 0)  // the last device-output frame still reads this band
+      VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], ctx->ev_gathered, 0));
+    if (counting)
+      VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.part[0]));
+    VRT_HIP(ctx, hipEventRecord(s.ev_start, s.part[0]));
+    const int32_t hb = band_rows(h, k, j);
+    if (hb > 0) {
+      const bool single = counting || hits;  // one counter replica set: one counted launch
+      const int32_t nparts = single ? 1 : kParts;
+      if (!single) VRT_HIP(ctx, hipStreamWaitEvent(s.part[1], s.ev_start, 0));
+      for (int32_t q = 0; q < nparts; ++q) {
+        const PartRows pr = single ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
+        if (pr.rows == 0) continue;
+        vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
+        a.pitch = int32_t(int64_t(w) * (single ? 1 : kParts));
+        const size_t off = size_t(pr.band_row0) * size_t(w);
+        if (rgba8) {
+          a.alpha = alpha;
+          a.prev = s.d_hist + off;
+          a.cur = s.d_hist + off;
+          a.raw = s.d_raw + off;
+          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q]);
+        } else {
+          launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
+                 s.part[q]);
+        }
+        VRT_HIP(ctx, hipGetLastError());
+      }
+      if (!single) {
+        VRT_HIP(ctx, hipEventRecord(s.ev_join, s.part[1]));
+        VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
+      }
+    }
+    VRT_HIP(ctx, hipEventRecord(s.ev_stop, s.part[0]));
+  }
+  ctx->gather_pending = false;
+  return VRT_OK;
+}
+
+// Wait for every device, then fill stats (kernel_ms = the slowest device; counters summed).
+int finish_frame(vrt_ctx* ctx, vrt_stats* stats, bool counting) {
+  float ms_max = 0.0f;
+  unsigned long long tot[VRT_CNT_COUNT] = {0};
+  for (Shard& s : ctx->sh) {
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    VRT_HIP(ctx, hipStreamSynchronize(s.part[0]));
+    if (stats) {
+      float ms = 0.0f;
+      VRT_HIP(ctx, hipEventElapsedTime(&ms, s.ev_start, s.ev_stop));
+      ms_max = std::max(ms_max, ms);
+    }
+    if (counting) {
+      unsigned long long c[VRT_CNT_COUNT];
+      VRT_HIP(ctx, hipMemcpy(c, s.d_cnt, sizeof(c), hipMemcpyDeviceToHost));
+      for (int q = 0; q < VRT_CNT_COUNT; ++q) tot[q] += c[q];
+    }
+  }
+  if (stats) {
+    stats->kernel_ms = ms_max;
+    if (counting)
+      for (int q = 0; q < VRT_CNT_COUNT; ++q) stats->counters[q] = tot[q];
+  }
+  return VRT_OK;
+}
+
+// Band j's rows (band row r = frame row j + r*k) to the host frame: one strided copy per device
+// on its own PCIe link.
+int copy_bands_to_host(vrt_ctx* ctx, int32_t w, int32_t h, const void* const* bands, size_t elem,
+                       void* host) {
+  const int32_t k = int32_t(ctx->sh.size());
+  for (int32_t j = 0; j < k; ++j) {
+    Shard& s = ctx->sh[j];
+    const int32_t hb = band_rows(h, k, j);
+    if (hb == 0) continue;
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    const size_t row = size_t(w) * elem;
+    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(host) + size_t(j) * row, size_t(k) * row, bands[j], row,
+                                  row, size_t(hb), hipMemcpyDeviceToHost, s.part[0]));
+  }
+  return VRT_OK;
+}
+
+int create(const std::vector<int>& devs, vrt_ctx** out) {
+  if (!out) return VRT_ERR_INVALID;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return VRT_ERR_DEVICE;
+  if (devs.empty() || devs.size() > 64) return VRT_ERR_INVALID;
+  for (int d : devs)
+    if (d < 0 || d >= count) return VRT_ERR_INVALID;
+  DeviceGuard guard;
+  vrt_ctx* c = new vrt_ctx();
+  c->sh.resize(devs.size());
+  for (size_t j = 0; j < devs.size(); ++j) {
+    if (shard_init(c->sh[j], devs[j]) != hipSuccess) {
+      vrt_destroy(c);
+      return VRT_ERR_DEVICE;
+    }
+    for (size_t i = 0; i < j; ++i)
+      if (devs[i] == devs[j]) c->distinct = false;
+  }
+  if (hipSetDevice(devs[0]) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming) != hipSuccess) {
+    vrt_destroy(c);
+    return VRT_ERR_DEVICE;
+  }
+  if (devs.size() > 1 && c->distinct) {  // one communicator per device, this process owns them all
+    c->comms.resize(devs.size());
+    if (ncclCommInitAll(c->comms.data(), int(devs.size()), devs.data()) != ncclSuccess) {
+      c->comms.clear();
+      vrt_destroy(c);
+      return VRT_ERR_DEVICE;
+    }
+  }
+  *out = c;
+  return VRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vrt_create(uint32_t device_mask, vrt_ctx** out) {
+  std::vector<int> devs;
+  for (int d = 0; d < 32; ++d)
+    if (device_mask & (1u << d)) devs.push_back(d);
+  if (devs.empty()) {
+    if (out) *out = nullptr;
+    return VRT_ERR_INVALID;
+  }
+  return create(devs, out);
+}
+
+int vrt_create_devices(const int32_t* devices, int32_t count, vrt_ctx** out) {
+  if (!devices || count < 1) {
+    if (out) *out = nullptr;
+    return VRT_ERR_INVALID;
+  }
+  return create(std::vector<int>(devices, devices + count), out);
+}
+
+void vrt_destroy(vrt_ctx* c) {
+  if (!c) return;
+  DeviceGuard guard;
+  for (ncclComm_t cm : c->comms) (void)ncclCommDestroy(cm);
+  if (!c->sh.empty()) {
+    (void)hipSetDevice(c->sh[0].device);
+    if (c->d_gather) (void)hipFree(c->d_gather);
+    if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
+  }
+  for (Shard& s : c->sh) shard_free(s);
+  delete c;
+}
+
+int vrt_device_count(const vrt_ctx* ctx) { return ctx ? int(ctx->sh.size()) : VRT_ERR_INVALID; }
+
+int vrt_device_ordinal(const vrt_ctx* ctx, int32_t i) {
+  if (!ctx || i < 0 || size_t(i) >= ctx->sh.size()) return -1;
+  return ctx->sh[size_t(i)].device;
+}
+
+const char* vrt_last_error(const vrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out) {
+  if (height < 1 || k < 1 || parts < 1 || !out) return VRT_ERR_INVALID;
+  for (int32_t j = 0; j < k; ++j)
+    for (int32_t p = 0; p < parts; ++p) {
+      const PartRows pr = part_rows(height, k, parts, j, p);
+      int32_t* o = out + (size_t(j) * parts + p) * 4;
+      o[0] = pr.row0;
+      o[1] = pr.rows;
+      o[2] = pr.row_step;
+      o[3] = pr.band_row0;
+    }
+  return band_cap(height, k);
+}
+
+int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!vol || !vol->voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
+  DeviceGuard guard;
+  int st = volume_alloc_all(ctx, vol->n);
+  if (st != VRT_OK) return st;
+  Shard& root = ctx->sh[0];
+  const size_t bytes = size_t(vol->n) * vol->n * vol->n;
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  VRT_HIP(ctx, hipMemcpyAsync(root.d_vox, vol->voxels, bytes, hipMemcpyHostToDevice, root.part[0]));
+  if ((st = broadcast_volume(ctx)) != VRT_OK) return st;
+  return volume_finish_all(ctx);
+}
+
+int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!d_voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
+  DeviceGuard guard;
+  int st = volume_alloc_all(ctx, n);
+  if (st != VRT_OK) return st;
+  Shard& root = ctx->sh[0];
+  const size_t bytes = size_t(n) * n * n;
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  // ordered after the caller's work on hip_stream (which produced d_voxels)
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  VRT_HIP(ctx, hipMemcpyAsync(root.d_vox, d_voxels, bytes, hipMemcpyDeviceToDevice, s));
+  VRT_HIP(ctx, hipEventRecord(root.ev_join, s));
+  VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], root.ev_join, 0));
+  if ((st = broadcast_volume(ctx)) != VRT_OK) return st;
+  return volume_finish_all(ctx);
+}
+
+int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (scene != VRT_SCENE_TERRAIN && scene != VRT_SCENE_GLASS_CUBE && scene != VRT_SCENE_REFRACTION)
+    return fail(ctx, VRT_ERR_INVALID, "unknown scene");
+  if (n < 8) return fail(ctx, VRT_ERR_INVALID, "scene edge must be >= 8");
+  DeviceGuard guard;
+  const int st = volume_alloc_all(ctx, n);
+  if (st != VRT_OK) return st;
+  std::vector<float> noise;
+  if (scene == VRT_SCENE_TERRAIN) {  // the heightfield (n*n floats) is built on the host
+    noise.resize(size_t(n) * n);
+    if (vrt_terrain_noise(n, seed, noise.data()) != VRT_OK) return fail(ctx, VRT_ERR_INVALID, "noise");
+  }
+  hipStream_t cs = static_cast<hipStream_t>(hip_stream);
+  for (Shard& s : ctx->sh) {  // every device builds its own replica: no transfer
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    const float* d_noise = nullptr;
+    if (!noise.empty()) {
+      // d_tmp (>= 2 N^3 bytes >= 4 N^2) is free until the distance passes
+      VRT_HIP(ctx, hipMemcpyAsync(s.d_tmp, noise.data(), noise.size() * sizeof(float),
+                                  hipMemcpyHostToDevice, s.part[0]));
+      d_noise = reinterpret_cast<const float*>(s.d_tmp);
+    }
+    if (&s == &ctx->sh[0] && cs) {  // ordered after the caller's prior work on its stream
+      VRT_HIP(ctx, hipEventRecord(s.ev_join, cs));
+      VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
+    }
+    vrt::launch_build_scene(s.d_vox, scene, uint32_t(n), d_noise, s.part[0]);
+    VRT_HIP(ctx, hipGetLastError());
+  }
+  return volume_finish_all(ctx);
+}
+
+const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->sh[0].d_vox : nullptr; }
+
+int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count) {
+  if (!ctx) return VRT_ERR_INVALID;
+  Shard& s = ctx->sh[0];
+  if (!s.d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
+  const uint64_t p = uint64_t(s.n) + 1, total = p * p * p * uint64_t(s.octants);
+  if (!out || count < total) return fail(ctx, VRT_ERR_INVALID, "output smaller than octants x (N+1)^3");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(s.device));
+  VRT_HIP(ctx, hipMemcpy(out, s.d_vox_pad, total * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  return VRT_OK;
+}
+
+int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (octants != 0 && octants != 1 && octants != 8)
+    return fail(ctx, VRT_ERR_INVALID, "skip layout must be 0 (auto), 1 or 8");
+  ctx->layout_req = octants;
+  return VRT_OK;
+}
+
+int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
+  ctx->tile_order = on != 0;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (mode < -1 || mode > 1) return fail(ctx, VRT_ERR_INVALID, "certified mode must be -1, 0 or 1");
+  ctx->cert_req = mode;
+  return VRT_OK;
+}
+
+int vrt_certified(const vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  const Shard& s = ctx->sh[0];
+  return s.octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || s.cert_auto) ? 1 : 0;
+}
+
+int vrt_volume_octants(const vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  return ctx->sh[0].d_vox_pad ? ctx->sh[0].octants : 0;
+}
+
+int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n, float randomness,
+                        float seed, float* out) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!dir || !pos || !out || n < 0) return fail(ctx, VRT_ERR_INVALID, "null buffer or n < 0");
+  if (n == 0) return VRT_OK;
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  const size_t bytes = size_t(n) * 3 * sizeof(float);
+  float *d_dir = nullptr, *d_pos = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_dir, bytes) != hipSuccess || hipMalloc(&d_pos, bytes) != hipSuccess ||
+      hipMalloc(&d_out, bytes) != hipSuccess) {
+    (void)hipFree(d_dir);
+    (void)hipFree(d_pos);
+    return fail(ctx, VRT_ERR_OOM, "hipMalloc");
+  }
+  hipError_t e = hipMemcpy(d_dir, dir, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_pos, pos, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    vrt::launch_randomize(d_dir, d_pos, n, randomness, seed, d_out, nullptr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(d_dir);
+  (void)hipFree(d_pos);
+  (void)hipFree(d_out);
+  if (e != hipSuccess) return hip_fail(ctx, e, "vrt_debug_randomize");
+  return VRT_OK;
+}
+
+// Band arguments shared by the async entry points: rows inside the image, pitch >= width.
+static int check_band(vrt_ctx* ctx, const vrt_camera* cam, int32_t row0, int32_t rows, int32_t row_step,
+                      int64_t pitch) {
+  if (rows < 0 || row_step < 1 || row0 < 0 ||
+      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
+    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
+  if (pitch < cam->width || pitch > INT32_MAX) return fail(ctx, VRT_ERR_INVALID, "row pitch must be >= the image width");
+  return VRT_OK;
+}
+
+int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                                  int32_t rows, int32_t row_step, int64_t pitch, float* d_out_rgba,
+                                  vrt_hit* d_out_hit, uint64_t* d_counters, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
+  if (rows == 0) return VRT_OK;
+  Shard& s = ctx->sh[0];
+  vrt::KArgs a = make_args(ctx, s, cam, p, row0, rows, row_step);
+  a.pitch = int32_t(pitch);
+  launch(ctx, s, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
+         reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0, int32_t rows,
+                          int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
+                          void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
+  return vrt_render_rows_pitched_async(ctx, cam, p, row0, rows, row_step, cam->width, d_out_rgba, d_out_hit,
+                                       d_counters, hip_stream);
+}
+
+int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
+                                           float alpha, int32_t row0, int32_t rows, int32_t row_step,
+                                           int64_t pitch, const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                           void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
+  if (rows == 0) return VRT_OK;
+  Shard& s = ctx->sh[0];
+  vrt::KArgs a = make_args(ctx, s, cam, p, row0, rows, row_step);
+  a.pitch = int32_t(pitch);
+  a.alpha = alpha;
+  a.prev = d_prev_rgba8;
+  a.cur = d_cur_rgba8;
+  a.raw = d_raw_rgba8;
+  launch(ctx, s, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
+         static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,
+                                   int32_t row0, int32_t rows, int32_t row_step, const uint32_t* d_prev_rgba8,
+                                   uint32_t* d_cur_rgba8, uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
+                                   uint64_t* d_counters, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
+  return vrt_render_temporal_rows_pitched_async(ctx, cam, p, alpha, row0, rows, row_step, cam->width,
+                                                d_prev_rgba8, d_cur_rgba8, d_raw_rgba8, d_out_hit, d_counters,
+                                                hip_stream);
+}
+
+int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, uint8_t* out_rgba8,
+                     vrt_stats* stats) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
+  DeviceGuard guard;
+  if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
+  const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
+  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
+  std::vector<const void*> bands;
+  for (Shard& s : ctx->sh) bands.push_back(s.d_hist);
+  if ((st = copy_bands_to_host(ctx, cam->width, cam->height, bands.data(), 4, out_rgba8)) != VRT_OK) return st;
+  if ((st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,
+                            uint32_t* d_out_rgba8, void* hip_stream, vrt_stats* stats) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!d_out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
+  DeviceGuard guard;
+  if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
+  const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
+  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
+  const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
+  Shard& root = ctx->sh[0];
+  hipStream_t cs = static_cast<hipStream_t>(hip_stream);
+  const size_t row = size_t(w) * 4;
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  // the copies into d_out follow the caller's prior work on its stream
+  VRT_HIP(ctx, hipEventRecord(root.ev_join, cs));
+  VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], root.ev_join, 0));
+  if (k == 1) {
+    VRT_HIP(ctx, hipMemcpyAsync(d_out_rgba8, root.d_hist, size_t(h) * row, hipMemcpyDeviceToDevice, root.part[0]));
+  } else {
+    const int32_t cap = band_cap(h, k);
+    const uint32_t* src[64];
+    if (ctx->distinct) {  // RCCL gather of the equal-size bands to the first device over xGMI
+      const size_t need = size_t(k) * size_t(cap) * size_t(w);
+      if (need > ctx->gather_pixels) {
+        VRT_HIP(ctx, hipDeviceSynchronize());
+        if (ctx->d_gather) (void)hipFree(ctx->d_gather);
+        ctx->d_gather = nullptr;
+        ctx->gather_pixels = 0;
+        if (hipMalloc(&ctx->d_gather, need * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc gather");
+        ctx->gather_pixels = need;
+      }
+      VRT_NCCL(ctx, ncclGroupStart());
+      for (int32_t j = 0; j < k; ++j) {
+        Shard& s = ctx->sh[j];
+        (void)hipSetDevice(s.device);
+        const ncclResult_t r = ncclGather(s.d_hist, j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
+                                          ncclUint8, 0, ctx->comms[j], s.part[0]);
+        if (r != ncclSuccess) {
+          (void)ncclGroupEnd();
+          return nccl_fail(ctx, r, "ncclGather(bands)");
+        }
+      }
+      VRT_NCCL(ctx, ncclGroupEnd());
+      for (int32_t j = 0; j < k; ++j) src[j] = ctx->d_gather + size_t(j) * cap * w;
+    } else {  // a device repeats: copy the bands device to device
+      for (int32_t j = 1; j < k; ++j) VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], ctx->sh[j].ev_stop, 0));
+      for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_hist;
+    }
+    VRT_HIP(ctx, hipSetDevice(root.device));
+    for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
+      const int32_t hb = band_rows(h, k, j);
+      if (hb > 0)
+        VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(d_out_rgba8) + size_t(j) * row, size_t(k) * row,
+                                      src[j], row, row, size_t(hb), hipMemcpyDeviceToDevice, root.part[0]));
+    }
+  }
+  VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.part[0]));
+  VRT_HIP(ctx, hipStreamWaitEvent(cs, ctx->ev_gathered, 0));
+  ctx->gather_pending = true;
+  if (stats && (st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size) {
+  if (!ctx) return VRT_ERR_INVALID;
+  DeviceGuard guard;
+  const int st = upload_atlas(ctx, rgba, atlas_size);
+  if (st == VRT_OK) ctx->err.clear();
+  return st;
+}
+
+int vrt_history_reset(vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer)
+  for (Shard& s : ctx->sh) std::swap(s.d_hist, s.d_raw);
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* out_rgba, vrt_hit* out_hit,
+               vrt_stats* stats) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int st = check_render_args(ctx, cam, p);
+  if (st != VRT_OK) return st;
+  if (!out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
+  DeviceGuard guard;
+  const int32_t k = int32_t(ctx->sh.size());
+  const size_t pixels = size_t(band_cap(cam->height, k)) * size_t(cam->width);
+  for (Shard& s : ctx->sh) {
+    if (pixels <= s.out_pixels) continue;
+    VRT_HIP(ctx, hipSetDevice(s.device));
+    VRT_HIP(ctx, hipDeviceSynchronize());
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.d_hit) (void)hipFree(s.d_hit);
+    s.d_out = nullptr;
+    s.d_hit = nullptr;
+    s.out_pixels = 0;
+    if (hipMalloc(&s.d_out, pixels * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&s.d_hit, pixels * sizeof(vrt_hit)) != hipSuccess)
+      return fail(ctx, VRT_ERR_OOM, "hipMalloc frame buffers");
+    s.out_pixels = pixels;
+  }
+  const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
+  if ((st = launch_frame(ctx, cam, p, 1.0f, false, out_hit != nullptr, counting)) != VRT_OK) return st;
+  std::vector<const void*> bands, hbands;
+  for (Shard& s : ctx->sh) {
+    bands.push_back(s.d_out);
+    hbands.push_back(s.d_hit);
+  }
+  if ((st = copy_bands_to_host(ctx, cam->width, cam->height, bands.data(), sizeof(float4), out_rgba)) != VRT_OK)
+    return st;
+  if (out_hit &&
+      (st = copy_bands_to_host(ctx, cam->width, cam->height, hbands.data(), sizeof(vrt_hit), out_hit)) != VRT_OK)
+    return st;
+  if ((st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+}  // extern "C"

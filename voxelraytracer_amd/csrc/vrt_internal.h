@@ -1,0 +1,74 @@
+// vrt_internal.h — the interface between the kernels (vrt_render.hip) and the C-ABI context
+// (vrt_context.cpp). Not installed; include/vrt.h is the public boundary.
+#ifndef VRT_INTERNAL_H
+#define VRT_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "vrt.h"
+
+namespace vrt {
+
+// Per-launch kernel arguments (by value: one kernarg segment per launch).
+struct KArgs {
+  float inv_pv[16];
+  float sun[3];
+  float sky_sy;      // max(u_SunDir.y, 0): the skybox's sun height factor (voxel.glsl:391), uniform
+  float sun_n[3];    // normalize(u_SunDir), GLSL normalize semantics (host: same IEEE ops)
+  float sun_rcp[3];  // RN(1 / sun_n): the shadow walk's per-axis reciprocals (uniform)
+  float time, ray_noise, refl_noise, refr_noise, max_len;
+  float fn;
+  int32_t n, width, height;
+  int32_t row0, rows, row_step;
+  int32_t pitch;  // pixels from one band row to the next in every output/history buffer (>= width)
+  uint32_t ostride;  // bytes from one direction octant's packed volume to the next (0: one volume)
+  int32_t max_refl, max_transp;
+  // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom
+  int32_t textured, atlas_size, atlas_tex_size;
+  const uint32_t* atlas;
+  // temporal epilogue (cur != nullptr): RGB8 store + temporal.glsl blend instead of float RGBA
+  float alpha;
+  const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
+  uint32_t* cur;         // filtered frame written here
+  uint32_t* raw;         // optional: the quantised ray-trace frame (the reference's rayTrace FBO)
+  // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
+  // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
+  int32_t cert;
+  // tile dispatch order (stats-free launches, vrt_set_tile_order): nullptr = dispatch order.
+  // tiles_x: tiles per row; tiles: tiles of the launch; ord_r / ord_w: the flag sets read and
+  // written by this launch (grid 2 x tiles: heavy tiles first)
+  uint32_t* order;
+  uint32_t tiles_x, tiles, ord_r, ord_w;
+};
+
+constexpr int kWgWaves = 4;                 // waves per workgroup, each an 8x8 pixel tile
+constexpr int kWgThreads = 64 * kWgWaves;
+constexpr int kTileW = 16;                  // a workgroup renders a 16x16 pixel tile
+constexpr int kTileH = 16;
+constexpr int kMaxStack = 17;               // bounce-stack entries: max_reflections + max_transparencies + 1
+constexpr int kCntReplicas = 256;           // counter replicas (per-wave atomics spread over them)
+constexpr uint32_t kOrdHdr = 0;             // tile-order buffer: per-tile wave counters, then two flag sets
+
+// ---- launches (vrt_render.hip); all asynchronous on `s` ------------------------------------
+
+// render_kernel: the instance is chosen from (stats, a.textured, a.cert); grid = a.tiles, or
+// 2 * a.tiles with a tile order (a.order). cnt_rep: the counter replicas (stats launches).
+void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,
+                   unsigned long long* cnt_rep, hipStream_t s);
+// fold the counter replicas into dst (accumulating) and re-zero them
+void launch_reduce_counters(unsigned long long* rep, unsigned long long* dst, hipStream_t s);
+// the kernel's packed volume from the canonical N^3 bytes: 8 octant forward-distance volumes
+// (octants == 8; tmp = 3 N^3 bytes) or one centred-distance volume (tmp = 2 N^3 bytes)
+void launch_volume_passes(const uint8_t* vox, uint8_t* tmp, uint16_t* packed, uint32_t n,
+                          int octants, hipStream_t s);
+// glass and non-empty voxel counts into out[0..1] (accumulating)
+void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* out, hipStream_t s);
+void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise, hipStream_t s);
+void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,
+                      float* out, hipStream_t s);
+
+}  // namespace vrt
+
+#endif  // VRT_INTERNAL_H

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "vrt.h"
+#include "vrt_internal.h"
 
 // Diagnostic instrumentation (per-wave timestamps, certified-walk outcome counts; images and
 // counters unchanged) exists only in `make variant` builds, never in the product library.
@@ -28,39 +29,6 @@
 #endif
 
 namespace vrt {
-
-// ------------------------------------------------------------------------ kernel arguments --
-
-struct KArgs {
-  float inv_pv[16];
-  float sun[3];
-  float sky_sy;      // max(u_SunDir.y, 0): the skybox's sun height factor (voxel.glsl:391), uniform
-  float sun_n[3];    // normalize(u_SunDir), GLSL normalize semantics (host: same IEEE ops)
-  float sun_rcp[3];  // RN(1 / sun_n): the shadow walk's per-axis reciprocals (uniform)
-  float time, ray_noise, refl_noise, refr_noise, max_len;
-  float fn;
-  int32_t n, width, height;
-  int32_t row0, rows, row_step;
-  int32_t pitch;  // pixels from one band row to the next in every output/history buffer (>= width)
-  uint32_t ostride;  // bytes from one direction octant's packed volume to the next (0: one volume)
-  int32_t max_refl, max_transp;
-  // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom
-  int32_t textured, atlas_size, atlas_tex_size;
-  const uint32_t* atlas;
-  // temporal epilogue (cur != nullptr): RGB8 store + temporal.glsl blend instead of float RGBA
-  float alpha;
-  const uint32_t* prev;  // last filtered frame (RGBA8 words), band-local like the output
-  uint32_t* cur;         // filtered frame written here
-  uint32_t* raw;         // optional: the quantised ray-trace frame (the reference's rayTrace FBO)
-  // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
-  // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
-  int32_t cert;
-  // tile dispatch order (stats-free launches, vrt_set_tile_order; tile_order_begin): nullptr =
-  // dispatch order. tiles_x: tiles per row; tiles: tiles of the launch; ord_r / ord_w: the flag
-  // sets read and written by this launch (grid 2 x tiles: heavy tiles first)
-  uint32_t* order;
-  uint32_t tiles_x, tiles, ord_r, ord_w;
-};
 
 // ------------------------------------------------------------------ GLSL vector semantics --
 
@@ -952,7 +920,6 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 // whose primary hit is glass (its secondary rays start at the exact hit point) take the exact
 // path. Only the stats-free colour-only instance uses it: hit records and counters need the
 // exact walk, and textured shading reads the hit point.
-constexpr int kMaxStack = 17;
 
 // Bounce stacks run at raised wave priority (s_setprio): they are a frame's longest waves
 // (-2 % at C3, profiles/r01_v45_ab_wave_priority.log).
@@ -1574,13 +1541,9 @@ __device__ __forceinline__ uint32_t lane_id() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
-// Four waves per workgroup, each rendering an 8x8 pixel tile: a workgroup covers 16x16 pixels
-// (wave = threadIdx.x >> 6, uniform). Tiles are dispatched in row order (an XCD-aware order that
+// Four waves per workgroup (kWgWaves), each rendering an 8x8 pixel tile: a workgroup covers
+// 16x16 pixels (wave = threadIdx.x >> 6, uniform). Tiles are dispatched in row order (an XCD-aware order that
 // keeps runs of tiles on one XCD's L2 was neutral or worse, profiles/r01_v29_ab_xcd_tile_swizzle_negative.log).
-constexpr int kWgWaves = 4;
-constexpr int kWgThreads = 64 * kWgWaves;
-constexpr int kTileW = 16;
-constexpr int kTileH = 16;
 
 // Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, the glass pixels'
 // bounce stacks; dispatched in row order, those start wherever the glass is in the image. Each
@@ -1591,7 +1554,6 @@ constexpr int kTileH = 16;
 // slot L < tiles renders tile L iff its flag is set, slot tiles + L renders it iff it is clear.
 // Both test the same immutable word, so every tile is rendered exactly once whatever the buffer
 // holds (a fresh zeroed buffer: no heavy tiles).
-constexpr uint32_t kOrdHdr = 0;  // the per-tile wave counters, then the two flag sets
 // The tile workgroup L renders, or ~0u (nothing to do); a tile's flag word of the last launch is 1
 // when it ran a bounce stack (heavy)
 __device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L) {
@@ -1639,9 +1601,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 #endif
 
-// Counter replicas: one 64-bit add per wave and counter into replica (block % kCntReplicas);
-// a single array would serialise ~300K same-address atomics per 1080p frame at the memory side.
-constexpr int kCntReplicas = 256;
+// Counters (STATS launches): one 64-bit add per wave and counter into replica
+// (block % kCntReplicas); a single array would serialise ~300K same-address atomics per 1080p
+// frame at the memory side.
 
 // Waves per SIMD the register budget is sized for: 7 -> 72 VGPRs. With certified walks inside the
 // bounce stacks, 64 VGPRs (8 waves) spill in the glass waves that bound a frame: 7 is 2-4 % faster
@@ -2079,467 +2041,89 @@ __global__ void __launch_bounds__(256) fwd_pack_kernel(const uint8_t* __restrict
 
 }  // namespace vrt
 
-// ---------------------------------------------------------------------------- C-ABI context --
+// ------------------------------------------------------------------------------- launches --
+// Host wrappers of the kernels above (vrt_internal.h); the C-ABI context is vrt_context.cpp.
 
-struct vrt_ctx {
-  int device = 0;
-  uint8_t* d_vox = nullptr;       // canonical N^3
-  uint8_t* d_tmp = nullptr;       // 3 x N^3 distance-field scratch (2 x for the single layout)
-  uint16_t* d_vox_pad = nullptr;  // octants x padded (N+1)^3 voxel | G << 8, the kernel's format
-  int32_t n = 0;
-  int32_t octants = 0;            // 8 (octant forward distances, N <= 512) or 1 (centred, N = 1024)
-  int32_t layout_req = 0;         // vrt_set_skip_layout: 0 auto, 1 single centred volume, 8 octants
-  int32_t cert_req = 0;           // vrt_set_certified: 0 automatic, 1 always, -1 never
-  bool cert_auto = true;          // the automatic choice for the resident volume (volume_finish)
-  bool has_glass = true;          // the resident volume has glass (bounce stacks; tile order)
-  unsigned long long* d_vstats = nullptr;  // glass and non-empty voxel counts of the last upload
-  float4* d_out = nullptr;
-  vrt_hit* d_hit = nullptr;
-  unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of vrt_render
-  unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
-  size_t out_pixels = 0;
-  // vrt_render_frame's ping-pong history (main.cpp:140-142, 363-393): RGBA8 words
-  uint32_t* d_hist[2] = {nullptr, nullptr};
-  uint32_t* d_raw = nullptr;
-  int hist_last = 0;  // index of lastFrameBuffer in d_hist
-  int32_t hist_w = 0, hist_h = 0;
-  // textured mode: the atlas (RGBA8 words), and which host buffer it came from
-  uint32_t* d_atlas = nullptr;
-  int32_t atlas_size = 0;
-  const uint8_t* atlas_src = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // heavy-first tile order (vrt_set_tile_order): one order buffer per band geometry and stream
-  struct OrderSlot {
-    int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
-    hipStream_t stream = nullptr;
-    uint32_t* d = nullptr;
-    uint64_t epoch = 0, tick = 0;
-  };
-  static constexpr int kOrderSlots = 8;
-  OrderSlot order[kOrderSlots];
-  uint64_t order_tick = 0;
-  bool tile_order = true;
-  std::string err;
-};
+namespace vrt {
 
-namespace {
-
-int fail(vrt_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-int hip_fail(vrt_ctx* c, hipError_t e, const char* what) {
-  return fail(c, VRT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-#define VRT_HIP(ctx, call)                                   \
-  do {                                                       \
-    hipError_t e_ = (call);                                  \
-    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
-  } while (0)
-
-int upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t size) {
-  if (!rgba || size < 1 || size > 8192 || (size & (size - 1)) != 0)
-    return fail(ctx, VRT_ERR_INVALID, "atlas edge must be a power of two in [1, 8192]");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t bytes = size_t(size) * size * 4;
-  if (ctx->atlas_size != size) {
-    if (ctx->d_atlas) (void)hipFree(ctx->d_atlas);
-    ctx->d_atlas = nullptr;
-    ctx->atlas_size = 0;
-    if (hipMalloc(&ctx->d_atlas, bytes) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc atlas");
-  }
-  VRT_HIP(ctx, hipMemcpy(ctx->d_atlas, rgba, bytes, hipMemcpyHostToDevice));
-  ctx->atlas_size = size;
-  ctx->atlas_src = rgba;
-  return VRT_OK;
-}
-
-int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) {
-  if (!cam || !p) return fail(ctx, VRT_ERR_INVALID, "null camera or params");
-  if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
-  if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
-    return fail(ctx, VRT_ERR_INVALID, "bad image size");
-  if (!p->color_only) {  // textured mode: the context's atlas (uploaded here when it changes)
-    if (p->atlas_rgba && (p->atlas_rgba != ctx->atlas_src || p->atlas_size != ctx->atlas_size)) {
-      const int st = upload_atlas(ctx, p->atlas_rgba, p->atlas_size);
-      if (st != VRT_OK) return st;
-    }
-    if (!ctx->d_atlas || p->atlas_size != ctx->atlas_size)
-      return fail(ctx, VRT_ERR_INVALID, "textured mode needs an atlas of atlas_size (vrt_upload_atlas)");
-    if (p->atlas_texture_size <= 0) return fail(ctx, VRT_ERR_INVALID, "atlas_texture_size must be > 0");
-  }
-  if (p->max_reflections < 0 || p->max_transparencies < 0 ||
-      p->max_reflections + p->max_transparencies + 1 > vrt::kMaxStack)
-    return fail(ctx, VRT_ERR_UNSUPPORTED, "max_reflections + max_transparencies must be <= 16");
-  return VRT_OK;
-}
-
-vrt::KArgs make_args(const vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
-                     int32_t rows, int32_t row_step) {
-  vrt::KArgs a;
-  std::memcpy(a.inv_pv, cam->inv_pv, sizeof(a.inv_pv));
-  std::memcpy(a.sun, p->sun_dir, sizeof(a.sun));
-  a.sky_sy = std::fmax(p->sun_dir[1], 0.0f);  // GLSL max(x, 0) with fmaxf's NaN rule, as gmax
-  // normalize(u_SunDir) exactly as the kernel's normalize3 (IEEE single ops, no contraction)
-  const float sx = p->sun_dir[0], sy = p->sun_dir[1], sz = p->sun_dir[2];
-  const float inv = 1.0f / std::sqrt(sx * sx + sy * sy + sz * sz);
-  a.sun_n[0] = sx * inv;
-  a.sun_n[1] = sy * inv;
-  a.sun_n[2] = sz * inv;
-  for (int i = 0; i < 3; ++i) a.sun_rcp[i] = 1.0f / a.sun_n[i];
-  a.time = p->time;
-  a.ray_noise = p->ray_noise;
-  a.refl_noise = p->reflection_noise;
-  a.refr_noise = p->refraction_noise;
-  a.max_len = p->max_ray_length;
-  a.n = ctx->n;
-  a.fn = float(ctx->n);
-  a.width = cam->width;
-  a.height = cam->height;
-  a.row0 = row0;
-  a.rows = rows;
-  a.row_step = row_step;
-  a.pitch = cam->width;
-  a.ostride = ctx->octants == 8
-                  ? uint32_t(uint64_t(ctx->n + 1) * (ctx->n + 1) * (ctx->n + 1) * sizeof(uint16_t))
-                  : 0u;
-  a.max_refl = p->max_reflections;
-  a.max_transp = p->max_transparencies;
-  a.textured = p->color_only ? 0 : 1;
-  a.atlas_size = p->color_only ? 1 : p->atlas_size;
-  a.atlas_tex_size = p->atlas_texture_size;
-  a.atlas = ctx->d_atlas;
-  a.alpha = 1.0f;
-  a.prev = nullptr;
-  a.cur = nullptr;
-  a.raw = nullptr;
-  a.cert = ctx->octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || ctx->cert_auto ? 2 : 1);
-  a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
-  a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
-  a.order = nullptr;
-  a.ord_r = a.ord_w = 0;
-  return a;
-}
-
-void free_history(vrt_ctx* ctx) {
-  for (uint32_t** b : {&ctx->d_hist[0], &ctx->d_hist[1], &ctx->d_raw}) {
-    if (*b) (void)hipFree(*b);
-    *b = nullptr;
-  }
-  ctx->hist_w = ctx->hist_h = 0;
-}
-
-// The order buffer of this launch's band and stream (heavy-first tile order, render_kernel):
-// found, or allocated zeroed (no heavy tiles yet) on the launch stream. Not while the stream is
-// being captured into a graph (a replayed node would reuse one buffer set): dispatch order then.
-// Recycling one of the kOrderSlots buffers (more bands x streams than that) synchronises the device.
-void tile_order_begin(vrt_ctx* ctx, vrt::KArgs& a, hipStream_t s) {
-  // only where it pays: glass in the volume (no bounce stacks otherwise: the first pass would be
-  // tiles empty workgroups, C2/C4 +4 %) and certified pixels (glass-heavy volumes, where most
-  // tiles are heavy, keep dispatch order: C1 +8 %)
-  if (!ctx->tile_order || a.tiles == 0 || a.textured || a.cert != 2 || !ctx->has_glass) return;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
-  vrt_ctx::OrderSlot* slot = nullptr;
-  for (auto& o : ctx->order)
-    if (o.d && o.width == a.width && o.rows == a.rows && o.row0 == a.row0 && o.row_step == a.row_step &&
-        o.stream == s)
-      slot = &o;
-  if (!slot) {
-    slot = &ctx->order[0];
-    for (auto& o : ctx->order)
-      if (!o.d || o.tick < slot->tick) slot = &o;
-    if (slot->d) {
-      if (hipDeviceSynchronize() != hipSuccess) return;
-      (void)hipFree(slot->d);
-      slot->d = nullptr;
-    }
-    const size_t words = vrt::kOrdHdr + 3u * size_t(a.tiles);
-    if (hipMalloc(&slot->d, words * sizeof(uint32_t)) != hipSuccess) {
-      slot->d = nullptr;
-      return;
-    }
-    if (hipMemsetAsync(slot->d, 0, words * sizeof(uint32_t), s) != hipSuccess) {
-      (void)hipFree(slot->d);
-      slot->d = nullptr;
-      return;
-    }
-    slot->width = a.width;
-    slot->rows = a.rows;
-    slot->row0 = a.row0;
-    slot->row_step = a.row_step;
-    slot->stream = s;
-    slot->epoch = 0;
-  }
-  slot->tick = ++ctx->order_tick;
-  a.order = slot->d;
-  a.ord_r = uint32_t(slot->epoch & 1u);
-  a.ord_w = uint32_t((slot->epoch + 1u) & 1u);
-  slot->epoch++;
-}
-
-void free_tile_order(vrt_ctx* ctx) {
-  for (auto& o : ctx->order) {
-    if (o.d) (void)hipFree(o.d);
-    o = vrt_ctx::OrderSlot();
-  }
-}
-
-// Render kernel (1-D grid of tiles; with a tile order, two passes: heavy tiles, then the rest),
-// then (when counting)
-// fold the replicas into `cnt` (accumulate) and re-zero them.
-void launch(vrt_ctx* ctx, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
-            hipStream_t s) {
-  const bool stats = hit || cnt;
-  if (!stats) tile_order_begin(ctx, a, s);
+void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,
+                   unsigned long long* cnt_rep, hipStream_t s) {
   const dim3 grid(a.order ? 2u * a.tiles : a.tiles);
   // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
   // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
   // ~5 %), exact walks only (0)
-  hipLaunchKernelGGL(a.textured ? (stats ? vrt::render_kernel<true, true> : vrt::render_kernel<false, true>)
-                                : (stats ? vrt::render_kernel<true, false>
-                                         : (a.cert == 2 ? vrt::render_kernel<false, false, 2>
-                                            : a.cert == 1 ? vrt::render_kernel<false, false, 1>
-                                                          : vrt::render_kernel<false, false, 0>)),
-                     grid,
-                     dim3(vrt::kWgThreads), 0, s, a, ctx->d_vox_pad, out, hit,
-                     cnt ? ctx->d_cnt_rep : nullptr);
-  if (cnt) hipLaunchKernelGGL(vrt::reduce_counters_kernel, dim3(1), dim3(64), 0, s, ctx->d_cnt_rep, cnt);
+  hipLaunchKernelGGL(a.textured ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
+                                : (stats ? render_kernel<true, false>
+                                         : (a.cert == 2 ? render_kernel<false, false, 2>
+                                            : a.cert == 1 ? render_kernel<false, false, 1>
+                                                          : render_kernel<false, false, 0>)),
+                     grid, dim3(kWgThreads), 0, s, a, vox, out, hit, cnt_rep);
 }
 
-int volume_alloc(vrt_ctx* ctx, int32_t n) {
-  if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
-    return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  // octant layout while 8 padded u16 volumes stay addressable by a 32-bit byte offset
-  const bool fits = uint64_t(n + 1) * (n + 1) * (n + 1) * 2 * 8 <= (uint64_t(1) << 32);
-  const int32_t octants = fits && ctx->layout_req != 1 ? 8 : 1;
-  if (ctx->d_vox && (ctx->n != n || ctx->octants != octants)) {
-    (void)hipFree(ctx->d_vox);
-    (void)hipFree(ctx->d_tmp);
-    (void)hipFree(ctx->d_vox_pad);
-    ctx->d_vox = ctx->d_tmp = nullptr;
-    ctx->d_vox_pad = nullptr;
-  }
-  if (!ctx->d_vox) {
-    const size_t bytes = size_t(n) * n * n,
-                 pbytes = size_t(n + 1) * (n + 1) * (n + 1) * 2 * size_t(octants);
-    if (hipMalloc(&ctx->d_vox, bytes) != hipSuccess ||
-        hipMalloc(&ctx->d_tmp, (octants == 8 ? 3 : 2) * bytes) != hipSuccess ||
-        hipMalloc(&ctx->d_vox_pad, pbytes) != hipSuccess) {
-      if (ctx->d_vox) (void)hipFree(ctx->d_vox);
-      if (ctx->d_tmp) (void)hipFree(ctx->d_tmp);
-      if (ctx->d_vox_pad) (void)hipFree(ctx->d_vox_pad);
-      ctx->d_vox = ctx->d_tmp = nullptr;
-      ctx->d_vox_pad = nullptr;
-      return fail(ctx, VRT_ERR_OOM, "hipMalloc volume buffers");
-    }
-  }
-  ctx->n = n;
-  ctx->octants = octants;
-  return VRT_OK;
+void launch_reduce_counters(unsigned long long* rep, unsigned long long* dst, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_counters_kernel, dim3(1), dim3(64), 0, s, rep, dst);
 }
 
-// Distance field (3 passes) + padded packing on the GPU, then wait (upload is not a hot call).
-int volume_finish(vrt_ctx* ctx, hipStream_t s) {
-  const uint32_t n = uint32_t(ctx->n);
+void launch_volume_passes(const uint8_t* vox, uint8_t* tmp, uint16_t* packed, uint32_t n,
+                          int octants, hipStream_t s) {
   const uint64_t vol = uint64_t(n) * n * n, pvol = uint64_t(n + 1) * (n + 1) * (n + 1);
   const unsigned b1 = unsigned(std::min<uint64_t>((vol + 255) / 256, 16384));
   const unsigned b2 = unsigned(std::min<uint64_t>((pvol + 255) / 256, 16384));
-  uint8_t* da = ctx->d_tmp;
-  uint8_t* db = ctx->d_tmp + vol;
-  if (ctx->octants == 8) {
+  uint8_t* da = tmp;
+  uint8_t* db = tmp + vol;
+  if (octants == 8) {
     // octant forward distances: 2 x passes, 4 y passes, 8 z passes + packs (x -> y -> z nesting)
-    uint8_t* dc = ctx->d_tmp + 2 * vol;
+    uint8_t* dc = tmp + 2 * vol;
     for (int sx = 1; sx >= -1; sx -= 2) {
-      hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, sx, 1);
+      hipLaunchKernelGGL(fwd_pass_kernel, dim3(b1), dim3(256), 0, s, vox, da, n, 0, sx, 1);
       for (int sy = 1; sy >= -1; sy -= 2) {
-        hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, sy, 0);
+        hipLaunchKernelGGL(fwd_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, sy, 0);
         for (int sz = 1; sz >= -1; sz -= 2) {
-          hipLaunchKernelGGL(vrt::fwd_pass_kernel, dim3(b1), dim3(256), 0, s, db, dc, n, 2, sz, 0);
+          hipLaunchKernelGGL(fwd_pass_kernel, dim3(b1), dim3(256), 0, s, db, dc, n, 2, sz, 0);
           const int o = (sx < 0 ? 1 : 0) | (sy < 0 ? 2 : 0) | (sz < 0 ? 4 : 0);
-          hipLaunchKernelGGL(vrt::fwd_pack_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, dc,
-                             ctx->d_vox_pad + size_t(o) * pvol, n, sx, sy, sz);
+          hipLaunchKernelGGL(fwd_pack_kernel, dim3(b2), dim3(256), 0, s, vox, dc,
+                             packed + size_t(o) * pvol, n, sx, sy, sz);
         }
       }
     }
   } else {
-    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, da, n, 0, 1);
-    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, 0);
-    hipLaunchKernelGGL(vrt::dist_pass_kernel, dim3(b1), dim3(256), 0, s, db, da, n, 2, 0);
-    hipLaunchKernelGGL(vrt::pack_volume_kernel, dim3(b2), dim3(256), 0, s, ctx->d_vox, da,
-                       ctx->d_vox_pad, n);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(b1), dim3(256), 0, s, vox, da, n, 0, 1);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(b1), dim3(256), 0, s, da, db, n, 1, 0);
+    hipLaunchKernelGGL(dist_pass_kernel, dim3(b1), dim3(256), 0, s, db, da, n, 2, 0);
+    hipLaunchKernelGGL(pack_volume_kernel, dim3(b2), dim3(256), 0, s, vox, da, packed, n);
   }
-  // certified walks cannot settle glass pixels (their secondary rays start at the exact hit
-  // point) and a glass pixel pays the certified primary walk before the exact path: the automatic
-  // mode turns them off when glass makes up more than 1/8 of the non-empty voxels
-  if (!ctx->d_vstats) VRT_HIP(ctx, hipMalloc(&ctx->d_vstats, 2 * sizeof(unsigned long long)));
-  VRT_HIP(ctx, hipMemsetAsync(ctx->d_vstats, 0, 2 * sizeof(unsigned long long), s));
-  hipLaunchKernelGGL(vrt::glass_share_kernel, dim3(b1), dim3(256), 0, s, ctx->d_vox, vol, ctx->d_vstats);
-  VRT_HIP(ctx, hipGetLastError());
-  VRT_HIP(ctx, hipStreamSynchronize(s));
-  unsigned long long vs[2] = {0, 0};
-  VRT_HIP(ctx, hipMemcpy(vs, ctx->d_vstats, sizeof(vs), hipMemcpyDeviceToHost));
-  ctx->cert_auto = vs[0] * 8 <= vs[1];
-  ctx->has_glass = vs[0] > 0;
-  ctx->err.clear();
-  return VRT_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int vrt_create(int device, vrt_ctx** out) {
-  if (!out) return VRT_ERR_INVALID;
-  *out = nullptr;
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count <= 0) return VRT_ERR_DEVICE;
-  if (device < 0 || device >= count) return VRT_ERR_INVALID;
-  vrt_ctx* c = new vrt_ctx();
-  c->device = device;
-  const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
-  if (hipSetDevice(device) != hipSuccess || hipEventCreate(&c->ev0) != hipSuccess ||
-      hipEventCreate(&c->ev1) != hipSuccess ||
-      hipMalloc(&c->d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT) != hipSuccess ||
-      hipMalloc(&c->d_cnt_rep, rep_bytes) != hipSuccess ||
-      hipMemset(c->d_cnt_rep, 0, rep_bytes) != hipSuccess) {
-    vrt_destroy(c);
-    return VRT_ERR_DEVICE;
-  }
-  *out = c;
-  return VRT_OK;
+void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* out, hipStream_t s) {
+  const unsigned b = unsigned(std::min<uint64_t>((total + 255) / 256, 16384));
+  hipLaunchKernelGGL(glass_share_kernel, dim3(b), dim3(256), 0, s, vox, total, out);
 }
 
-void vrt_destroy(vrt_ctx* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->d_vox) (void)hipFree(c->d_vox);
-  if (c->d_vox_pad) (void)hipFree(c->d_vox_pad);
-  if (c->d_tmp) (void)hipFree(c->d_tmp);
-  if (c->d_out) (void)hipFree(c->d_out);
-  if (c->d_hit) (void)hipFree(c->d_hit);
-  if (c->d_cnt) (void)hipFree(c->d_cnt);
-  if (c->d_cnt_rep) (void)hipFree(c->d_cnt_rep);
-  if (c->d_atlas) (void)hipFree(c->d_atlas);
-  if (c->d_vstats) (void)hipFree(c->d_vstats);
-  free_history(c);
-  free_tile_order(c);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  delete c;
-}
-
-const char* vrt_last_error(const vrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
-
-int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!vol || !vol->voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
-  const int st = volume_alloc(ctx, vol->n);
-  if (st != VRT_OK) return st;
-  const size_t bytes = size_t(vol->n) * vol->n * vol->n;
-  VRT_HIP(ctx, hipMemcpy(ctx->d_vox, vol->voxels, bytes, hipMemcpyHostToDevice));
-  return volume_finish(ctx, nullptr);
-}
-
-int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!d_voxels) return fail(ctx, VRT_ERR_INVALID, "null volume");
-  const int st = volume_alloc(ctx, n);
-  if (st != VRT_OK) return st;
-  const size_t bytes = size_t(n) * n * n;
-  hipStream_t s = static_cast<hipStream_t>(hip_stream);
-  VRT_HIP(ctx, hipMemcpyAsync(ctx->d_vox, d_voxels, bytes, hipMemcpyDeviceToDevice, s));
-  return volume_finish(ctx, s);
-}
-
-int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed, void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (scene != VRT_SCENE_TERRAIN && scene != VRT_SCENE_GLASS_CUBE && scene != VRT_SCENE_REFRACTION)
-    return fail(ctx, VRT_ERR_INVALID, "unknown scene");
-  if (n < 8) return fail(ctx, VRT_ERR_INVALID, "scene edge must be >= 8");
-  const int st = volume_alloc(ctx, n);
-  if (st != VRT_OK) return st;
-  hipStream_t s = static_cast<hipStream_t>(hip_stream);
-  std::vector<float> noise;
-  const float* d_noise = nullptr;
-  if (scene == VRT_SCENE_TERRAIN) {  // the heightfield (n*n floats) is built on the host
-    noise.resize(size_t(n) * n);
-    if (vrt_terrain_noise(n, seed, noise.data()) != VRT_OK) return fail(ctx, VRT_ERR_INVALID, "noise");
-    // d_tmp (2*N^3 bytes >= 4*N^2) is free until volume_finish's distance passes
-    VRT_HIP(ctx, hipMemcpyAsync(ctx->d_tmp, noise.data(), noise.size() * sizeof(float),
-                                hipMemcpyHostToDevice, s));
-    d_noise = reinterpret_cast<const float*>(ctx->d_tmp);
-  }
+void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise, hipStream_t s) {
   const uint64_t vol = uint64_t(n) * n * n;
   const unsigned blocks = unsigned(std::min<uint64_t>((vol + 255) / 256, 16384));
-  hipLaunchKernelGGL(vrt::build_scene_kernel, dim3(blocks), dim3(256), 0, s, ctx->d_vox, scene,
-                     uint32_t(n), d_noise);
-  VRT_HIP(ctx, hipGetLastError());
-  return volume_finish(ctx, s);
+  hipLaunchKernelGGL(build_scene_kernel, dim3(blocks), dim3(256), 0, s, vox, scene, n, noise);
 }
 
-const uint8_t* vrt_volume_device_ptr(const vrt_ctx* ctx) { return ctx ? ctx->d_vox : nullptr; }
-
-int vrt_debug_packed_volume(vrt_ctx* ctx, uint16_t* out, uint64_t count) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!ctx->d_vox_pad) return fail(ctx, VRT_ERR_NO_VOLUME, "no volume uploaded");
-  const uint64_t p = uint64_t(ctx->n) + 1, total = p * p * p * uint64_t(ctx->octants);
-  if (!out || count < total)
-    return fail(ctx, VRT_ERR_INVALID, "output smaller than octants x (N+1)^3");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  VRT_HIP(ctx, hipMemcpy(out, ctx->d_vox_pad, total * sizeof(uint16_t), hipMemcpyDeviceToHost));
-  return VRT_OK;
-}
-
-int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (octants != 0 && octants != 1 && octants != 8)
-    return fail(ctx, VRT_ERR_INVALID, "skip layout must be 0 (auto), 1 or 8");
-  ctx->layout_req = octants;
-  return VRT_OK;
-}
-
-int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
-  ctx->tile_order = on != 0;
-  ctx->err.clear();
-  return VRT_OK;
-}
-
-int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (mode < -1 || mode > 1) return fail(ctx, VRT_ERR_INVALID, "certified mode must be -1, 0 or 1");
-  ctx->cert_req = mode;
-  return VRT_OK;
-}
-
-int vrt_certified(const vrt_ctx* ctx) {
-  if (!ctx) return VRT_ERR_INVALID;
-  return ctx->octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || ctx->cert_auto) ? 1 : 0;
-}
-
-int vrt_volume_octants(const vrt_ctx* ctx) {
-  if (!ctx) return VRT_ERR_INVALID;
-  return ctx->d_vox_pad ? ctx->octants : 0;
+void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,
+                      float* out, hipStream_t s) {
+  hipLaunchKernelGGL(randomize_kernel, dim3((n + 63) / 64), dim3(64), 0, s, dir, pos, n,
+                     randomness, seed, out);
 }
 
 #ifdef VRT_CERT_DIAG
 // diagnostic build only: read and reset the certified-walk outcome counts (16 x u64)
-int vrt_debug_cert_diag(uint64_t* out) {
-  if (!out) return VRT_ERR_INVALID;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_cert_diag), 16 * 8) != hipSuccess) return VRT_ERR_DEVICE;
+int debug_cert_diag(uint64_t* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cert_diag), 16 * 8) != hipSuccess) return VRT_ERR_DEVICE;
   static const uint64_t zero[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(vrt::g_cert_diag), zero, 16 * 8) == hipSuccess ? VRT_OK
-                                                                                    : VRT_ERR_DEVICE;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cert_diag), zero, 16 * 8) == hipSuccess ? VRT_OK : VRT_ERR_DEVICE;
 }
 #endif
 
+}  // namespace vrt
+
 #ifdef VRT_STAMPS
+extern "C" {
 // diagnostic build only: copy the per-wave stamps of the last render (count = 3 x waves)
 int vrt_debug_stamps(uint64_t* out, uint64_t count) {
   if (!out || count > 3ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
@@ -2556,213 +2140,10 @@ int vrt_debug_stamps3(uint64_t* out, uint64_t count) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps3), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
+#ifdef VRT_CERT_DIAG
+int vrt_debug_cert_diag(uint64_t* out) { return out ? vrt::debug_cert_diag(out) : VRT_ERR_INVALID; }
 #endif
-
-int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
-                        float randomness, float seed, float* out) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!dir || !pos || !out || n < 0) return fail(ctx, VRT_ERR_INVALID, "null buffer or n < 0");
-  if (n == 0) return VRT_OK;
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t bytes = size_t(n) * 3 * sizeof(float);
-  float *d_dir = nullptr, *d_pos = nullptr, *d_out = nullptr;
-  if (hipMalloc(&d_dir, bytes) != hipSuccess || hipMalloc(&d_pos, bytes) != hipSuccess ||
-      hipMalloc(&d_out, bytes) != hipSuccess) {
-    (void)hipFree(d_dir);
-    (void)hipFree(d_pos);
-    return fail(ctx, VRT_ERR_OOM, "hipMalloc");
-  }
-  hipError_t e = hipMemcpy(d_dir, dir, bytes, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_pos, pos, bytes, hipMemcpyHostToDevice);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(vrt::randomize_kernel, dim3((n + 63) / 64), dim3(64), 0, nullptr, d_dir,
-                       d_pos, n, randomness, seed, d_out);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost);
-  (void)hipFree(d_dir);
-  (void)hipFree(d_pos);
-  (void)hipFree(d_out);
-  if (e != hipSuccess) return hip_fail(ctx, e, "vrt_debug_randomize");
-  return VRT_OK;
-}
-
-// Band arguments shared by the async entry points: rows inside the image, pitch >= width.
-static int check_band(vrt_ctx* ctx, const vrt_camera* cam, int32_t row0, int32_t rows,
-                      int32_t row_step, int64_t pitch) {
-  if (rows < 0 || row_step < 1 || row0 < 0 ||
-      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
-    return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
-  if (pitch < cam->width || pitch > INT32_MAX)
-    return fail(ctx, VRT_ERR_INVALID, "row pitch must be >= the image width");
-  return VRT_OK;
-}
-
-int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
-                                  int32_t row0, int32_t rows, int32_t row_step, int64_t pitch,
-                                  float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters,
-                                  void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  int st = check_render_args(ctx, cam, p);
-  if (st != VRT_OK) return st;
-  if (!d_out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
-  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
-  if (rows == 0) return VRT_OK;
-  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
-  a.pitch = int32_t(pitch);
-  launch(ctx, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
-         reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
-  VRT_HIP(ctx, hipGetLastError());
-  return VRT_OK;
-}
-
-int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
-                          int32_t rows, int32_t row_step, float* d_out_rgba, vrt_hit* d_out_hit,
-                          uint64_t* d_counters, void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
-  return vrt_render_rows_pitched_async(ctx, cam, p, row0, rows, row_step, cam->width, d_out_rgba,
-                                       d_out_hit, d_counters, hip_stream);
-}
-
-int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
-                                           const vrt_params* p, float alpha, int32_t row0,
-                                           int32_t rows, int32_t row_step, int64_t pitch,
-                                           const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
-                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
-                                           uint64_t* d_counters, void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  int st = check_render_args(ctx, cam, p);
-  if (st != VRT_OK) return st;
-  if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
-  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
-  if (rows == 0) return VRT_OK;
-  vrt::KArgs a = make_args(ctx, cam, p, row0, rows, row_step);
-  a.pitch = int32_t(pitch);
-  a.alpha = alpha;
-  a.prev = d_prev_rgba8;
-  a.cur = d_cur_rgba8;
-  a.raw = d_raw_rgba8;
-  launch(ctx, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
-         static_cast<hipStream_t>(hip_stream));
-  VRT_HIP(ctx, hipGetLastError());
-  return VRT_OK;
-}
-
-int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
-                                   float alpha, int32_t row0, int32_t rows, int32_t row_step,
-                                   const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
-                                   uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
-                                   void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (!cam) return fail(ctx, VRT_ERR_INVALID, "null camera");
-  return vrt_render_temporal_rows_pitched_async(ctx, cam, p, alpha, row0, rows, row_step,
-                                                cam->width, d_prev_rgba8, d_cur_rgba8, d_raw_rgba8,
-                                                d_out_hit, d_counters, hip_stream);
-}
-
-int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,
-                     uint8_t* out_rgba8, vrt_stats* stats) {
-  if (!ctx) return VRT_ERR_INVALID;
-  int st = check_render_args(ctx, cam, p);
-  if (st != VRT_OK) return st;
-  if (!out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t pixels = size_t(cam->width) * cam->height;
-  if (cam->width != ctx->hist_w || cam->height != ctx->hist_h) {  // (re)create: black history
-    free_history(ctx);
-    for (uint32_t** b : {&ctx->d_hist[0], &ctx->d_hist[1], &ctx->d_raw}) {
-      if (hipMalloc(b, pixels * 4) != hipSuccess) {
-        free_history(ctx);
-        return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
-      }
-      VRT_HIP(ctx, hipMemset(*b, 0, pixels * 4));
-    }
-    ctx->hist_w = cam->width;
-    ctx->hist_h = cam->height;
-    ctx->hist_last = 0;
-  }
-  if (stats)
-    VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
-  uint32_t* last = ctx->d_hist[ctx->hist_last];
-  uint32_t* cur = ctx->d_hist[1 - ctx->hist_last];
-  vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
-  a.alpha = alpha;
-  a.prev = last;
-  a.cur = cur;
-  a.raw = ctx->d_raw;
-  VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
-  launch(ctx, a, nullptr, nullptr, stats ? ctx->d_cnt : nullptr, nullptr);
-  VRT_HIP(ctx, hipGetLastError());
-  VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
-  VRT_HIP(ctx, hipMemcpy(out_rgba8, cur, pixels * 4, hipMemcpyDeviceToHost));
-  ctx->hist_last = 1 - ctx->hist_last;  // PostRender: std::swap(last, current) (main.cpp:391)
-  if (stats) {
-    unsigned long long h[VRT_CNT_COUNT];
-    VRT_HIP(ctx, hipMemcpy(h, ctx->d_cnt, sizeof(h), hipMemcpyDeviceToHost));
-    for (int q = 0; q < VRT_CNT_COUNT; ++q) stats->counters[q] = h[q];
-    float ms = 0.0f;
-    VRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    stats->kernel_ms = ms;
-  }
-  ctx->err.clear();
-  return VRT_OK;
-}
-
-int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size) {
-  if (!ctx) return VRT_ERR_INVALID;
-  const int st = upload_atlas(ctx, rgba, atlas_size);
-  if (st == VRT_OK) ctx->err.clear();
-  return st;
-}
-
-int vrt_history_reset(vrt_ctx* ctx) {
-  if (!ctx) return VRT_ERR_INVALID;
-  // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer)
-  std::swap(ctx->d_hist[ctx->hist_last], ctx->d_raw);
-  ctx->err.clear();
-  return VRT_OK;
-}
-
-int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* out_rgba,
-               vrt_hit* out_hit, vrt_stats* stats) {
-  if (!ctx) return VRT_ERR_INVALID;
-  int st = check_render_args(ctx, cam, p);
-  if (st != VRT_OK) return st;
-  if (!out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
-  VRT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t pixels = size_t(cam->width) * cam->height;
-  if (pixels > ctx->out_pixels) {
-    if (ctx->d_out) (void)hipFree(ctx->d_out);
-    if (ctx->d_hit) (void)hipFree(ctx->d_hit);
-    ctx->d_out = nullptr;
-    ctx->d_hit = nullptr;
-    ctx->out_pixels = 0;
-    if (hipMalloc(&ctx->d_out, pixels * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&ctx->d_hit, pixels * sizeof(vrt_hit)) != hipSuccess)
-      return fail(ctx, VRT_ERR_OOM, "hipMalloc frame buffers");
-    ctx->out_pixels = pixels;
-  }
-  if (stats)
-    VRT_HIP(ctx, hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, nullptr));
-  const vrt::KArgs a = make_args(ctx, cam, p, 0, cam->height, 1);
-  VRT_HIP(ctx, hipEventRecord(ctx->ev0, nullptr));
-  launch(ctx, a, ctx->d_out, out_hit ? ctx->d_hit : nullptr, stats ? ctx->d_cnt : nullptr, nullptr);
-  VRT_HIP(ctx, hipGetLastError());
-  VRT_HIP(ctx, hipEventRecord(ctx->ev1, nullptr));
-  VRT_HIP(ctx, hipMemcpy(out_rgba, ctx->d_out, pixels * sizeof(float4), hipMemcpyDeviceToHost));
-  if (out_hit)
-    VRT_HIP(ctx, hipMemcpy(out_hit, ctx->d_hit, pixels * sizeof(vrt_hit), hipMemcpyDeviceToHost));
-  if (stats) {
-    unsigned long long h[VRT_CNT_COUNT];
-    VRT_HIP(ctx, hipMemcpy(h, ctx->d_cnt, sizeof(h), hipMemcpyDeviceToHost));
-    for (int q = 0; q < VRT_CNT_COUNT; ++q) stats->counters[q] = h[q];
-    float ms = 0.0f;
-    VRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    stats->kernel_ms = ms;
-  }
-  ctx->err.clear();
-  return VRT_OK;
-}
-
 }  // extern "C"
+#elif defined(VRT_CERT_DIAG)
+extern "C" int vrt_debug_cert_diag(uint64_t* out) { return out ? vrt::debug_cert_diag(out) : VRT_ERR_INVALID; }
+#endif

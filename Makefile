@@ -28,7 +28,8 @@ app: build/bin/vrt_headless
 
 build/bin/vrt_headless: examples/headless_app.cpp $(HDR) $(LIBDIR)/libvrt.so
 	mkdir -p build/bin
-	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ examples/headless_app.cpp -L$(LIBDIR) -lvrt \
+	g++ -O2 -std=c++17 -Wall -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ \
+	    examples/headless_app.cpp -L$(LIBDIR) -lvrt -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 
 # experiment / diagnostic variants for scripts/ab.py, stamps.py, cert_diag.py (never the product

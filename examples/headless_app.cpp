@@ -13,6 +13,11 @@
 //   - the GUI's FPS label from GL_TIME_ELAPSED (:350-360) -> vrt_stats.kernel_ms (timing only:
 //     the fast kernel instance; --counters also counts rays, which runs the exact instance)
 //   - more than one GPU (--device-mask): vrt_create's mask, the frame split into row bands
+//   - --pipelined: the display path. Frames go to a device buffer (vrt_render_frame_device, as a
+//     texture upload for display would consume them) with no per-frame host sync, so consecutive
+//     frames overlap on the GPU; GPU time per frame = hipEvents around the timed frames / count.
+//     The default synchronous loop waits for every frame like the reference's blocking
+//     GL_TIME_ELAPSED readback (main.cpp:352-356) and reports each frame's own GPU time.
 //   - Utils::Screenshot of the last frame (key F1, :424-428) -> a binary PPM (--ppm), and the raw
 //     RGBA8 frame (--raw, row 0 = bottom) for tests
 // Build: make app (-> build/vrt_headless). Usage: build/vrt_headless --help
@@ -22,6 +27,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <hip/hip_runtime.h>
 
 #include "vrt.h"
 
@@ -37,7 +44,7 @@ struct Options {
   std::string atlas_raw;       // textured mode: raw RGBA8 atlas file (size^2 * 4 bytes)
   int atlas_size = 256, atlas_tile = 128;
   std::string ppm, raw;
-  bool quiet = false, counters = false;
+  bool quiet = false, counters = false, pipelined = false;
   uint32_t device_mask = 1;  // bit i = HIP device i
   int warmup = 0;            // frames excluded from the reported mean
 };
@@ -48,7 +55,7 @@ void usage() {
       "             [--bounces R T] [--alpha A] [--ray-noise x] [--reflection-noise x]\n"
       "             [--refraction-noise x] [--day-night SECONDS_PER_FRAME] [--reset-at K]\n"
       "             [--atlas-raw FILE --atlas-size S --atlas-tile T] [--ppm FILE] [--raw FILE]\n"
-      "             [--device-mask M] [--counters] [--warmup K] [--quiet]");
+      "             [--device-mask M] [--counters] [--warmup K] [--pipelined] [--quiet]");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -82,6 +89,7 @@ bool parse(int argc, char** argv, Options& o) {
     else if (a == "--raw") o.raw = next("--raw");
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--counters") o.counters = true;
+    else if (a == "--pipelined") o.pipelined = true;
     else if (a == "--device-mask") o.device_mask = uint32_t(std::strtoul(next(a.c_str()), nullptr, 0));
     else if (a == "--warmup") o.warmup = std::atoi(next("--warmup"));
     else if (a == "--help" || a == "-h") return false;
@@ -177,6 +185,49 @@ int main(int argc, char** argv) {
   const float day_time = 50.0f;        // dayTime (main.cpp:153)
   float time_of_day = 0.9f * day_time;  // "Make day" (main.cpp:577)
   std::vector<uint8_t> frame(size_t(o.width) * o.height * 4);
+  if (o.pipelined) {  // display path: device frames, no per-frame host sync
+    uint32_t* d_frame = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipSetDevice(vrt_device_ordinal(rt, 0)) != hipSuccess || hipMalloc(&d_frame, frame.size()) != hipSuccess ||
+        hipStreamCreate(&s) != hipSuccess || hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+      std::fprintf(stderr, "HIP setup failed\n");
+      vrt_destroy(rt);
+      return 1;
+    }
+    for (int f = 0; f < o.frames && status == 0; ++f) {
+      if (f == o.warmup) (void)hipEventRecord(e0, s);
+      if (f == o.reset_at) vrt_history_reset(rt);
+      p.time = float(f + 1);
+      vrt_sun_dir(time_of_day, day_time, p.sun_dir);
+      if (vrt_render_frame_device(rt, &cam, &p, o.alpha, d_frame, s, nullptr) != VRT_OK) {
+        std::fprintf(stderr, "vrt_render_frame_device: %s\n", vrt_last_error(rt));
+        status = 1;
+      }
+      if (o.frame_seconds > 0.0f) {
+        time_of_day += o.frame_seconds;
+        while (time_of_day > day_time) time_of_day -= day_time;
+      }
+    }
+    (void)hipEventRecord(e1, s);
+    if (status == 0 && hipMemcpyAsync(frame.data(), d_frame, frame.size(), hipMemcpyDeviceToHost, s) != hipSuccess)
+      status = 1;
+    if (hipStreamSynchronize(s) != hipSuccess) status = 1;
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const int timed = o.frames - o.warmup;
+    if (status == 0 && timed > 0)
+      std::printf("pipelined: timed %d frames (after %d warm-up) on %d device(s): mean %.4f ms GPU time per frame\n",
+                  timed, o.warmup, vrt_device_count(rt), ms / timed);
+    (void)hipFree(d_frame);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(s);
+    if (status == 0 && !o.raw.empty() && !write_file(o.raw, frame.data(), frame.size())) status = 1;
+    if (status == 0 && !o.ppm.empty() && !write_ppm(o.ppm, frame, o.width, o.height)) status = 1;
+    vrt_destroy(rt);
+    return status;
+  }
   double ms_sum = 0.0;
   int timed = 0;
   for (int f = 0; f < o.frames && status == 0; ++f) {

@@ -54,8 +54,12 @@ struct Shard {
   unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
   // streams and events of whole-frame renders
   hipStream_t part[kParts] = {nullptr, nullptr};
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;  // timing, on part[0]
-  hipEvent_t ev_join = nullptr;                      // part[1] done
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;  // frame begin / end on part[0] (ordering)
+  hipEvent_t ev_join = nullptr;                      // part[1] done / caller-stream marker
+  hipEvent_t ev_pdone[kParts] = {nullptr, nullptr};  // a part's rows copied to the device output
+  // GPU time of each part launch: recorded when the kernel starts / ends on the device
+  hipEvent_t ev_kbeg[kParts] = {nullptr, nullptr}, ev_kend[kParts] = {nullptr, nullptr};
+  bool timed[kParts] = {false, false};               // parts launched by the last frame
   // this device's row band of the whole-frame buffers (band_cap rows x width)
   uint32_t* d_hist = nullptr;  // filtered frame = temporal history, filtered in place
   uint32_t* d_raw = nullptr;   // quantised ray-trace frame (the rayTrace FBO; key F)
@@ -147,7 +151,8 @@ void shard_free(Shard& s) {
     if (p) (void)hipFree(p);
   for (auto& o : s.order)
     if (o.done) (void)hipEventDestroy(o.done);
-  for (hipEvent_t e : {s.ev_start, s.ev_stop, s.ev_join})
+  for (hipEvent_t e : {s.ev_start, s.ev_stop, s.ev_join, s.ev_kbeg[0], s.ev_kbeg[1], s.ev_kend[0], s.ev_kend[1],
+                       s.ev_pdone[0], s.ev_pdone[1]})
     if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : s.part)
     if (st) (void)hipStreamDestroy(st);
@@ -163,6 +168,11 @@ hipError_t shard_init(Shard& s, int device) {
   if (e == hipSuccess) e = hipEventCreate(&s.ev_start);
   if (e == hipSuccess) e = hipEventCreate(&s.ev_stop);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming);
+  for (int p = 0; p < kParts && e == hipSuccess; ++p) {
+    e = hipEventCreateWithFlags(&s.ev_pdone[p], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&s.ev_kbeg[p]);
+    if (e == hipSuccess) e = hipEventCreate(&s.ev_kend[p]);
+  }
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT);
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt_rep, rep_bytes);
   if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
@@ -299,12 +309,13 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
 }
 
 // One band launch on `st` (heavy-first tile order for uncounted launches), then, when counting,
-// the fold of the counter replicas into `cnt` (accumulating).
+// the fold of the counter replicas into `cnt` (accumulating). ev_begin / ev_end: optional device
+// timestamps of the kernel's start and end.
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
-            hipStream_t st) {
+            hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr) {
   const bool stats = hit || cnt;
   OrderSlot* slot = stats ? nullptr : tile_order_begin(ctx, s, a, st);
-  vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st);
+  vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
   if (slot) (void)hipEventRecord(slot->done, st);
 }
@@ -439,8 +450,10 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
 // (or, when counting or writing hit records, one exact-instance launch on part[0]), bracketed by
 // ev_start / ev_stop on part[0] with part[1] joined. rgba8: the temporal path into d_hist (in
 // place) + d_raw; else the float band into d_out (+ d_hit).
+// pipelined (one device, uncounted): no cross-part ordering at all — each part stream depends
+// only on its own previous frame (disjoint rows), so frame k+1's parts fill frame k's tail.
 int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, bool rgba8,
-                 bool hits, bool counting) {
+                 bool hits, bool counting, bool pipelined = false) {
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
@@ -450,30 +463,32 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
     if (counting)
       VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.part[0]));
     VRT_HIP(ctx, hipEventRecord(s.ev_start, s.part[0]));
+    s.timed[0] = s.timed[1] = false;
     const int32_t hb = band_rows(h, k, j);
     if (hb > 0) {
       const bool single = counting || hits;  // one counter replica set: one counted launch
       const int32_t nparts = single ? 1 : kParts;
-      if (!single) VRT_HIP(ctx, hipStreamWaitEvent(s.part[1], s.ev_start, 0));
+      if (!single && !pipelined) VRT_HIP(ctx, hipStreamWaitEvent(s.part[1], s.ev_start, 0));
       for (int32_t q = 0; q < nparts; ++q) {
         const PartRows pr = single ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
         if (pr.rows == 0) continue;
         vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
         a.pitch = int32_t(int64_t(w) * (single ? 1 : kParts));
         const size_t off = size_t(pr.band_row0) * size_t(w);
+        s.timed[q] = true;
         if (rgba8) {
           a.alpha = alpha;
           a.prev = s.d_hist + off;
           a.cur = s.d_hist + off;
           a.raw = s.d_raw + off;
-          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q]);
+          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q], s.ev_kbeg[q], s.ev_kend[q]);
         } else {
           launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
-                 s.part[q]);
+                 s.part[q], s.ev_kbeg[q], s.ev_kend[q]);
         }
         VRT_HIP(ctx, hipGetLastError());
       }
-      if (!single) {
+      if (!single && !pipelined) {
         VRT_HIP(ctx, hipEventRecord(s.ev_join, s.part[1]));
         VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
       }
@@ -484,17 +499,31 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
   return VRT_OK;
 }
 
-// Wait for every device, then fill stats (kernel_ms = the slowest device; counters summed).
+// Wait for every device, then fill stats: kernel_ms = the slowest device's span from its first
+// part kernel's start to its last part kernel's end (device timestamps: the GPU time of the
+// frame, as GL_TIME_ELAPSED measured the draw); counters summed.
 int finish_frame(vrt_ctx* ctx, vrt_stats* stats, bool counting) {
   float ms_max = 0.0f;
   unsigned long long tot[VRT_CNT_COUNT] = {0};
   for (Shard& s : ctx->sh) {
     VRT_HIP(ctx, hipSetDevice(s.device));
-    VRT_HIP(ctx, hipStreamSynchronize(s.part[0]));
+    for (hipStream_t st : s.part) VRT_HIP(ctx, hipStreamSynchronize(st));
     if (stats) {
-      float ms = 0.0f;
-      VRT_HIP(ctx, hipEventElapsedTime(&ms, s.ev_start, s.ev_stop));
-      ms_max = std::max(ms_max, ms);
+      int first = -1;
+      for (int q = 0; q < kParts; ++q)
+        if (s.timed[q] && first < 0) first = q;
+      if (first >= 0) {  // times relative to the first part's start (may be negative)
+        float lo = 0.0f, hi = 0.0f;
+        for (int q = 0; q < kParts; ++q) {
+          if (!s.timed[q]) continue;
+          float b = 0.0f, e = 0.0f;
+          VRT_HIP(ctx, hipEventElapsedTime(&b, s.ev_kbeg[first], s.ev_kbeg[q]));
+          VRT_HIP(ctx, hipEventElapsedTime(&e, s.ev_kbeg[first], s.ev_kend[q]));
+          lo = std::min(lo, b);
+          hi = std::max(hi, e);
+        }
+        ms_max = std::max(ms_max, hi - lo);
+      }
     }
     if (counting) {
       unsigned long long c[VRT_CNT_COUNT];
@@ -863,11 +892,33 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   DeviceGuard guard;
   if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
-  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
   Shard& root = ctx->sh[0];
   hipStream_t cs = static_cast<hipStream_t>(hip_stream);
   const size_t row = size_t(w) * 4;
+  if (k == 1 && !counting) {
+    // one device: pipelined. Each part stream renders its rows in place, then (after the caller's
+    // prior work on hip_stream, which may still read d_out) copies them into d_out; the caller's
+    // stream waits for both parts. No part waits for the other, so consecutive frames overlap as
+    // in the bench's FrameTiler.
+    VRT_HIP(ctx, hipSetDevice(root.device));
+    VRT_HIP(ctx, hipEventRecord(root.ev_join, cs));
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, false, true)) != VRT_OK) return st;
+    for (int q = 0; q < kParts; ++q) {
+      const PartRows pr = part_rows(h, 1, kParts, 0, q);
+      if (pr.rows == 0) continue;
+      VRT_HIP(ctx, hipStreamWaitEvent(root.part[q], root.ev_join, 0));
+      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(d_out_rgba8) + size_t(q) * row, kParts * row,
+                                    root.d_hist + size_t(q) * w, kParts * row, row, size_t(pr.rows),
+                                    hipMemcpyDeviceToDevice, root.part[q]));
+      VRT_HIP(ctx, hipEventRecord(root.ev_pdone[q], root.part[q]));
+      VRT_HIP(ctx, hipStreamWaitEvent(cs, root.ev_pdone[q], 0));
+    }
+    if (stats && (st = finish_frame(ctx, stats, false)) != VRT_OK) return st;
+    ctx->err.clear();
+    return VRT_OK;
+  }
+  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
   VRT_HIP(ctx, hipSetDevice(root.device));
   // the copies into d_out follow the caller's prior work on its stream
   VRT_HIP(ctx, hipEventRecord(root.ev_join, cs));

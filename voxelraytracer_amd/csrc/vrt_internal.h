@@ -55,8 +55,11 @@ constexpr uint32_t kOrdHdr = 0;             // tile-order buffer: per-tile wave 
 
 // render_kernel: the instance is chosen from (stats, a.textured, a.cert); grid = a.tiles, or
 // 2 * a.tiles with a tile order (a.order). cnt_rep: the counter replicas (stats launches).
+// ev_begin / ev_end (optional, timing events) are recorded when the kernel starts and ends on
+// the device (hipExtLaunchKernelGGL), not when the host enqueues it.
 void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,
-                   unsigned long long* cnt_rep, hipStream_t s);
+                   unsigned long long* cnt_rep, hipStream_t s, hipEvent_t ev_begin = nullptr,
+                   hipEvent_t ev_end = nullptr);
 // fold the counter replicas into dst (accumulating) and re-zero them
 void launch_reduce_counters(unsigned long long* rep, unsigned long long* dst, hipStream_t s);
 // the kernel's packed volume from the canonical N^3 bytes: 8 octant forward-distance volumes

@@ -9,6 +9,7 @@
 // Device volume layout: (N+1)^3 bytes, x fastest, where plane N repeats plane 0 on each axis.
 // GetVoxel's texel for a coordinate c in [0, N] is then simply floor(c) (GL_REPEAT folded into
 // the layout), and the hot loop addresses it with two 24-bit multiply-adds.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2047,17 +2048,20 @@ __global__ void __launch_bounds__(256) fwd_pack_kernel(const uint8_t* __restrict
 namespace vrt {
 
 void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,
-                   unsigned long long* cnt_rep, hipStream_t s) {
+                   unsigned long long* cnt_rep, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end) {
   const dim3 grid(a.order ? 2u * a.tiles : a.tiles);
   // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
   // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
   // ~5 %), exact walks only (0)
-  hipLaunchKernelGGL(a.textured ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
-                                : (stats ? render_kernel<true, false>
-                                         : (a.cert == 2 ? render_kernel<false, false, 2>
-                                            : a.cert == 1 ? render_kernel<false, false, 1>
-                                                          : render_kernel<false, false, 0>)),
-                     grid, dim3(kWgThreads), 0, s, a, vox, out, hit, cnt_rep);
+  auto kern = a.textured ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
+                         : (stats ? render_kernel<true, false>
+                                  : (a.cert == 2 ? render_kernel<false, false, 2>
+                                     : a.cert == 1 ? render_kernel<false, false, 1>
+                                                   : render_kernel<false, false, 0>));
+  if (ev_begin || ev_end)
+    hipExtLaunchKernelGGL(kern, grid, dim3(kWgThreads), 0, s, ev_begin, ev_end, 0, a, vox, out, hit, cnt_rep);
+  else
+    hipLaunchKernelGGL(kern, grid, dim3(kWgThreads), 0, s, a, vox, out, hit, cnt_rep);
 }
 
 void launch_reduce_counters(unsigned long long* rep, unsigned long long* dst, hipStream_t s) {

@@ -13,7 +13,7 @@
 //   - the GUI's FPS label from GL_TIME_ELAPSED (:350-360) -> vrt_stats.kernel_ms (timing only:
 //     the fast kernel instance; --counters also counts rays, which runs the exact instance)
 //   - more than one GPU (--device-mask): vrt_create's mask, the frame split into row bands
-//   - --pipelined: the display path. Frames go to a device buffer (vrt_render_frame_device, as a
+//   - --pipelined: the display path. Frames stay on the device (vrt_render_frame_device, where a
 //     texture upload for display would consume them) with no per-frame host sync, so consecutive
 //     frames overlap on the GPU; GPU time per frame = hipEvents around the timed frames / count.
 //     The default synchronous loop waits for every frame like the reference's blocking
@@ -186,11 +186,11 @@ int main(int argc, char** argv) {
   float time_of_day = 0.9f * day_time;  // "Make day" (main.cpp:577)
   std::vector<uint8_t> frame(size_t(o.width) * o.height * 4);
   if (o.pipelined) {  // display path: device frames, no per-frame host sync
-    uint32_t* d_frame = nullptr;
+    const uint32_t* d_frame = nullptr;
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (hipSetDevice(vrt_device_ordinal(rt, 0)) != hipSuccess || hipMalloc(&d_frame, frame.size()) != hipSuccess ||
-        hipStreamCreate(&s) != hipSuccess || hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    if (hipSetDevice(vrt_device_ordinal(rt, 0)) != hipSuccess || hipStreamCreate(&s) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
       std::fprintf(stderr, "HIP setup failed\n");
       vrt_destroy(rt);
       return 1;
@@ -200,7 +200,7 @@ int main(int argc, char** argv) {
       if (f == o.reset_at) vrt_history_reset(rt);
       p.time = float(f + 1);
       vrt_sun_dir(time_of_day, day_time, p.sun_dir);
-      if (vrt_render_frame_device(rt, &cam, &p, o.alpha, d_frame, s, nullptr) != VRT_OK) {
+      if (vrt_render_frame_device(rt, &cam, &p, o.alpha, s, &d_frame, nullptr) != VRT_OK) {
         std::fprintf(stderr, "vrt_render_frame_device: %s\n", vrt_last_error(rt));
         status = 1;
       }
@@ -219,7 +219,6 @@ int main(int argc, char** argv) {
     if (status == 0 && timed > 0)
       std::printf("pipelined: timed %d frames (after %d warm-up) on %d device(s): mean %.4f ms GPU time per frame\n",
                   timed, o.warmup, vrt_device_count(rt), ms / timed);
-    (void)hipFree(d_frame);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipStreamDestroy(s);

@@ -281,15 +281,19 @@ int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
 int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params, float alpha,
                      uint8_t* out_rgba8, vrt_stats* stats);
 
-/* ABI v8: the same frame assembled on the first device: the new filtered frame (W*H RGBA8 words,
- * row 0 = bottom) is written to the DEVICE buffer d_out_rgba8 on the context's first GPU, ordered
- * after prior work on hip_stream and before later work on it (e.g. a texture upload for display).
- * With several devices the bands are gathered to the first one over xGMI by ncclGather
- * (rccl.h) and placed into their rows by strided copies; one device copies its frame. Returns
- * after the launches (asynchronous); stats (kernel_ms only) may be NULL and then no host sync
- * happens. */
+/* ABI v8: the same frame for display on the first device, asynchronously. *d_frame receives a
+ * device pointer (first GPU) to the new filtered frame, W*H RGBA8 words, row 0 = bottom, owned by
+ * the context; hip_stream is made to wait for it, so work the caller enqueues there afterwards
+ * (e.g. the texture upload / blit of main.cpp:379-385) sees the frame. The frame stays valid until
+ * the third later call, which overwrites it only after the work the caller had enqueued on
+ * hip_stream before the next call. One device: the frame is rendered straight into that buffer
+ * (no copy) and consecutive frames overlap on the GPU; several devices: the bands are gathered to
+ * the first one over xGMI by ncclGather (rccl.h) and placed into their rows by strided copies.
+ * Returns after the launches; stats may be NULL (then no host sync happens; with stats the call
+ * waits for the frame). */
 int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
-                            float alpha, uint32_t* d_out_rgba8, void* hip_stream, vrt_stats* stats);
+                            float alpha, void* hip_stream, const uint32_t** d_frame,
+                            vrt_stats* stats);
 
 /* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history. */
 int vrt_history_reset(vrt_ctx* ctx);

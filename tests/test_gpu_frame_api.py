@@ -88,23 +88,44 @@ def test_device_list_splits_frames_into_bands(built, devs):
 
 @pytest.mark.parametrize("devs", [0, [0, 0]], ids=["k1", "k2"])
 def test_frame_device_output(built, devs):
+    """vrt_render_frame_device hands out the frame on the first device (k1: the ring buffer it was
+    rendered into; k2: the assembled bands), identical to the synchronous frames; a frame stays
+    valid for two more frames."""
     scene, n, w, h, R, T = "refraction", 128, 320, 181, 4, 4
-    ref = sequence(0, scene, n, w, h, R, T, [1.0, 0.5])
+    alphas = [1.0, 0.5, 0.5, 0.5, 0.7]
+    ref = sequence(0, scene, n, w, h, R, T, alphas)
     with vrt.Renderer(devs) as r:
         r.upload_volume(vrt.build_scene(scene, n), n)
         cam = vrt.make_camera(w, h)
         s = torch.cuda.Stream()
-        outs = []
-        for i, a in enumerate([1.0, 0.5]):
-            d = torch.full((h, w, 4), 7, dtype=torch.uint8, device="cuda")
+        ptrs = []
+        ms = None
+        for i, a in enumerate(alphas):
             s.wait_stream(torch.cuda.current_stream())
-            ms = r.render_frame_device(cam, vrt.default_params(R, T, time=float(i + 1)), a,
-                                       d.data_ptr(), s.cuda_stream, timing=(i == 1))
-            torch.cuda.current_stream().wait_stream(s)
-            outs.append(d.cpu().numpy())
+            ptr, t = r.render_frame_device(cam, vrt.default_params(R, T, time=float(i + 1)), a,
+                                           s.cuda_stream, timing=(i == 1))
+            ms = ms or t
+            ptrs.append(ptr)
+            if i >= 2:   # frame i-2 is still valid after frame i
+                torch.cuda.current_stream().wait_stream(s)
+                for j in (i - 2, i):
+                    got = np.empty((h, w, 4), np.uint8)
+                    hipcopy(got, ptrs[j])
+                    assert np.array_equal(got, ref[j]), f"frame {j} read after frame {i}"
         assert ms is not None and ms > 0
-    for k, (a, b) in enumerate(zip(outs, ref)):
-        assert np.array_equal(a, b), f"frame {k}"
+        assert len(set(ptrs[:3])) == 3 and ptrs[3] == ptrs[0]
+
+
+def hipcopy(dst: np.ndarray, ptr: int):
+    """Device -> host copy of a raw device pointer, viewed as a torch tensor through
+    __cuda_array_interface__."""
+
+    class View:
+        __cuda_array_interface__ = {"shape": dst.shape, "typestr": "|u1", "data": (ptr, True),
+                                    "version": 3}
+
+    torch.cuda.synchronize()
+    dst[...] = torch.as_tensor(View(), device="cuda").cpu().numpy()
 
 
 def test_headless_app_gets_the_bench_frame_time(built, tmp_path):

@@ -327,17 +327,18 @@ class Renderer:
         stats["kernel_ms"] = float(st.kernel_ms)
         return out, stats
 
-    def render_frame_device(self, cam: Camera, params: Params, alpha: float, d_out: int,
-                            stream: int = 0, timing: bool = False):
-        """vrt_render_frame_device: the filtered frame assembled on the first device into d_out
-        (W*H RGBA8 words, e.g. a torch uint32/uint8 tensor's data_ptr()), ordered on `stream`.
-        timing=True waits for the frame and returns kernel_ms."""
+    def render_frame_device(self, cam: Camera, params: Params, alpha: float, stream: int = 0,
+                            timing: bool = False):
+        """vrt_render_frame_device: the next filtered frame for display, on the first device,
+        ordered on `stream`. Returns (device pointer of the W*H RGBA8 frame, owned by the context
+        and valid until the third later call; kernel_ms or None). timing=True waits for the frame."""
         st = abi.Stats() if timing else None
+        ptr = C.c_void_p()
         self._check(self._lib.vrt_render_frame_device(self._h, C.byref(cam), C.byref(params), alpha,
-                                                      d_out, stream or None,
+                                                      stream or None, C.byref(ptr),
                                                       C.byref(st) if st is not None else None),
                     "vrt_render_frame_device")
-        return float(st.kernel_ms) if st is not None else None
+        return ptr.value, (float(st.kernel_ms) if st is not None else None)
 
     def history_reset(self):
         """Key F (main.cpp:417-421): the last ray-traced frame becomes the temporal history."""

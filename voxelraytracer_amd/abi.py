@@ -153,8 +153,8 @@ SIGNATURES = {
     ),
     "vrt_render_frame_device": (
         C.c_int,
-        [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p, C.c_void_p,
-         C.POINTER(Stats)],
+        [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p,
+         C.POINTER(C.c_void_p), C.POINTER(Stats)],
     ),
     "vrt_history_reset": (C.c_int, [C.c_void_p]),
     "vrt_upload_atlas": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),

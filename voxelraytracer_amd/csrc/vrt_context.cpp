@@ -29,12 +29,16 @@ namespace {
 constexpr int kParts = 2;              // interleaved row parts per device band
 constexpr int kOrderSlots = 8;         // tile-order buffers per device (band geometry x stream)
 constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 4096 x 4096 pixels
+// Filtered frames rotate through kRing buffers: frame f reads ring[(f-1) % kRing] (the temporal
+// history) and writes ring[f % kRing]. A device-output frame (vrt_render_frame_device) is handed
+// to the caller as its ring buffer and stays valid for two more frames with no copy.
+constexpr int kRing = 3;
 
 struct OrderSlot {
   int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
   hipStream_t stream = nullptr;
   uint32_t* d = nullptr;       // 3 x kOrderMaxTiles words inside the shard's pool
-  hipEvent_t done = nullptr;   // recorded after every launch that used the slot
+  hipEvent_t done = nullptr;   // recorded on the slot's stream when the slot is handed over
   bool used = false;
   uint64_t epoch = 0, tick = 0;
 };
@@ -56,13 +60,13 @@ struct Shard {
   hipStream_t part[kParts] = {nullptr, nullptr};
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;  // frame begin / end on part[0] (ordering)
   hipEvent_t ev_join = nullptr;                      // part[1] done / caller-stream marker
-  hipEvent_t ev_pdone[kParts] = {nullptr, nullptr};  // a part's rows copied to the device output
+  hipEvent_t ev_pdone[kParts] = {nullptr, nullptr};  // a part of a device-output frame is done
   // GPU time of each part launch: recorded when the kernel starts / ends on the device
   hipEvent_t ev_kbeg[kParts] = {nullptr, nullptr}, ev_kend[kParts] = {nullptr, nullptr};
   bool timed[kParts] = {false, false};               // parts launched by the last frame
   // this device's row band of the whole-frame buffers (band_cap rows x width)
-  uint32_t* d_hist = nullptr;  // filtered frame = temporal history, filtered in place
-  uint32_t* d_raw = nullptr;   // quantised ray-trace frame (the rayTrace FBO; key F)
+  uint32_t* d_ring[kRing] = {nullptr, nullptr, nullptr};  // filtered bands (history ring)
+  uint32_t* d_raw = nullptr;   // quantised ray-trace band (the rayTrace FBO; key F)
   size_t hist_pixels = 0;
   float4* d_out = nullptr;     // vrt_render's float band
   vrt_hit* d_hit = nullptr;
@@ -87,8 +91,12 @@ struct vrt_ctx {
   bool tile_order = true;               // vrt_set_tile_order
   const uint8_t* atlas_src = nullptr;   // host buffer of the last atlas upload
   int32_t hist_w = 0, hist_h = 0;       // image size of the resident whole-frame history
+  uint64_t fk = 0;                      // frames rendered into the resident history
   uint32_t* d_gather = nullptr;         // first device: k x band_cap x width words (ncclGather)
-  size_t gather_pixels = 0;
+  size_t hist_pixels_gather = 0;
+  uint32_t* d_frames[kRing] = {nullptr, nullptr, nullptr};  // first device, k > 1: assembled frames
+  hipEvent_t ev_consumed[kRing] = {nullptr, nullptr, nullptr};  // caller stream: ring slot consumed
+  bool consumed_valid[kRing] = {false, false, false};
   hipEvent_t ev_gathered = nullptr;     // first device: the last device-output frame is assembled
   bool gather_pending = false;
   std::string err;
@@ -146,7 +154,8 @@ PartRows part_rows(int32_t height, int32_t k, int32_t parts, int32_t j, int32_t 
 void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
   for (void* p : {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats, (void*)s.d_cnt,
-                  (void*)s.d_cnt_rep, (void*)s.d_hist, (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
+                  (void*)s.d_cnt_rep, (void*)s.d_ring[0], (void*)s.d_ring[1], (void*)s.d_ring[2],
+                  (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
                   (void*)s.d_atlas, (void*)s.d_order_pool})
     if (p) (void)hipFree(p);
   for (auto& o : s.order)
@@ -165,8 +174,10 @@ hipError_t shard_init(Shard& s, int device) {
   const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
   const size_t pool_words = size_t(kOrderSlots) * 3u * kOrderMaxTiles;
   for (int p = 0; p < kParts && e == hipSuccess; ++p) e = hipStreamCreateWithFlags(&s.part[p], hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&s.ev_start);
-  if (e == hipSuccess) e = hipEventCreate(&s.ev_stop);
+  // ordering markers without timestamps (timing events make the command processor stamp and
+  // flush around them: ~20 us gaps between the launches of a stream, measured)
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_start, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_stop, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming);
   for (int p = 0; p < kParts && e == hipSuccess; ++p) {
     e = hipEventCreateWithFlags(&s.ev_pdone[p], hipEventDisableTiming);
@@ -269,9 +280,12 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
 }
 
 // The tile-order slot of this launch's band and stream, from the shard's pool (no allocation, no
-// host sync). Reusing the least recently used slot for another band / stream waits on the device
-// for that slot's last launch, then zeroes it on this stream (no heavy tiles yet). Not while the
-// stream is being captured into a graph (a replayed node would reuse one flag set): dispatch order.
+// host sync). Reusing the least recently used slot for another band / stream first marks the
+// slot's old stream (everything enqueued there so far, its last launch with the slot included)
+// and makes this stream wait for that mark on the device, then zeroes the slot on this stream (no
+// heavy tiles yet). No marker is needed per launch: launches on one stream are ordered. Not while
+// the stream is being captured into a graph (a replayed node would reuse one flag set): dispatch
+// order then.
 OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
   // only where it pays: glass in the volume (no bounce stacks otherwise: the first pass would be
   // `tiles` empty workgroups, C2/C4 +4 %) and certified pixels (glass-heavy volumes, where most
@@ -290,7 +304,14 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
     slot = &s.order[0];
     for (auto& o : s.order)
       if (!o.used || (slot->used && o.tick < slot->tick)) slot = &o;
-    if (slot->used && hipStreamWaitEvent(st, slot->done, 0) != hipSuccess) return nullptr;
+    if (slot->used && slot->stream != st) {
+      // the old stream may have been destroyed by its owner: then wait for the whole device
+      if (hipEventRecord(slot->done, slot->stream) == hipSuccess) {
+        if (hipStreamWaitEvent(st, slot->done, 0) != hipSuccess) return nullptr;
+      } else if (hipDeviceSynchronize() != hipSuccess) {
+        return nullptr;
+      }
+    }
     if (hipMemsetAsync(slot->d, 0, size_t(3) * a.tiles * sizeof(uint32_t), st) != hipSuccess) return nullptr;
     slot->width = a.width;
     slot->rows = a.rows;
@@ -314,10 +335,9 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
             hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr) {
   const bool stats = hit || cnt;
-  OrderSlot* slot = stats ? nullptr : tile_order_begin(ctx, s, a, st);
+  if (!stats) tile_order_begin(ctx, s, a, st);
   vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
-  if (slot) (void)hipEventRecord(slot->done, st);
 }
 
 int volume_alloc(vrt_ctx* ctx, Shard& s, int32_t n) {
@@ -419,7 +439,9 @@ int broadcast_volume(vrt_ctx* ctx) {
   return VRT_OK;
 }
 
-// Whole-frame band buffers of every device for a W x H frame (history black on (re)creation).
+// Whole-frame band buffers of every device for a W x H frame (history black on (re)creation):
+// the ring of filtered bands and the raw band; with several devices, the first device's ring of
+// assembled frames.
 int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
   if (w == ctx->hist_w && h == ctx->hist_h) return VRT_OK;
   const int32_t k = int32_t(ctx->sh.size());
@@ -428,32 +450,46 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     VRT_HIP(ctx, hipDeviceSynchronize());  // nothing may still read the old buffers
     if (pixels > s.hist_pixels) {
-      for (uint32_t** b : {&s.d_hist, &s.d_raw}) {
+      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_raw}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
       }
       s.hist_pixels = 0;
-      if (hipMalloc(&s.d_hist, pixels * 4) != hipSuccess || hipMalloc(&s.d_raw, pixels * 4) != hipSuccess)
-        return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
+      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_raw})
+        if (hipMalloc(b, pixels * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
       s.hist_pixels = pixels;
     }
-    VRT_HIP(ctx, hipMemset(s.d_hist, 0, pixels * 4));
-    VRT_HIP(ctx, hipMemset(s.d_raw, 0, pixels * 4));
+    for (uint32_t* b : {s.d_ring[0], s.d_ring[1], s.d_ring[2], s.d_raw}) VRT_HIP(ctx, hipMemset(b, 0, pixels * 4));
+  }
+  if (k > 1) {
+    VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+    for (uint32_t*& f : ctx->d_frames) {
+      if (f) (void)hipFree(f);
+      f = nullptr;
+      if (hipMalloc(&f, size_t(w) * size_t(h) * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc frames");
+    }
   }
   ctx->hist_w = w;
   ctx->hist_h = h;
+  ctx->fk = 0;
   ctx->gather_pending = false;
+  for (bool& v : ctx->consumed_valid) v = false;
   return VRT_OK;
 }
 
 // Launch one whole frame on every device: band j as kParts interleaved parts on the part streams
 // (or, when counting or writing hit records, one exact-instance launch on part[0]), bracketed by
-// ev_start / ev_stop on part[0] with part[1] joined. rgba8: the temporal path into d_hist (in
-// place) + d_raw; else the float band into d_out (+ d_hit).
+// ev_start / ev_stop on part[0] with part[1] joined. rgba8: the temporal path from the history
+// ring[(fk-1) % kRing] into ring[fk % kRing] + d_raw (frame fk); else the float band into d_out
+// (+ d_hit). wait_consumed: every part first waits for the caller's consumption of the ring slot
+// it overwrites (device-output frames, one device).
 // pipelined (one device, uncounted): no cross-part ordering at all — each part stream depends
 // only on its own previous frame (disjoint rows), so frame k+1's parts fill frame k's tail.
+// timing: device timestamps of every part kernel's start and end (vrt_stats.kernel_ms); only
+// when the caller asked for stats, since timing events cost latency between launches.
 int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, bool rgba8,
-                 bool hits, bool counting, bool pipelined = false) {
+                 bool hits, bool counting, bool timing, bool pipelined = false,
+                 hipEvent_t wait_consumed = nullptr) {
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
@@ -462,29 +498,32 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
       VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], ctx->ev_gathered, 0));
     if (counting)
       VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.part[0]));
-    VRT_HIP(ctx, hipEventRecord(s.ev_start, s.part[0]));
+    if (!pipelined) VRT_HIP(ctx, hipEventRecord(s.ev_start, s.part[0]));
     s.timed[0] = s.timed[1] = false;
     const int32_t hb = band_rows(h, k, j);
     if (hb > 0) {
       const bool single = counting || hits;  // one counter replica set: one counted launch
       const int32_t nparts = single ? 1 : kParts;
       if (!single && !pipelined) VRT_HIP(ctx, hipStreamWaitEvent(s.part[1], s.ev_start, 0));
+      if (wait_consumed)
+        for (int32_t q = 0; q < nparts; ++q) VRT_HIP(ctx, hipStreamWaitEvent(s.part[q], wait_consumed, 0));
       for (int32_t q = 0; q < nparts; ++q) {
         const PartRows pr = single ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
         if (pr.rows == 0) continue;
         vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
         a.pitch = int32_t(int64_t(w) * (single ? 1 : kParts));
         const size_t off = size_t(pr.band_row0) * size_t(w);
-        s.timed[q] = true;
+        s.timed[q] = timing;
+        hipEvent_t kb = timing ? s.ev_kbeg[q] : nullptr, ke = timing ? s.ev_kend[q] : nullptr;
         if (rgba8) {
           a.alpha = alpha;
-          a.prev = s.d_hist + off;
-          a.cur = s.d_hist + off;
+          a.prev = s.d_ring[(ctx->fk + kRing - 1) % kRing] + off;
+          a.cur = s.d_ring[ctx->fk % kRing] + off;
           a.raw = s.d_raw + off;
-          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q], s.ev_kbeg[q], s.ev_kend[q]);
+          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q], kb, ke);
         } else {
           launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
-                 s.part[q], s.ev_kbeg[q], s.ev_kend[q]);
+                 s.part[q], kb, ke);
         }
         VRT_HIP(ctx, hipGetLastError());
       }
@@ -493,7 +532,7 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
         VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
       }
     }
-    VRT_HIP(ctx, hipEventRecord(s.ev_stop, s.part[0]));
+    if (!pipelined) VRT_HIP(ctx, hipEventRecord(s.ev_stop, s.part[0]));
   }
   ctx->gather_pending = false;
   return VRT_OK;
@@ -576,7 +615,10 @@ int create(const std::vector<int>& devs, vrt_ctx** out) {
       if (devs[i] == devs[j]) c->distinct = false;
   }
   if (hipSetDevice(devs[0]) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_consumed[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_consumed[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_consumed[2], hipEventDisableTiming) != hipSuccess) {
     vrt_destroy(c);
     return VRT_ERR_DEVICE;
   }
@@ -622,6 +664,10 @@ void vrt_destroy(vrt_ctx* c) {
   if (!c->sh.empty()) {
     (void)hipSetDevice(c->sh[0].device);
     if (c->d_gather) (void)hipFree(c->d_gather);
+    for (uint32_t* f : c->d_frames)
+      if (f) (void)hipFree(f);
+    for (hipEvent_t e : c->ev_consumed)
+      if (e) (void)hipEventDestroy(e);
     if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
   }
   for (Shard& s : c->sh) shard_free(s);
@@ -874,9 +920,10 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, f
   DeviceGuard guard;
   if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
-  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
+  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr)) != VRT_OK) return st;
   std::vector<const void*> bands;
-  for (Shard& s : ctx->sh) bands.push_back(s.d_hist);
+  for (Shard& s : ctx->sh) bands.push_back(s.d_ring[ctx->fk % kRing]);
+  ctx->fk++;
   if ((st = copy_bands_to_host(ctx, cam->width, cam->height, bands.data(), 4, out_rgba8)) != VRT_OK) return st;
   if ((st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
   ctx->err.clear();
@@ -884,65 +931,58 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, f
 }
 
 int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,
-                            uint32_t* d_out_rgba8, void* hip_stream, vrt_stats* stats) {
+                            void* hip_stream, const uint32_t** d_frame, vrt_stats* stats) {
   if (!ctx) return VRT_ERR_INVALID;
   int st = check_render_args(ctx, cam, p);
   if (st != VRT_OK) return st;
-  if (!d_out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
+  if (!d_frame) return fail(ctx, VRT_ERR_INVALID, "null frame pointer");
   DeviceGuard guard;
   if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
   Shard& root = ctx->sh[0];
   hipStream_t cs = static_cast<hipStream_t>(hip_stream);
-  const size_t row = size_t(w) * 4;
-  if (k == 1 && !counting) {
-    // one device: pipelined. Each part stream renders its rows in place, then (after the caller's
-    // prior work on hip_stream, which may still read d_out) copies them into d_out; the caller's
-    // stream waits for both parts. No part waits for the other, so consecutive frames overlap as
-    // in the bench's FrameTiler.
-    VRT_HIP(ctx, hipSetDevice(root.device));
-    VRT_HIP(ctx, hipEventRecord(root.ev_join, cs));
-    if ((st = launch_frame(ctx, cam, p, alpha, true, false, false, true)) != VRT_OK) return st;
+  const uint64_t f = ctx->fk;
+  const int slot = int(f % kRing), prev_slot = int((f + kRing - 1) % kRing);
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  // whatever the caller enqueued on its stream so far consumed the previous frame's slot
+  if (f > 0) {
+    VRT_HIP(ctx, hipEventRecord(ctx->ev_consumed[prev_slot], cs));
+    ctx->consumed_valid[prev_slot] = true;
+  }
+  hipEvent_t reuse = ctx->consumed_valid[slot] ? ctx->ev_consumed[slot] : nullptr;
+  if (k == 1) {
+    // one device: the frame is rendered straight into the ring slot handed to the caller, as two
+    // pipelined parts — no part waits for the other (disjoint rows), so consecutive frames overlap
+    // as in the bench's FrameTiler; only the slot's consumption three frames ago is waited for.
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, !counting, reuse)) !=
+        VRT_OK)
+      return st;
     for (int q = 0; q < kParts; ++q) {
-      const PartRows pr = part_rows(h, 1, kParts, 0, q);
-      if (pr.rows == 0) continue;
-      VRT_HIP(ctx, hipStreamWaitEvent(root.part[q], root.ev_join, 0));
-      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(d_out_rgba8) + size_t(q) * row, kParts * row,
-                                    root.d_hist + size_t(q) * w, kParts * row, row, size_t(pr.rows),
-                                    hipMemcpyDeviceToDevice, root.part[q]));
       VRT_HIP(ctx, hipEventRecord(root.ev_pdone[q], root.part[q]));
       VRT_HIP(ctx, hipStreamWaitEvent(cs, root.ev_pdone[q], 0));
     }
-    if (stats && (st = finish_frame(ctx, stats, false)) != VRT_OK) return st;
-    ctx->err.clear();
-    return VRT_OK;
-  }
-  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting)) != VRT_OK) return st;
-  VRT_HIP(ctx, hipSetDevice(root.device));
-  // the copies into d_out follow the caller's prior work on its stream
-  VRT_HIP(ctx, hipEventRecord(root.ev_join, cs));
-  VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], root.ev_join, 0));
-  if (k == 1) {
-    VRT_HIP(ctx, hipMemcpyAsync(d_out_rgba8, root.d_hist, size_t(h) * row, hipMemcpyDeviceToDevice, root.part[0]));
+    *d_frame = root.d_ring[slot];
   } else {
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr)) != VRT_OK) return st;
     const int32_t cap = band_cap(h, k);
+    const size_t row = size_t(w) * 4;
     const uint32_t* src[64];
     if (ctx->distinct) {  // RCCL gather of the equal-size bands to the first device over xGMI
-      const size_t need = size_t(k) * size_t(cap) * size_t(w);
-      if (need > ctx->gather_pixels) {
+      if (!ctx->d_gather || size_t(k) * size_t(cap) * size_t(w) > ctx->hist_pixels_gather) {
         VRT_HIP(ctx, hipDeviceSynchronize());
         if (ctx->d_gather) (void)hipFree(ctx->d_gather);
         ctx->d_gather = nullptr;
-        ctx->gather_pixels = 0;
+        ctx->hist_pixels_gather = 0;
+        const size_t need = size_t(k) * size_t(cap) * size_t(w);
         if (hipMalloc(&ctx->d_gather, need * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc gather");
-        ctx->gather_pixels = need;
+        ctx->hist_pixels_gather = need;
       }
       VRT_NCCL(ctx, ncclGroupStart());
       for (int32_t j = 0; j < k; ++j) {
         Shard& s = ctx->sh[j];
         (void)hipSetDevice(s.device);
-        const ncclResult_t r = ncclGather(s.d_hist, j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
+        const ncclResult_t r = ncclGather(s.d_ring[slot], j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
                                           ncclUint8, 0, ctx->comms[j], s.part[0]);
         if (r != ncclSuccess) {
           (void)ncclGroupEnd();
@@ -953,19 +993,23 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
       for (int32_t j = 0; j < k; ++j) src[j] = ctx->d_gather + size_t(j) * cap * w;
     } else {  // a device repeats: copy the bands device to device
       for (int32_t j = 1; j < k; ++j) VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], ctx->sh[j].ev_stop, 0));
-      for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_hist;
+      for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_ring[slot];
     }
     VRT_HIP(ctx, hipSetDevice(root.device));
+    if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], reuse, 0));
+    uint32_t* out = ctx->d_frames[slot];
     for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
       const int32_t hb = band_rows(h, k, j);
       if (hb > 0)
-        VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(d_out_rgba8) + size_t(j) * row, size_t(k) * row,
-                                      src[j], row, row, size_t(hb), hipMemcpyDeviceToDevice, root.part[0]));
+        VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + size_t(j) * row, size_t(k) * row, src[j], row,
+                                      row, size_t(hb), hipMemcpyDeviceToDevice, root.part[0]));
     }
+    VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.part[0]));
+    VRT_HIP(ctx, hipStreamWaitEvent(cs, ctx->ev_gathered, 0));
+    ctx->gather_pending = !ctx->distinct;  // the next frame's other devices wait for the copies
+    *d_frame = out;
   }
-  VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.part[0]));
-  VRT_HIP(ctx, hipStreamWaitEvent(cs, ctx->ev_gathered, 0));
-  ctx->gather_pending = true;
+  ctx->fk++;
   if (stats && (st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
   ctx->err.clear();
   return VRT_OK;
@@ -982,7 +1026,7 @@ int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size) {
 int vrt_history_reset(vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
   // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer)
-  for (Shard& s : ctx->sh) std::swap(s.d_hist, s.d_raw);
+  for (Shard& s : ctx->sh) std::swap(s.d_ring[(ctx->fk + kRing - 1) % kRing], s.d_raw);
   ctx->err.clear();
   return VRT_OK;
 }
@@ -1011,7 +1055,7 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* 
     s.out_pixels = pixels;
   }
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
-  if ((st = launch_frame(ctx, cam, p, 1.0f, false, out_hit != nullptr, counting)) != VRT_OK) return st;
+  if ((st = launch_frame(ctx, cam, p, 1.0f, false, out_hit != nullptr, counting, stats != nullptr)) != VRT_OK) return st;
   std::vector<const void*> bands, hbands;
   for (Shard& s : ctx->sh) {
     bands.push_back(s.d_out);

@@ -121,7 +121,7 @@ def hipcopy(dst: np.ndarray, ptr: int):
     __cuda_array_interface__."""
 
     class View:
-        __cuda_array_interface__ = {"shape": dst.shape, "typestr": "|u1", "data": (ptr, True),
+        __cuda_array_interface__ = {"shape": dst.shape, "typestr": "|u1", "data": (ptr, False),
                                     "version": 3}
 
     torch.cuda.synchronize()

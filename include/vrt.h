@@ -238,8 +238,10 @@ int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt
  * t = 0), NEAREST + REPEAT; material slot (texX, texY) covers columns [texX*ts, (texX+1)*ts) and
  * rows [size-(texY+1)*ts, size-texY*ts). atlas_size must be a power of two. The context keeps
  * the atlas: it is uploaded by vrt_upload_atlas, or by any render call whose
- * vrt_params.atlas_rgba is non-NULL and differs (pointer or size) from the last upload
- * (a synchronous copy). Replaces the Atlas texture of main.cpp:187-193. */
+ * vrt_params.atlas_rgba is non-NULL and whose bytes (or size) differ from the last upload
+ * (compared on the host each call; a synchronous copy when they differ; ABI v8: by content, not
+ * by pointer identity). atlas_rgba = NULL renders with the context's atlas. Replaces the Atlas
+ * texture of main.cpp:187-193. */
 int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size);
 
 /* ---- temporal filter + RGB8 framebuffer ------------------------------ */

@@ -200,6 +200,13 @@ def test_atlas_upload_and_switching(renderer):
     g0, _, _ = renderer.render(cam, vrt.default_params(4, 2))
     r0, _, _ = oracle.render(cam, vox, 16, vrt.default_params(4, 2), threads=THREADS)
     assert np.abs(np.clip(g0, 0, 1) - np.clip(r0, 0, 1)).max() <= COLOR_TOL
+    # the same host buffer with new bytes is re-uploaded (content, not pointer identity)
+    buf = a1.copy()
+    p3 = vrt.textured_params(vrt.default_params(4, 2), buf)
+    renderer.render(cam, p3)
+    buf[...] = a2
+    g3, _, _ = renderer.render(cam, p3)
+    assert np.abs(np.clip(g3, 0, 1) - np.clip(ref2, 0, 1)).max() <= COLOR_TOL
 
 
 def test_errors_are_reported(renderer):

@@ -89,7 +89,8 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
-  const uint8_t* atlas_src = nullptr;   // host buffer of the last atlas upload
+  std::vector<uint8_t> atlas_host;      // bytes of the last atlas upload (a params pointer is
+                                        // re-uploaded when its bytes differ, not by identity)
   int32_t hist_w = 0, hist_h = 0;       // image size of the resident whole-frame history
   uint64_t fk = 0;                      // frames rendered into the resident history
   uint32_t* d_gather = nullptr;         // first device: k x band_cap x width words (ncclGather)
@@ -210,7 +211,7 @@ int upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t size) {
     VRT_HIP(ctx, hipMemcpy(s.d_atlas, rgba, bytes, hipMemcpyHostToDevice));
     s.atlas_size = size;
   }
-  ctx->atlas_src = rgba;
+  ctx->atlas_host.assign(rgba, rgba + bytes);
   return VRT_OK;
 }
 
@@ -220,7 +221,9 @@ int check_render_args(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p) 
   if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
     return fail(ctx, VRT_ERR_INVALID, "bad image size");
   if (!p->color_only) {  // textured mode: the context's atlas (uploaded here when it changes)
-    if (p->atlas_rgba && (p->atlas_rgba != ctx->atlas_src || p->atlas_size != ctx->sh[0].atlas_size)) {
+    const size_t abytes = p->atlas_size > 0 ? size_t(p->atlas_size) * size_t(p->atlas_size) * 4 : 0;
+    if (p->atlas_rgba && (p->atlas_size != ctx->sh[0].atlas_size || abytes != ctx->atlas_host.size() ||
+                          std::memcmp(p->atlas_rgba, ctx->atlas_host.data(), abytes) != 0)) {
       const int st = upload_atlas(ctx, p->atlas_rgba, p->atlas_size);
       if (st != VRT_OK) return st;
     }

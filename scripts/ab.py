@@ -51,7 +51,7 @@ def main():
     for name, path in libs.items():
         L = load(path)
         h = C.c_void_p()
-        assert L.vrt_create(0, C.byref(h)) == 0
+        assert L.vrt_create(1, C.byref(h)) == 0
         handles[name] = (L, h)
     res = {}
     for cfg in args.configs.split(","):
@@ -65,7 +65,8 @@ def main():
         imgs = {}
         times = {k: [] for k in handles}
         stream = torch.cuda.current_stream()
-        outs = {k: torch.empty((hgt, w, 4), dtype=torch.float32, device="cuda") for k in handles}
+        # the bench's output: RGB8 store + temporal filter (alpha 1), in place, one launch
+        outs = {k: torch.zeros((hgt, w, 4), dtype=torch.uint8, device="cuda") for k in handles}
         for r in range(args.rounds + 2):
             for name, (L, h) in handles.items():
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -73,9 +74,9 @@ def main():
                 nb = 1 if r == 0 else args.batch
                 e0.record(stream)
                 for _ in range(nb):
-                    rc = L.vrt_render_rows_async(h, C.byref(cam), C.byref(p), 0, hgt, 1,
-                                                 outs[name].data_ptr(), None, None,
-                                                 stream.cuda_stream)
+                    d = outs[name].data_ptr()
+                    rc = L.vrt_render_temporal_rows_async(h, C.byref(cam), C.byref(p), 1.0, 0, hgt, 1,
+                                                          d, d, None, None, None, stream.cuda_stream)
                     assert rc == 0
                 e1.record(stream)
                 torch.cuda.synchronize()
@@ -86,7 +87,7 @@ def main():
         base = imgs["base"]
         for name in handles:
             t = np.array(times[name])
-            same = bool(np.array_equal(imgs[name].view(np.uint32), base.view(np.uint32)))
+            same = bool(np.array_equal(imgs[name], base))
             res[f"{name}/{cfg}"] = dict(median_ms=float(np.median(t)), min_ms=float(t.min()),
                                         identical_to_base=same)
             print(f"{cfg} {name:>12s} median {np.median(t):.4f} ms  min {t.min():.4f} ms  "

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Build ablation variants of the kernel for scripts/ab.py (timing breakdown only; they render
+WRONG images and are never the product library): each variant is the product source with one
+text substitution, compiled into build/variants/libvrt_<name>.so.
+Usage: python scripts/ablate.py [names...]   (default: all)"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "voxelraytracer_amd", "csrc")
+K = "vrt_render.hip"
+
+ABLATIONS = {
+    # the sky colour: no pow / normalize, a constant sky
+    "nosky": ("__device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3& color) {\n",
+              "__device__ __forceinline__ void apply_sky_color(const Ctx& c, const Ray& ray, f3& color) {\n"
+              "  color = mk(0.1f, 0.2f, 0.3f); return;\n"),
+    # the lit brightness of hits: no pow / reflect
+    "nolit": ("__device__ __forceinline__ float lit_brightness(const Hit& h, const f3 sun_dir, const f3 ray_dir) {\n",
+              "__device__ __forceinline__ float lit_brightness(const Hit& h, const f3 sun_dir, const f3 ray_dir) {\n"
+              "  return 0.7f;\n"),
+    # the temporal epilogue: store the quantised colour only (no history read, no blend)
+    "noepi": ("    a.cur[o] = temporal_blend(rw, a.prev[o], a.alpha);\n", "    a.cur[o] = rw;\n"),
+    # certified shadow walks of certified hits: always lit
+    "noshadow": ("    const CertResult s = cert_walk<true>(c, hh.point, S, c.sun_rcp, c.max_len - hh.len, ax, ay, az,\n"
+                 "                                         h.eu, ed, hh.len, 0u);\n",
+                 "    CertResult s; s.res = CERT_MISS;\n"),
+    # the primary certified walk: every pixel a certified miss (sky), no exact path
+    "nowalk": ("  CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f,\n"
+               "                                  mk(0.0f, 0.0f, 0.0f), 0.0f, 0u);\n",
+               "  CertResult h; h.res = CERT_MISS;\n"),
+    # the exact path of unsure and glass pixels: skipped (their colour stays black)
+    "noexact": ("    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, color);\n",
+                "    const bool need_exact = CERT < 2 || (!cert_pixel(c, ray, color) && ray.len < 0.0f);\n"),
+    # the bounce stacks of glass pixels: no secondary rays
+    "nostack": ("  if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)\n",
+                "  if (h0.found && mat_id(h0.voxel) == 2 && ray.len < 0.0f) {\n"),
+}
+
+
+def build(name):
+    old, new = ABLATIONS[name]
+    out = os.path.join(ROOT, "build", "ablate", name)
+    os.makedirs(out, exist_ok=True)
+    for f in os.listdir(SRC):
+        shutil.copy(os.path.join(SRC, f), out)
+    text = open(os.path.join(SRC, K)).read()
+    assert text.count(old) == 1, f"{name}: anchor not found once"
+    open(os.path.join(out, K), "w").write(text.replace(old, new))
+    srcs = [os.path.join(out, f) for f in ("vrt_render.hip", "vrt_context.cpp", "vrt_host.cpp")]
+    os.makedirs(os.path.join(ROOT, "build", "variants"), exist_ok=True)
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"),
+           "-I" + out, "-DVRT_DIAGNOSTIC_BUILD", "-shared", "-o",
+           os.path.join(ROOT, "build", "variants", f"libvrt_{name}.so")] + srcs + \
+          ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.check_call(cmd)
+    print("built", name)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(ABLATIONS):
+        build(n)

@@ -43,10 +43,21 @@ struct KArgs {
   uint32_t tiles_x, tiles, ord_r, ord_w;
 };
 
-constexpr int kWgWaves = 4;                 // waves per workgroup, each an 8x8 pixel tile
+// Waves per workgroup, each rendering an 8x8 pixel tile. Two (a 16x8 tile): a finished
+// workgroup frees its slots two waves at a time, so the dispatcher refills them sooner than with
+// four-wave 16x16 workgroups (C3 -4.4 %, C2 -2.8 %, C4 -8.1 % per frame; one wave per workgroup:
+// C3 -1.7 %, profiles/r02_s06). Images are identical at 1, 2 and 4 (A/B builds only: make variant).
+#if defined(VRT_WG_WAVES) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_WG_WAVES is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_WG_WAVES
+#define VRT_WG_WAVES 2
+#endif
+constexpr int kWgWaves = VRT_WG_WAVES;
+static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "1, 2 or 4 waves per workgroup");
 constexpr int kWgThreads = 64 * kWgWaves;
-constexpr int kTileW = 16;                  // a workgroup renders a 16x16 pixel tile
-constexpr int kTileH = 16;
+constexpr int kTileW = kWgWaves >= 2 ? 16 : 8;  // a workgroup's pixel tile: 16x16, 16x8 or 8x8
+constexpr int kTileH = kWgWaves == 4 ? 16 : 8;
 constexpr int kMaxStack = 17;               // bounce-stack entries: max_reflections + max_transparencies + 1
 constexpr int kCntReplicas = 256;           // counter replicas (per-wave atomics spread over them)
 constexpr uint32_t kOrdHdr = 0;             // tile-order buffer: per-tile wave counters, then two flag sets

@@ -1,7 +1,7 @@
-// vrt_render.hip — gfx950 HIP kernel for the per-pixel program of res/shaders/voxel.glsl and
-// the C-ABI context around it (include/vrt.h).
+// vrt_render.hip — gfx950 HIP kernels for the per-pixel program of res/shaders/voxel.glsl; the
+// C-ABI context around them is vrt_context.cpp (include/vrt.h).
 //
-// One work-item per pixel; a 256-thread workgroup covers a 16x16 pixel tile and each wave64 an
+// One work-item per pixel; a 128-thread workgroup covers a 16x8 pixel tile and each wave64 an
 // 8x8 sub-tile, so the 64 rays of a wave start coherent. Every float operation of the DDA is
 // replayed in the reference's order with -ffp-contract=off and correctly rounded div/sqrt, which
 // makes hit records bit-exact against the CPU oracle (DESIGN.md "Numerics").
@@ -1542,8 +1542,9 @@ __device__ __forceinline__ uint32_t lane_id() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
-// Four waves per workgroup (kWgWaves), each rendering an 8x8 pixel tile: a workgroup covers
-// 16x16 pixels (wave = threadIdx.x >> 6, uniform). Tiles are dispatched in row order (an XCD-aware order that
+// kWgWaves waves per workgroup (vrt_internal.h), each rendering an 8x8 pixel tile: a workgroup
+// covers kTileW x kTileH pixels (wave = threadIdx.x >> 6, uniform). Tiles are dispatched in row
+// order (an XCD-aware order that
 // keeps runs of tiles on one XCD's L2 was neutral or worse, profiles/r01_v29_ab_xcd_tile_swizzle_negative.log).
 
 // Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, the glass pixels'
@@ -1609,6 +1610,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
 // Waves per SIMD the register budget is sized for: 7 -> 72 VGPRs. With certified walks inside the
 // bounce stacks, 64 VGPRs (8 waves) spill in the glass waves that bound a frame: 7 is 2-4 % faster
 // on C1-C4 (profiles/r01_v56_ab_occupancy.log), 6 (80 VGPRs) no better.
+#if defined(VRT_MIN_WAVES) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_MIN_WAVES is an A/B knob of make variant builds"
+#endif
 #ifndef VRT_MIN_WAVES  // occupancy A/B builds (make variant); images identical at any value
 #define VRT_MIN_WAVES 7
 #endif

@@ -28,11 +28,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4). A part
-# stream that shares the null stream's queue loses its overlap (measured: C3 0.21 -> 0.35 ms per
-# frame, scripts/streams_exp.py with STREAMS_FRESH=1); with the RCCL and assembly streams of the
-# multi-GPU path there are more streams than 4 queues. Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4). One rank
+# does not depend on it (C3 0.0667 ms/frame at 4 queues, 0.0669 at 16, profiles/r02_s08); with
+# the RCCL and assembly streams of the multi-rank path there are more streams than 4 queues, so
+# ranks of a multi-GPU run raise it (before HIP initialises).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 CONFIGS = {
     # name: (scene, N, W, H, R, T, description)

@@ -287,7 +287,7 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* para
  * device pointer (first GPU) to the new filtered frame, W*H RGBA8 words, row 0 = bottom, owned by
  * the context; hip_stream is made to wait for it, so work the caller enqueues there afterwards
  * (e.g. the texture upload / blit of main.cpp:379-385) sees the frame. The frame stays valid until
- * the third later call, which overwrites it only after the work the caller had enqueued on
+ * the fourth later call, which overwrites it only after the work the caller had enqueued on
  * hip_stream before the next call. One device: the frame is rendered straight into that buffer
  * (no copy) and consecutive frames overlap on the GPU; several devices: the bands are gathered to
  * the first one over xGMI by ncclGather (rccl.h) and placed into their rows by strided copies.

@@ -40,16 +40,27 @@ ABLATIONS = {
 }
 
 
+# context experiments (timing only; unsafe orderings): file, anchor, replacement
+CONTEXT = {
+    # device-output frames: no wait for the caller's consumption of a reused ring slot
+    "noconsumed": ("vrt_context.cpp", "  hipEvent_t reuse = ctx->consumed_valid[slot] ? ctx->ev_consumed[slot] : nullptr;\n",
+                   "  hipEvent_t reuse = nullptr;\n"),
+}
+
+
 def build(name):
-    old, new = ABLATIONS[name]
+    if name in CONTEXT:
+        f, old, new = CONTEXT[name]
+    else:
+        f, (old, new) = K, ABLATIONS[name]
     out = os.path.join(ROOT, "build", "ablate", name)
     os.makedirs(out, exist_ok=True)
-    for f in os.listdir(SRC):
-        shutil.copy(os.path.join(SRC, f), out)
-    text = open(os.path.join(SRC, K)).read()
+    for src in os.listdir(SRC):
+        shutil.copy(os.path.join(SRC, src), out)
+    text = open(os.path.join(SRC, f)).read()
     assert text.count(old) == 1, f"{name}: anchor not found once"
-    open(os.path.join(out, K), "w").write(text.replace(old, new))
-    srcs = [os.path.join(out, f) for f in ("vrt_render.hip", "vrt_context.cpp", "vrt_host.cpp")]
+    open(os.path.join(out, f), "w").write(text.replace(old, new))
+    srcs = [os.path.join(out, x) for x in ("vrt_render.hip", "vrt_context.cpp", "vrt_host.cpp")]
     os.makedirs(os.path.join(ROOT, "build", "variants"), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include"),

@@ -1,0 +1,30 @@
+"""GPU time of each of the first frames of a fresh process (C3, bench's FrameTiler), in groups."""
+import os, sys
+import numpy as np
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import voxelraytracer_amd as vrt
+from voxelraytracer_amd.tiles import FrameTiler, row_pitch
+dev = torch.device("cuda", 0)
+torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+ren = vrt.Renderer(0)
+ren.upload_volume(vrt.build_scene("refraction", 128), 128)
+cam = vrt.make_camera(1920, 1080)
+p = vrt.default_params(4, 4)
+def band(row0, rows, step, out, prev):
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    ren.render_temporal_rows_async(cam, p, 1.0, row0, rows, step, prev.data_ptr(), out.data_ptr(), 0, 0, 0, sp, pitch=row_pitch(out))
+t = FrameTiler(1920, 1080, band, dev, dtype=torch.uint8, parts=2)
+s = torch.cuda.current_stream(dev)
+ms = []
+for g in range(30):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(10):
+        t.frame()
+    t.finish()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms.append(e0.elapsed_time(e1) / 10)
+print("ms/frame per group of 10 frames:", " ".join(f"{x:.4f}" for x in ms))

@@ -90,9 +90,9 @@ def test_device_list_splits_frames_into_bands(built, devs):
 def test_frame_device_output(built, devs):
     """vrt_render_frame_device hands out the frame on the first device (k1: the ring buffer it was
     rendered into; k2: the assembled bands), identical to the synchronous frames; a frame stays
-    valid for two more frames."""
+    valid for three more frames (ring of four)."""
     scene, n, w, h, R, T = "refraction", 128, 320, 181, 4, 4
-    alphas = [1.0, 0.5, 0.5, 0.5, 0.7]
+    alphas = [1.0, 0.5, 0.5, 0.5, 0.7, 0.5, 0.4, 0.5]
     ref = sequence(0, scene, n, w, h, R, T, alphas)
     with vrt.Renderer(devs) as r:
         r.upload_volume(vrt.build_scene(scene, n), n)
@@ -106,14 +106,14 @@ def test_frame_device_output(built, devs):
                                            s.cuda_stream, timing=(i == 1))
             ms = ms or t
             ptrs.append(ptr)
-            if i >= 2:   # frame i-2 is still valid after frame i
+            if i >= 3:   # frame i-3 is still valid after frame i
                 torch.cuda.current_stream().wait_stream(s)
-                for j in (i - 2, i):
+                for j in (i - 3, i):
                     got = np.empty((h, w, 4), np.uint8)
                     hipcopy(got, ptrs[j])
                     assert np.array_equal(got, ref[j]), f"frame {j} read after frame {i}"
         assert ms is not None and ms > 0
-        assert len(set(ptrs[:3])) == 3 and ptrs[3] == ptrs[0]
+        assert len(set(ptrs[:4])) == 4 and ptrs[4] == ptrs[0]
 
 
 def hipcopy(dst: np.ndarray, ptr: int):

@@ -331,7 +331,7 @@ class Renderer:
                             timing: bool = False):
         """vrt_render_frame_device: the next filtered frame for display, on the first device,
         ordered on `stream`. Returns (device pointer of the W*H RGBA8 frame, owned by the context
-        and valid until the third later call; kernel_ms or None). timing=True waits for the frame."""
+        and valid until the fourth later call; kernel_ms or None). timing=True waits for the frame."""
         st = abi.Stats() if timing else None
         ptr = C.c_void_p()
         self._check(self._lib.vrt_render_frame_device(self._h, C.byref(cam), C.byref(params), alpha,

@@ -32,7 +32,7 @@ constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 4096 x 4096 pixels
 // Filtered frames rotate through kRing buffers: frame f reads ring[(f-1) % kRing] (the temporal
 // history) and writes ring[f % kRing]. A device-output frame (vrt_render_frame_device) is handed
 // to the caller as its ring buffer and stays valid for two more frames with no copy.
-constexpr int kRing = 3;
+constexpr int kRing = 4;
 
 struct OrderSlot {
   int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
@@ -65,7 +65,7 @@ struct Shard {
   hipEvent_t ev_kbeg[kParts] = {nullptr, nullptr}, ev_kend[kParts] = {nullptr, nullptr};
   bool timed[kParts] = {false, false};               // parts launched by the last frame
   // this device's row band of the whole-frame buffers (band_cap rows x width)
-  uint32_t* d_ring[kRing] = {nullptr, nullptr, nullptr};  // filtered bands (history ring)
+  uint32_t* d_ring[kRing] = {};  // filtered bands (history ring)
   uint32_t* d_raw = nullptr;   // quantised ray-trace band (the rayTrace FBO; key F)
   size_t hist_pixels = 0;
   float4* d_out = nullptr;     // vrt_render's float band
@@ -95,9 +95,11 @@ struct vrt_ctx {
   uint64_t fk = 0;                      // frames rendered into the resident history
   uint32_t* d_gather = nullptr;         // first device: k x band_cap x width words (ncclGather)
   size_t hist_pixels_gather = 0;
-  uint32_t* d_frames[kRing] = {nullptr, nullptr, nullptr};  // first device, k > 1: assembled frames
-  hipEvent_t ev_consumed[kRing] = {nullptr, nullptr, nullptr};  // caller stream: ring slot consumed
-  bool consumed_valid[kRing] = {false, false, false};
+  uint32_t* d_frames[kRing] = {};  // first device, k > 1: assembled frames
+  // caller stream, device-output frames: E_f = ev_consumed[f % kRing], recorded at call f, marks
+  // the caller's work enqueued before call f (its consumption of frames <= f - 1)
+  hipEvent_t ev_consumed[kRing] = {};
+  bool consumed_valid[kRing] = {};
   hipEvent_t ev_gathered = nullptr;     // first device: the last device-output frame is assembled
   bool gather_pending = false;
   std::string err;
@@ -156,7 +158,7 @@ void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
   for (void* p : {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats, (void*)s.d_cnt,
                   (void*)s.d_cnt_rep, (void*)s.d_ring[0], (void*)s.d_ring[1], (void*)s.d_ring[2],
-                  (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
+                  (void*)s.d_ring[3], (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
                   (void*)s.d_atlas, (void*)s.d_order_pool})
     if (p) (void)hipFree(p);
   for (auto& o : s.order)
@@ -453,16 +455,17 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     VRT_HIP(ctx, hipDeviceSynchronize());  // nothing may still read the old buffers
     if (pixels > s.hist_pixels) {
-      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_raw}) {
+      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_ring[3], &s.d_raw}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
       }
       s.hist_pixels = 0;
-      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_raw})
+      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_ring[3], &s.d_raw})
         if (hipMalloc(b, pixels * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
       s.hist_pixels = pixels;
     }
-    for (uint32_t* b : {s.d_ring[0], s.d_ring[1], s.d_ring[2], s.d_raw}) VRT_HIP(ctx, hipMemset(b, 0, pixels * 4));
+    for (uint32_t* b : {s.d_ring[0], s.d_ring[1], s.d_ring[2], s.d_ring[3], s.d_raw})
+      VRT_HIP(ctx, hipMemset(b, 0, pixels * 4));
   }
   if (k > 1) {
     VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
@@ -621,7 +624,8 @@ int create(const std::vector<int>& devs, vrt_ctx** out) {
       hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_consumed[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_consumed[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_consumed[2], hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_consumed[2], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_consumed[3], hipEventDisableTiming) != hipSuccess) {
     vrt_destroy(c);
     return VRT_ERR_DEVICE;
   }
@@ -948,12 +952,15 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   const uint64_t f = ctx->fk;
   const int slot = int(f % kRing), prev_slot = int((f + kRing - 1) % kRing);
   VRT_HIP(ctx, hipSetDevice(root.device));
-  // whatever the caller enqueued on its stream so far consumed the previous frame's slot
-  if (f > 0) {
-    VRT_HIP(ctx, hipEventRecord(ctx->ev_consumed[prev_slot], cs));
-    ctx->consumed_valid[prev_slot] = true;
-  }
-  hipEvent_t reuse = ctx->consumed_valid[slot] ? ctx->ev_consumed[slot] : nullptr;
+  // E_f: whatever the caller enqueued on its stream so far (its consumption of frames <= f - 1)
+  VRT_HIP(ctx, hipEventRecord(ctx->ev_consumed[slot], cs));
+  ctx->consumed_valid[slot] = true;
+  // Frame f overwrites frame f - kRing's buffer, which must follow E_{f-kRing+1}. Waiting every
+  // kRing - 1 frames on E_{f-1} covers it by stream order: the last such wait before frame f was at
+  // a frame g >= f - kRing + 2 on E_{g-1}, g - 1 >= f - kRing + 1 (one marker per kRing - 1 frames
+  // per part stream instead of one per frame: -8 % per frame at C3, profiles/r02_s08)
+  hipEvent_t reuse = nullptr;
+  if (f >= 2 && f % (kRing - 1) == 0 && ctx->consumed_valid[prev_slot]) reuse = ctx->ev_consumed[prev_slot];
   if (k == 1) {
     // one device: the frame is rendered straight into the ring slot handed to the caller, as two
     // pipelined parts — no part waits for the other (disjoint rows), so consecutive frames overlap

@@ -46,20 +46,38 @@ CONTEXT = {
     "noconsumed": ("vrt_context.cpp", "  hipEvent_t reuse = ctx->consumed_valid[slot] ? ctx->ev_consumed[slot] : nullptr;\n",
                    "  hipEvent_t reuse = nullptr;\n"),
 }
+# multi-file experiments: name -> [(file, anchor, replacement), ...]
+MULTI = {
+    # heavy tiles = tiles with any exact-path pixel (not only bounce stacks), tile order on for
+    # every certified-pixel launch (also without glass)
+    "heavyexact": [
+        ("vrt_render.hip", "      stack = exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(",
+         "      stack = true; exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>("),
+        ("vrt_context.cpp", "      !s.has_glass)", "      false)"),
+    ],
+    # the same marking, tile order still only for volumes with glass
+    "heavyexact2": [
+        ("vrt_render.hip", "      stack = exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(",
+         "      stack = true; exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>("),
+    ],
+}
 
 
 def build(name):
-    if name in CONTEXT:
-        f, old, new = CONTEXT[name]
+    if name in MULTI:
+        subs = MULTI[name]
+    elif name in CONTEXT:
+        subs = [CONTEXT[name]]
     else:
-        f, (old, new) = K, ABLATIONS[name]
+        subs = [(K,) + ABLATIONS[name]]
     out = os.path.join(ROOT, "build", "ablate", name)
     os.makedirs(out, exist_ok=True)
     for src in os.listdir(SRC):
         shutil.copy(os.path.join(SRC, src), out)
-    text = open(os.path.join(SRC, f)).read()
-    assert text.count(old) == 1, f"{name}: anchor not found once"
-    open(os.path.join(out, f), "w").write(text.replace(old, new))
+    for f, old, new in subs:
+        text = open(os.path.join(out, f)).read()
+        assert text.count(old) == 1, f"{name}: anchor not found once in {f}"
+        open(os.path.join(out, f), "w").write(text.replace(old, new))
     srcs = [os.path.join(out, x) for x in ("vrt_render.hip", "vrt_context.cpp", "vrt_host.cpp")]
     os.makedirs(os.path.join(ROOT, "build", "variants"), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",

@@ -1547,9 +1547,10 @@ __device__ __forceinline__ uint32_t lane_id() {
 // order (an XCD-aware order that
 // keeps runs of tiles on one XCD's L2 was neutral or worse, profiles/r01_v29_ab_xcd_tile_swizzle_negative.log).
 
-// Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, the glass pixels'
-// bounce stacks; dispatched in row order, those start wherever the glass is in the image. Each
-// stats-free launch therefore records which of its tiles ran a bounce stack, and the next launch
+// Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, those with exact-path
+// pixels (glass bounce stacks, walks the certified walk could not settle); dispatched in row
+// order, they start wherever they are in the image. Each stats-free launch therefore records which
+// of its tiles had such a pixel (until r02: only bounce stacks; C3 -2 %, profiles/r02_s09), and the next launch
 // of the same band (same stream) dispatches those first. The order buffer of a band holds a
 // per-tile wave counter and two per-tile flag sets: launch e reads set e % 2 (complete: written by
 // launch e - 1) and writes set (e + 1) % 2. The grid is two passes over the tiles in row order:
@@ -1779,7 +1780,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const int px = pixel_x(tx, wave, lane_id());
   const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
-  bool stack = false;  // this lane ran a bounce stack (tile order)
+  bool heavy = false;  // this lane took the exact path (tile order: the tile runs long next frame)
 
   Counters k;
 #pragma unroll
@@ -1814,8 +1815,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #endif
     if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
-      stack = exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
-                                                            hit_len);
+      heavy = true;
+      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2));
@@ -1842,8 +1843,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
 #endif
   if constexpr (!STATS) {
     if (a.order) {
-      const bool heavy = __ballot(stack) != 0ull;
-      if (lane_id() == 0) order_record(a, tile, heavy);
+      const bool heavy_wave = __ballot(heavy) != 0ull;
+      if (lane_id() == 0) order_record(a, tile, heavy_wave);
     }
   }
   if (STATS && counters) {

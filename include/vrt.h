@@ -195,7 +195,9 @@ int vrt_certified(const vrt_ctx* ctx);
  * tile is rendered exactly once in any case: images are identical with and without it.
  * ABI v8: the state is a pool allocated by vrt_create (8 slots of bands up to 65536 tiles, i.e.
  * 4096 x 4096 pixels; larger bands use dispatch order); reusing a slot on another stream waits
- * for its last launch on the device (hipStreamWaitEvent), never on the host. */
+ * for its last launch on the device (hipStreamWaitEvent), not on the host — unless the caller has
+ * destroyed that stream, when the device is synchronised once. Tiles with any pixel that took the
+ * exact path (glass bounce stacks, near-edge walks) count as heavy (ABI v8). */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3

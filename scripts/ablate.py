@@ -35,6 +35,12 @@ ABLATIONS = {
     "noexact": ("    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, color);\n",
                 "    const bool need_exact = CERT < 2 || (!cert_pixel(c, ray, color) && ray.len < 0.0f);\n"),
     # the bounce stacks of glass pixels: no secondary rays
+    # shadow starts the certified walk cannot place: assume lit instead of the exact path
+    "nostartunsure": ("      CERT_DIAG(6);\n      return false;\n",
+                      "      CERT_DIAG(6);\n      apply_hit_color<false>(c, hh, ray.energy, lit, color);\n      return true;\n"),
+    # primary walks that end unsure: treat as a miss (sky) instead of the exact path
+    "noprimunsure": ("  if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }\n",
+                     "  if (h.res == CERT_UNSURE) { CERT_DIAG(1); h.res = CERT_MISS; }\n"),
     "nostack": ("  if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)\n",
                 "  if (h0.found && mat_id(h0.voxel) == 2 && ray.len < 0.0f) {\n"),
 }

@@ -73,3 +73,21 @@ def test_ema_sequence_converges(built):
         _, hist = oracle.temporal(f, hist, 0.5)
         seq.append(int(hist[0, 0]))
     assert seq[0] == 100 and seq == sorted(seq) and seq[-1] in (199, 200)
+
+
+def test_alpha_one_blend_is_identity(built):
+    """temporal.glsl:18 at u_Alpha = 1 on RGB8 texels: 1 * b/255 + 0 * old/255 stores b back for
+    every byte b and every history byte (the kernel then skips the history read, vrt_render.hip
+    store_pixel)."""
+    b = np.arange(256, dtype=np.uint8)
+    raw = np.zeros((256, 256, 4), np.uint8)
+    raw[..., 0] = b[:, None]
+    raw[..., 1] = b[None, :]
+    raw[..., 2] = b[::-1, None]
+    raw[..., 3] = 255
+    prev = np.empty_like(raw)
+    prev[..., 0] = b[None, :]
+    prev[..., 1] = b[:, None]
+    prev[..., 2] = b[None, ::-1]
+    prev[..., 3] = 255
+    assert np.array_equal(oracle.temporal_from_raw(raw, prev, 1.0), raw)

@@ -261,6 +261,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.fn = float(s.n);
   a.width = cam->width;
   a.height = cam->height;
+  a.rcp_w = 1.0f / float(cam->width);
+  a.rcp_h = 1.0f / float(cam->height);
   a.row0 = row0;
   a.rows = rows;
   a.row_step = row_step;

@@ -14,6 +14,7 @@ namespace vrt {
 // Per-launch kernel arguments (by value: one kernarg segment per launch).
 struct KArgs {
   float inv_pv[16];
+  float rcp_w, rcp_h;  // RN(1 / width), RN(1 / height) (host IEEE division): the NDC's divisions
   float sun[3];
   float sky_sy;      // max(u_SunDir.y, 0): the skybox's sun height factor (voxel.glsl:391), uniform
   float sun_n[3];    // normalize(u_SunDir), GLSL normalize semantics (host: same IEEE ops)

@@ -1640,9 +1640,27 @@ __device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t*
 
 // The primary ray of pixel (px, frame row py): vertex stage (voxel.glsl:467-472) evaluated at the
 // pixel centre, then stack[0] of main (:430)
+// a / d correctly rounded for the vertex stage's divisions: Markstein's division (div_rn) from
+// y = RN(1/d) when every operand is far from overflow and underflow (|a|, |d| in [2^-60, 2^60]),
+// else the IEEE division; bit-identical either way. Zero numerators take the IEEE division: div_rn
+// returns +0 for a = -0 (the residual's zeros cancel to +0), IEEE -0 / d keeps the sign, and a
+// -0 component of the direction decides RandomizeDirection's hashes.
+__device__ __forceinline__ bool markstein_safe(float x) {
+  const float m = __builtin_fabsf(x);
+  return m >= 0x1p-60f && m <= 0x1p60f;
+}
+__device__ __forceinline__ f3 div3_rn(float x, float y, float z, float d) {
+  if (markstein_safe(x) && markstein_safe(y) && markstein_safe(z) && markstein_safe(d)) {
+    const float r = 1.0f / d;
+    return mk(div_rn(x, d, r), div_rn(y, d, r), div_rn(z, d, r));
+  }
+  return mk(x / d, y / d, z / d);
+}
+
 __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px, int py) {
-  const float ndx = (2.0f * (float(px) + 0.5f)) / float(a.width) - 1.0f;
-  const float ndy = (2.0f * (float(py) + 0.5f)) / float(a.height) - 1.0f;
+  // (2 (p + 0.5)) / W with RN(1/W) from the host: the numerator is in (0, 2W), W <= 32768
+  const float ndx = div_rn(2.0f * (float(px) + 0.5f), float(a.width), a.rcp_w) - 1.0f;
+  const float ndy = div_rn(2.0f * (float(py) + 0.5f), float(a.height), a.rcp_h) - 1.0f;
   float n4[4], f4[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1650,8 +1668,8 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
     n4[i] = (base + a.inv_pv[2 * 4 + i] * -1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
     f4[i] = (base + a.inv_pv[2 * 4 + i] * 1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
   }
-  const f3 vnear = mk(n4[0] / n4[3], n4[1] / n4[3], n4[2] / n4[3]);
-  const f3 vdir = mk(f4[0] / f4[3], f4[1] / f4[3], f4[2] / f4[3]) - vnear;
+  const f3 vnear = div3_rn(n4[0], n4[1], n4[2], n4[3]);
+  const f3 vdir = div3_rn(f4[0], f4[1], f4[2], f4[3]) - vnear;
   Ray ray;
   ray.pos = mk(vnear.x + c.fn * 0.5f, vnear.y + c.fn * 0.5f, vnear.z + c.fn * 0.5f);
   ray.dir = randomize(normalize3(vdir), vnear, a.ray_noise, c.time);

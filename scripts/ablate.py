@@ -51,6 +51,8 @@ CONTEXT = {
     # device-output frames: no wait for the caller's consumption of a reused ring slot
     "noconsumed": ("vrt_context.cpp", "  hipEvent_t reuse = ctx->consumed_valid[slot] ? ctx->ev_consumed[slot] : nullptr;\n",
                    "  hipEvent_t reuse = nullptr;\n"),
+    # tile order for every certified-pixel launch (also volumes without glass)
+    "orderall": ("vrt_context.cpp", "      !s.has_glass)", "      false)"),
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {

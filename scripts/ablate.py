@@ -41,6 +41,10 @@ ABLATIONS = {
     # primary walks that end unsure: treat as a miss (sky) instead of the exact path
     "noprimunsure": ("  if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }\n",
                      "  if (h.res == CERT_UNSURE) { CERT_DIAG(1); h.res = CERT_MISS; }\n"),
+    # waves raise their priority when a lane enters the exact path (timing A/B, images unchanged)
+    "exprio2": ("      heavy = true;\n", "      heavy = true;\n      __builtin_amdgcn_s_setprio(2);\n"),
+    "exprio3": ("      heavy = true;\n", "      heavy = true;\n      __builtin_amdgcn_s_setprio(3);\n"),
+    "exprio1": ("      heavy = true;\n", "      heavy = true;\n      __builtin_amdgcn_s_setprio(1);\n"),
     "nostack": ("  if (h0.found && mat_id(h0.voxel) == 2) {  // only glass spawns secondary rays (:440-448)\n",
                 "  if (h0.found && mat_id(h0.voxel) == 2 && ray.len < 0.0f) {\n"),
 }

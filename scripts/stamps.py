@@ -29,7 +29,7 @@ from bench import CONFIGS  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C3")
-    ap.add_argument("--wg-waves", type=int, default=4)
+    ap.add_argument("--wg-waves", type=int, default=2)
     ap.add_argument("--slots", type=int, default=256 * 4 * 6, help="wave slots (CUs*SIMDs*occupancy)")
     ap.add_argument("--save", default="")
     ap.add_argument("--band", default="", help="ROW0,ROWS: also time that band alone (few waves, "

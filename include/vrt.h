@@ -205,6 +205,13 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
                         float randomness, float seed, float* out);
 
+/* Diagnostic (test rehearsal of the multi-GPU path on a one-GPU box): a one-device context takes
+ * the k-device path through RCCL with a one-rank communicator (ncclCommInitAll over its device):
+ * the volume upload goes through ncclBroadcast (in place) and vrt_render_frame_device through
+ * ncclGather of the band into the gather buffer and the strided assembly copy, as with k distinct
+ * GPUs. Call once, right after vrt_create with one device; frames are identical either way. */
+int vrt_debug_collectives(vrt_ctx* ctx);
+
 /* Synchronous whole-frame render (replaces main.cpp:325-361): writes W*H RGBA floats
  * (alpha = 1, voxel.glsl:451) to the HOST buffer out_rgba. out_hit (W*H records) and stats may
  * be NULL. Hit records or counters run the exact-walk instance; otherwise the fast instance on

@@ -10,8 +10,9 @@ alone (vrt_stats.kernel_ms) no longer selects the exact-walk instance, counting 
     hit records;
   - vrt_render_frame_device assembles the same frame on the first device;
   - the C++ host (examples/headless_app.cpp) gets the bench's per-frame GPU time through the ABI.
-The RCCL paths (ncclBroadcast of the volume, ncclGather of the bands) need two distinct GPUs and
-are not exercised on the one-GPU test box."""
+The RCCL paths (ncclBroadcast of the volume, ncclGather of the bands) between distinct GPUs need
+two of them; on the one-GPU test box they run with a one-rank communicator
+(vrt_debug_collectives: the same calls, streams and assembly, no xGMI traffic)."""
 import json
 import os
 import re
@@ -86,15 +87,17 @@ def test_device_list_splits_frames_into_bands(built, devs):
                        {k: v for k, v in sb.items() if k != "kernel_ms"}
 
 
-@pytest.mark.parametrize("devs", [0, [0, 0]], ids=["k1", "k2"])
+@pytest.mark.parametrize("devs", [0, [0, 0], "rccl1"], ids=["k1", "k2", "rccl1"])
 def test_frame_device_output(built, devs):
     """vrt_render_frame_device hands out the frame on the first device (k1: the ring buffer it was
-    rendered into; k2: the assembled bands), identical to the synchronous frames; a frame stays
-    valid for three more frames (ring of four)."""
+    rendered into; k2: the assembled bands; rccl1: one device through ncclBroadcast / ncclGather),
+    identical to the synchronous frames; a frame stays valid for three more frames (ring of four)."""
     scene, n, w, h, R, T = "refraction", 128, 320, 181, 4, 4
     alphas = [1.0, 0.5, 0.5, 0.5, 0.7, 0.5, 0.4, 0.5]
     ref = sequence(0, scene, n, w, h, R, T, alphas)
-    with vrt.Renderer(devs) as r:
+    with vrt.Renderer(0 if devs == "rccl1" else devs) as r:
+        if devs == "rccl1":
+            r.debug_collectives()
         r.upload_volume(vrt.build_scene(scene, n), n)
         cam = vrt.make_camera(w, h)
         s = torch.cuda.Stream()

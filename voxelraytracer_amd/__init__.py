@@ -340,6 +340,11 @@ class Renderer:
                     "vrt_render_frame_device")
         return ptr.value, (float(st.kernel_ms) if st is not None else None)
 
+    def debug_collectives(self):
+        """vrt_debug_collectives: this one-device context takes the multi-GPU path through RCCL
+        (one-rank communicator: ncclBroadcast of the volume, ncclGather of the band)."""
+        self._check(self._lib.vrt_debug_collectives(self._h), "vrt_debug_collectives")
+
     def history_reset(self):
         """Key F (main.cpp:417-421): the last ray-traced frame becomes the temporal history."""
         self._check(self._lib.vrt_history_reset(self._h), "vrt_history_reset")

@@ -85,6 +85,7 @@ struct Shard {
 struct vrt_ctx {
   std::vector<Shard> sh;
   bool distinct = true;                 // devices pairwise distinct: RCCL communicators exist
+  bool coll1 = false;                   // one device through the RCCL path (vrt_debug_collectives)
   std::vector<ncclComm_t> comms;
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
@@ -418,7 +419,7 @@ int volume_finish_all(vrt_ctx* ctx) {
 // ncclBroadcast over xGMI, or device-to-device copies when a device repeats.
 int broadcast_volume(vrt_ctx* ctx) {
   const size_t k = ctx->sh.size();
-  if (k == 1) return VRT_OK;
+  if (k == 1 && !ctx->coll1) return VRT_OK;
   Shard& root = ctx->sh[0];
   const size_t bytes = size_t(root.n) * root.n * root.n;
   if (ctx->distinct) {
@@ -469,7 +470,7 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
     for (uint32_t* b : {s.d_ring[0], s.d_ring[1], s.d_ring[2], s.d_ring[3], s.d_raw})
       VRT_HIP(ctx, hipMemset(b, 0, pixels * 4));
   }
-  if (k > 1) {
+  if (k > 1 || ctx->coll1) {
     VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
     for (uint32_t*& f : ctx->d_frames) {
       if (f) (void)hipFree(f);
@@ -963,7 +964,7 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   // per part stream instead of one per frame: -8 % per frame at C3, profiles/r02_s08)
   hipEvent_t reuse = nullptr;
   if (f >= 2 && f % (kRing - 1) == 0 && ctx->consumed_valid[prev_slot]) reuse = ctx->ev_consumed[prev_slot];
-  if (k == 1) {
+  if (k == 1 && !ctx->coll1) {
     // one device: the frame is rendered straight into the ring slot handed to the caller, as two
     // pipelined parts — no part waits for the other (disjoint rows), so consecutive frames overlap
     // as in the bench's FrameTiler; only the slot's consumption three frames ago is waited for.
@@ -1023,6 +1024,21 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   }
   ctx->fk++;
   if (stats && (st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_debug_collectives(vrt_ctx* ctx) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (ctx->sh.size() != 1 || !ctx->comms.empty())
+    return fail(ctx, VRT_ERR_INVALID, "vrt_debug_collectives: a one-device context without communicators");
+  DeviceGuard guard;
+  int dev = ctx->sh[0].device;
+  ncclComm_t comm = nullptr;
+  VRT_NCCL(ctx, ncclCommInitAll(&comm, 1, &dev));
+  ctx->comms.push_back(comm);
+  ctx->coll1 = true;
+  ctx->hist_w = ctx->hist_h = 0;  // the next frame allocates the assembled-frame ring
   ctx->err.clear();
   return VRT_OK;
 }

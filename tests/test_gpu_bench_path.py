@@ -37,3 +37,21 @@ def test_bench_path_c3_three_frames(built, alpha):
     oc = out["oracle_check"]
     assert oc["frames"] == 3 and oc["ok"] and oc["max_lsb"] <= 1
     assert out["config"]["parallelism"].endswith("2 interleaved row parts on 2 HIP streams")
+
+
+@pytest.mark.parametrize("config", ["C1", "C2", "C4"])
+def test_bench_path_other_configs(built, config):
+    """The same end-to-end check for the other BASELINE GPU configs (full size): C1 (glass cube,
+    exact primary walks: glass-heavy volume), C2 (terrain 128^3), C4 (terrain 512^3 at 3840x2160)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", config, "--steps", "10",
+           "--warmup", "3", "--alpha", "0.5", "--verify-frames", "2", "--cpu-seconds", "0",
+           "--oracle-check"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    v = out["verify"]
+    w, h = out["config"]["width"], out["config"]["height"]
+    assert v["frames"] == 2 and v["elements"] == 2 * w * h * 4
+    assert v["verified"] and v["mismatched_elements"] == 0 and out["verified"]
+    oc = out["oracle_check"]
+    assert oc["frames"] == 2 and oc["ok"] and oc["max_lsb"] <= 1

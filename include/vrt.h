@@ -186,18 +186,18 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode);
 int vrt_certified(const vrt_ctx* ctx);
 
 /* ABI v7: heavy-first tile order for stats-free colour-only launches with certified pixels
- * (vrt_certified() == 1; DESIGN.md §6 "Tile order"): on = 1 (default), off = 0. Each launch
- * records which of its 16x16 tiles ran a glass bounce stack; the next launch of the same band
- * (width, rows, row0, row_step) on the same stream dispatches those tiles first, so the frame's
- * longest waves start first. Device state per band and stream: 3 x tiles words, up to 8 bands x
- * streams, allocated and zeroed on the launch stream at first use (recycling one synchronises the
- * device). Launches on a stream that is being captured into a graph use dispatch order. Every
- * tile is rendered exactly once in any case: images are identical with and without it.
- * ABI v8: the state is a pool allocated by vrt_create (8 slots of bands up to 65536 tiles, i.e.
- * 4096 x 4096 pixels; larger bands use dispatch order); reusing a slot on another stream waits
- * for its last launch on the device (hipStreamWaitEvent), not on the host — unless the caller has
- * destroyed that stream, when the device is synchronised once. Tiles with any pixel that took the
- * exact path (glass bounce stacks, near-edge walks) count as heavy (ABI v8). */
+ * (vrt_certified() == 1) of volumes with glass (DESIGN.md §6 "Tile order"): on = 1 (default),
+ * off = 0. Each launch records which of its 16x8 tiles had a pixel on the exact path (glass
+ * bounce stacks, near-edge walks; until ABI v8 only bounce stacks); the next launch of the same
+ * band (width, rows, row0, row_step) on the same stream dispatches those tiles first, each on the
+ * same XCD as before, the last to finish first, so the frame's longest waves start first.
+ * Launches on a stream that is being captured into a graph use dispatch order. Every tile is
+ * rendered exactly once in any case: images are identical with and without it.
+ * ABI v8: the state is a pool allocated by vrt_create (8 slots of 5 x 65536 words + a header:
+ * bands up to 65536 tiles, i.e. 4096 x 2048 pixels; larger bands use dispatch order), zeroed on the
+ * launch stream when a slot is (re)assigned; reusing a slot on another stream waits for its last
+ * launch on the device (hipStreamWaitEvent), not on the host — unless the caller has destroyed
+ * that stream, when the device is synchronised once. */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3

@@ -60,6 +60,11 @@ CONTEXT = {
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {
+    # the tile-order bookkeeping out of line (codegen of the render body independent of it)
+    "ordnoinline": [
+        ("vrt_render.hip", "__device__ __forceinline__ uint32_t ordered_tile(", "__device__ __noinline__ uint32_t ordered_tile("),
+        ("vrt_render.hip", "__device__ __forceinline__ void order_record(", "__device__ __noinline__ void order_record("),
+    ],
     # heavy tiles = tiles with any exact-path pixel (not only bounce stacks), tile order on for
     # every certified-pixel launch (also without glass)
     "heavyexact": [

@@ -29,6 +29,15 @@ namespace {
 constexpr int kParts = 2;              // interleaved row parts per device band
 constexpr int kOrderSlots = 8;         // tile-order buffers per device (band geometry x stream)
 constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 4096 x 4096 pixels
+constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 2u * vrt::kOrdClasses;  // KArgs::order
+// first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
+// 8160 tiles are heavy)
+#if defined(VRT_ORD_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_ORD_DIV is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_ORD_DIV
+#define VRT_ORD_DIV 4
+#endif
 // Filtered frames rotate through kRing buffers: frame f reads ring[(f-1) % kRing] (the temporal
 // history) and writes ring[f % kRing]. A device-output frame (vrt_render_frame_device) is handed
 // to the caller as its ring buffer and stays valid for two more frames with no copy.
@@ -37,7 +46,7 @@ constexpr int kRing = 4;
 struct OrderSlot {
   int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
   hipStream_t stream = nullptr;
-  uint32_t* d = nullptr;       // 3 x kOrderMaxTiles words inside the shard's pool
+  uint32_t* d = nullptr;       // kOrderSlotWords words inside the shard's pool
   hipEvent_t done = nullptr;   // recorded on the slot's stream when the slot is handed over
   bool used = false;
   uint64_t epoch = 0, tick = 0;
@@ -176,7 +185,7 @@ hipError_t shard_init(Shard& s, int device) {
   s.device = device;
   hipError_t e = hipSetDevice(device);
   const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
-  const size_t pool_words = size_t(kOrderSlots) * 3u * kOrderMaxTiles;
+  const size_t pool_words = size_t(kOrderSlots) * kOrderSlotWords;
   for (int p = 0; p < kParts && e == hipSuccess; ++p) e = hipStreamCreateWithFlags(&s.part[p], hipStreamNonBlocking);
   // ordering markers without timestamps (timing events make the command processor stamp and
   // flush around them: ~20 us gaps between the launches of a stream, measured)
@@ -193,7 +202,7 @@ hipError_t shard_init(Shard& s, int device) {
   if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
   if (e == hipSuccess) e = hipMalloc(&s.d_order_pool, pool_words * sizeof(uint32_t));
   for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) {
-    s.order[i].d = s.d_order_pool + size_t(i) * 3u * kOrderMaxTiles;
+    s.order[i].d = s.d_order_pool + size_t(i) * kOrderSlotWords;
     e = hipEventCreateWithFlags(&s.order[i].done, hipEventDisableTiming);
   }
   return e;
@@ -283,7 +292,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
   a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
   a.order = nullptr;
-  a.ord_r = a.ord_w = 0;
+  a.ord_r = a.ord_w = a.ctr_r = a.ctr_w = a.ctr_z = a.ord_q = 0;
   return a;
 }
 
@@ -320,7 +329,9 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
         return nullptr;
       }
     }
-    if (hipMemsetAsync(slot->d, 0, size_t(3) * a.tiles * sizeof(uint32_t), st) != hipSuccess) return nullptr;
+    // zero the list counters, the wave counters and both rank sets (no heavy tiles yet)
+    if (hipMemsetAsync(slot->d, 0, (vrt::kOrdHdr + size_t(3) * a.tiles) * sizeof(uint32_t), st) != hipSuccess)
+      return nullptr;
     slot->width = a.width;
     slot->rows = a.rows;
     slot->row0 = a.row0;
@@ -332,7 +343,11 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
   slot->tick = ++s.order_tick;
   a.order = slot->d;
   a.ord_r = uint32_t(slot->epoch & 1u);
-  a.ord_w = uint32_t((slot->epoch + 1u) & 1u);
+  a.ord_w = a.ord_r ^ 1u;
+  a.ctr_r = uint32_t(slot->epoch % 3u);
+  a.ctr_w = (a.ctr_r + 1u) % 3u;
+  a.ctr_z = (a.ctr_r + 2u) % 3u;
+  a.ord_q = (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
   slot->epoch++;
   return slot;
 }

@@ -37,11 +37,14 @@ struct KArgs {
   // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
   // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
   int32_t cert;
-  // tile dispatch order (stats-free launches, vrt_set_tile_order): nullptr = dispatch order.
-  // tiles_x: tiles per row; tiles: tiles of the launch; ord_r / ord_w: the flag sets read and
-  // written by this launch (grid 2 x tiles: heavy tiles first)
+  // tile dispatch order (stats-free launches, vrt_set_tile_order): nullptr = dispatch order, else
+  // the band's order buffer: three sets of kOrdClasses list counters, the per-tile wave counters,
+  // two rank sets of `tiles` words and two list sets of tiles + 8 words (see ordered_tile).
+  // tiles_x: tiles per row; tiles: tiles of the launch; ord_r / ord_w: the rank and list set read /
+  // written; ctr_r / ctr_w / ctr_z: the counter set read / appended to / zeroed; ord_q: first-pass
+  // slots per class (grid = 8 * ord_q + tiles)
   uint32_t* order;
-  uint32_t tiles_x, tiles, ord_r, ord_w;
+  uint32_t tiles_x, tiles, ord_r, ord_w, ctr_r, ctr_w, ctr_z, ord_q;
 };
 
 // Waves per workgroup, each rendering an 8x8 pixel tile. Two (a 16x8 tile): a finished
@@ -61,12 +64,14 @@ constexpr int kTileW = kWgWaves >= 2 ? 16 : 8;  // a workgroup's pixel tile: 16x
 constexpr int kTileH = kWgWaves == 4 ? 16 : 8;
 constexpr int kMaxStack = 17;               // bounce-stack entries: max_reflections + max_transparencies + 1
 constexpr int kCntReplicas = 256;           // counter replicas (per-wave atomics spread over them)
-constexpr uint32_t kOrdHdr = 0;             // tile-order buffer: per-tile wave counters, then two flag sets
+constexpr uint32_t kOrdClasses = 8;         // tile-order lists: tile % 8 (the XCD of its slot)
+constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 256-byte line each)
+constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
 
 // ---- launches (vrt_render.hip); all asynchronous on `s` ------------------------------------
 
 // render_kernel: the instance is chosen from (stats, a.textured, a.cert); grid = a.tiles, or
-// 2 * a.tiles with a tile order (a.order). cnt_rep: the counter replicas (stats launches).
+// 8 * a.ord_q + a.tiles with a tile order (a.order). cnt_rep: the counter replicas (stats launches).
 // ev_begin / ev_end (optional, timing events) are recorded when the kernel starts and ends on
 // the device (hipExtLaunchKernelGGL), not when the host enqueues it.
 void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,

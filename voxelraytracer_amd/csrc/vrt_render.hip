@@ -1550,20 +1550,41 @@ __device__ __forceinline__ uint32_t lane_id() {
 // Heavy tiles first (vrt_set_tile_order). A frame ends with its longest waves, those with exact-path
 // pixels (glass bounce stacks, walks the certified walk could not settle); dispatched in row
 // order, they start wherever they are in the image. Each stats-free launch therefore records which
-// of its tiles had such a pixel (until r02: only bounce stacks; C3 -2 %, profiles/r02_s09), and the next launch
-// of the same band (same stream) dispatches those first. The order buffer of a band holds a
-// per-tile wave counter and two per-tile flag sets: launch e reads set e % 2 (complete: written by
-// launch e - 1) and writes set (e + 1) % 2. The grid is two passes over the tiles in row order:
-// slot L < tiles renders tile L iff its flag is set, slot tiles + L renders it iff it is clear.
-// Both test the same immutable word, so every tile is rendered exactly once whatever the buffer
-// holds (a fresh zeroed buffer: no heavy tiles).
-// The tile workgroup L renders, or ~0u (nothing to do); a tile's flag word of the last launch is 1
-// when it ran a bounce stack (heavy)
+// of its tiles had such a pixel (until r02: only bounce stacks; C3 -2 %, profiles/r02_s09), and the
+// next launch of the same band (same stream) dispatches those first.
+// Workgroups are dealt to the 8 XCDs round-robin (workgroup L on XCD L % 8), and a tile keeps its
+// XCD — its L2 — from launch to launch only if it keeps its slot's residue mod 8: every
+// permutation that ignored this was 9-60 % slower at C3 (profiles/r02_s12_tileperm, r02_s14).
+// So heavy tiles are listed per class r = tile % 8: as a heavy tile finishes, its last wave
+// appends it to its class's list (kOrdClasses counters, one 256-byte line each) and stores its
+// rank (list position + 1; 0 for the other tiles). The next launch's grid is 8*ord_q + tiles
+// workgroups: slot L < 8*ord_q renders entry n - 1 - L / 8 of class L % 8's list (n = its length,
+// at most ord_q) if L / 8 < n, else exits — the class's heavy tiles in reverse completion order,
+// those that finished last first (C3 -4 % against completion order and against the flag passes,
+// profiles/r02_s14); slot 8*ord_q + t renders tile t unless its rank is in [1, ord_q] (rendered by
+// the first pass). The list and the ranks of a launch are written together, so every tile is rendered
+// exactly once (a fresh zeroed buffer: no heavy tiles). Until r02 s14 the first pass was `tiles`
+// workgroups testing per-tile flags (same slot residues), most of them empty.
+__device__ __forceinline__ uint32_t* ord_ctr(const KArgs& a, uint32_t set, uint32_t r) {
+  return a.order + (set * kOrdClasses + r) * kOrdCtrStride;
+}
+__device__ __forceinline__ uint32_t* ord_rank(const KArgs& a, uint32_t set) {
+  return a.order + kOrdHdr + (1u + set) * a.tiles;
+}
+__device__ __forceinline__ uint32_t* ord_list(const KArgs& a, uint32_t set) {  // entry j of class r: [j*8 + r]
+  return a.order + kOrdHdr + 3u * a.tiles + set * (a.tiles + kOrdClasses);
+}
+// The tile workgroup L renders, or ~0u (nothing to do)
 __device__ __forceinline__ uint32_t ordered_tile(const KArgs& a, uint32_t L) {
-  const uint32_t* flags = a.order + kOrdHdr + a.tiles + a.ord_r * a.tiles;
-  const bool first = L < a.tiles;
-  const uint32_t j = first ? L : L - a.tiles;
-  return ((flags[j] & 1u) != 0u) == first ? j : ~0u;
+  const uint32_t cap = kOrdClasses * a.ord_q;
+  if (L < cap) {
+    const uint32_t r = L % kOrdClasses, j = L / kOrdClasses;
+    if (j == 0u && threadIdx.x == 0u) *ord_ctr(a, a.ctr_z, r) = 0u;  // for the launch after the next
+    const uint32_t n = min(*ord_ctr(a, a.ctr_r, r), a.ord_q);
+    return j < n ? ord_list(a, a.ord_r)[(n - 1u - j) * kOrdClasses + r] : ~0u;  // last finished first
+  }
+  const uint32_t t = L - cap;
+  return ord_rank(a, a.ord_r)[t] - 1u < a.ord_q ? ~0u : t;  // rank 0 wraps to ~0u: not listed
 }
 // after the trace: the tile's last wave files it for the next launch
 // (counter: bits 0-7 waves done, 8-15 heavy waves)
@@ -1573,8 +1594,14 @@ __device__ __forceinline__ void order_record(const KArgs& a, uint32_t tile, bool
   const uint32_t old = atomicAdd(cnt, add);
   if ((old & 0xFFu) != uint32_t(kWgWaves) - 1u) return;
   *cnt = 0u;
-  const uint32_t all = old + add;
-  a.order[kOrdHdr + a.tiles + a.ord_w * a.tiles + tile] = (all & 0xFF00u) != 0u ? 1u : 0u;
+  uint32_t rank = 0u;
+  if (((old + add) & 0xFF00u) != 0u) {
+    const uint32_t r = tile % kOrdClasses;
+    const uint32_t k = atomicAdd(ord_ctr(a, a.ctr_w, r), 1u);  // <= tiles / 8: one per tile of class r
+    ord_list(a, a.ord_w)[k * kOrdClasses + r] = tile;
+    rank = k + 1u;
+  }
+  ord_rank(a, a.ord_w)[tile] = rank;
 }
 
 __device__ __forceinline__ int pixel_x(uint32_t tx, int wave, uint32_t lane) {
@@ -1775,7 +1802,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
 // CERT (stats-free colour-only instances): 0 exact walks only, 1 certified walks for the exact
 // path's shadow and air-medium secondary rays, 2 also whole pixels first.
-template <bool STATS, bool TEX, int CERT = 0>
+template <bool STATS, bool TEX, int CERT = 0, bool ORD = false>
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -1789,11 +1816,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
   uint32_t tile = blockIdx.x;
-  if constexpr (!STATS) {
-    if (a.order) {
-      tile = ordered_tile(a, blockIdx.x);
-      if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
-    }
+  if constexpr (ORD) {  // heavy-first tile order (a.order): its own instance
+    tile = ordered_tile(a, blockIdx.x);
+    if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
   const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
@@ -1861,11 +1886,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     }
   }
 #endif
-  if constexpr (!STATS) {
-    if (a.order) {
-      const bool heavy_wave = __ballot(heavy) != 0ull;
-      if (lane_id() == 0) order_record(a, tile, heavy_wave);
-    }
+  if constexpr (ORD) {
+    const bool heavy_wave = __ballot(heavy) != 0ull;
+    if (lane_id() == 0) order_record(a, tile, heavy_wave);
   }
   if (STATS && counters) {
     unsigned long long* slot = counters + size_t(blockIdx.x % kCntReplicas) * VRT_CNT_COUNT;
@@ -2074,13 +2097,14 @@ namespace vrt {
 
 void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out, vrt_hit* hit,
                    unsigned long long* cnt_rep, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end) {
-  const dim3 grid(a.order ? 2u * a.tiles : a.tiles);
+  const dim3 grid(a.order ? kOrdClasses * a.ord_q + a.tiles : a.tiles);
   // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
   // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
   // ~5 %), exact walks only (0)
   auto kern = a.textured ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
                          : (stats ? render_kernel<true, false>
-                                  : (a.cert == 2 ? render_kernel<false, false, 2>
+                                  : (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true>
+                                                            : render_kernel<false, false, 2>)
                                      : a.cert == 1 ? render_kernel<false, false, 1>
                                                    : render_kernel<false, false, 0>));
   if (ev_begin || ev_end)

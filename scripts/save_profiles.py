@@ -43,7 +43,7 @@ if passes:
         f.write(summ)
     s = json.loads(summ)
     if "fetch_bytes" in s and "write_bytes" in s:
-        out = {"config": a.config, "output": a.output, "kernel": "vrt::render_kernel<false, false, 2> (stats-free, colour-only, certified walks)",
+        out = {"config": a.config, "output": a.output, "kernel": "vrt::render_kernel<false, false, 2, true> (stats-free, colour-only, certified walks, heavy-first tile order)",
                "source": f"profiles/{os.path.basename(dst)}/pmc (rocprofv3 --pmc FETCH_SIZE and --pmc "
                          "WRITE_SIZE in separate passes over bench.py --steps 5 --warmup 1 --parts 1: one launch = one frame)",
                "fetch_size_bytes_raw": s["fetch_bytes"], "write_size_bytes": s["write_bytes"],

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--wg-waves", type=int, default=2)
     ap.add_argument("--slots", type=int, default=256 * 4 * 6, help="wave slots (CUs*SIMDs*occupancy)")
     ap.add_argument("--save", default="")
+    ap.add_argument("--tile-order", action="store_true",
+                    help="keep the heavy-first tile order on (grid = 8*q + tiles slots; empty slots "
+                         "leave no stamps and are dropped)")
     ap.add_argument("--band", default="", help="ROW0,ROWS: also time that band alone (few waves, "
                     "each alone on its SIMD) against the same tiles inside the full frame")
     args = ap.parse_args()
@@ -53,14 +56,20 @@ def main():
             ren.upload_volume_device(vox.data_ptr(), n, stream.cuda_stream)
             # stamps are indexed by workgroup: the heavy-first tile order's two-pass grid leaves
             # slots without stamps (their tile is rendered by the other pass), so time dispatch order
-            ren.set_tile_order(False)
+            ren.set_tile_order(args.tile_order)
             for _ in range(5):   # warm; the stamps of the last launch are kept
                 ren.render_rows_async(cam, params, 0, h, 1, out.data_ptr(), 0, 0, stream.cuda_stream)
             torch.cuda.synchronize()
         tw, th = (16, 16) if args.wg_waves == 4 else ((16, 8) if args.wg_waves == 2 else (8, 8))
         waves = ((w + tw - 1) // tw) * ((h + th - 1) // th) * args.wg_waves
-        st = np.zeros((waves, 3), dtype=np.uint64)
+        tiles = waves // args.wg_waves
+        slots = tiles + (8 * ((tiles + 31) // 32) if args.tile_order else 0)  # VRT_ORD_DIV 4
+        st = np.zeros((slots * args.wg_waves, 3), dtype=np.uint64)
         assert lib.vrt_debug_stamps(st.ctypes.data, st.size) == 0
+        keep = st[:, 0] != 0
+        if args.tile_order:
+            st = st[keep]
+            waves = len(st)
         t0 = st[:, 0].min()
         start = (st[:, 0] - t0).astype(np.float64) * 10.0   # ns (100 MHz)
         end = (st[:, 1] - t0).astype(np.float64) * 10.0
@@ -116,14 +125,16 @@ def main():
             if hasattr(lib, "vrt_debug_stamps2"):  # {time after the certified attempt, exact lanes}
                 lib.vrt_debug_stamps2.restype = C.c_int
                 lib.vrt_debug_stamps2.argtypes = [C.c_void_p, C.c_uint64]
-                st2 = np.zeros((waves, 2), dtype=np.uint64)
+                st2 = np.zeros((len(keep), 2), dtype=np.uint64)
                 assert lib.vrt_debug_stamps2(st2.ctypes.data, st2.size) == 0
+                st2 = st2[keep] if args.tile_order else st2[:waves]
                 extra["stamps2"] = st2
             if hasattr(lib, "vrt_debug_stamps3"):  # {after the exact primary trace, after the stacks}
                 lib.vrt_debug_stamps3.restype = C.c_int
                 lib.vrt_debug_stamps3.argtypes = [C.c_void_p, C.c_uint64]
-                st3 = np.zeros((waves, 2), dtype=np.uint64)
+                st3 = np.zeros((len(keep), 2), dtype=np.uint64)
                 assert lib.vrt_debug_stamps3(st3.ctypes.data, st3.size) == 0
+                st3 = st3[keep] if args.tile_order else st3[:waves]
                 extra["stamps3"] = st3
             np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st, **extra)
     return report

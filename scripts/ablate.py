@@ -60,6 +60,12 @@ CONTEXT = {
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {
+    # the tile order also for certified-exact-path launches (CERT 1: glass-heavy volumes, C1)
+    "ordcert1": [
+        ("vrt_context.cpp", "a.textured || a.cert != 2 ||", "a.textured || a.cert < 1 ||"),
+        ("vrt_render.hip", "                                     : a.cert == 1 ? render_kernel<false, false, 1>",
+         "                                     : a.cert == 1 ? (a.order ? render_kernel<false, false, 1, true> : render_kernel<false, false, 1>)"),
+    ],
     # the tile-order bookkeeping out of line (codegen of the render body independent of it)
     "ordnoinline": [
         ("vrt_render.hip", "__device__ __forceinline__ uint32_t ordered_tile(", "__device__ __noinline__ uint32_t ordered_tile("),

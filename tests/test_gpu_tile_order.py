@@ -102,3 +102,48 @@ def test_tile_order_temporal_in_place(renderer):
 def test_tile_order_switch(renderer):
     assert renderer._lib.vrt_set_tile_order(renderer._h, 2) == vrt.abi.VRT_ERR_INVALID
     renderer.set_tile_order(True)
+
+
+def test_tile_order_slot_recycling(renderer):
+    """More (band geometry, stream) pairs than the pool's 8 slots, on three streams in turn: slots
+    are recycled across streams (the new stream waits for the old one on the device) and every
+    frame still equals the exact instance's."""
+    n, w, h = 128, 256, 160
+    renderer.upload_volume(vrt.build_scene("refraction", n), n)
+    p = vrt.default_params(4, 4)
+    renderer.set_tile_order(True)
+    cam = vrt.make_camera(w, h)
+    exact, _, _ = renderer.render(cam, p)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    for rnd in range(3):
+        for k in range(1, 5):   # k interleaved bands: 1 + 2 + 3 + 4 = 10 geometries per round
+            bands = tuple((r, k) for r in range(k))
+            sts = [streams[(rnd + i) % 3] for i in range(k)]
+            img = frames(renderer, cam, p, h, w, 1, bands=bands, streams=sts)[0]
+            assert same(img, exact), f"round {rnd}, {k} bands"
+
+
+def test_tile_order_graph_capture(renderer):
+    """A launch captured into a HIP graph uses dispatch order (a replayed node cannot rotate the
+    order state); replays equal the exact instance."""
+    n, w, h = 128, 240, 136
+    renderer.upload_volume(vrt.build_scene("refraction", n), n)
+    p = vrt.default_params(4, 4)
+    renderer.set_tile_order(True)
+    cam = vrt.make_camera(w, h)
+    exact, _, _ = renderer.render(cam, p)
+    img = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # warm the stream outside the capture (the order slot exists)
+        renderer.render_rows_async(cam, p, 0, h, 1, img.data_ptr(), 0, 0, s.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        renderer.render_rows_async(cam, p, 0, h, 1, img.data_ptr(), 0, 0,
+                                   torch.cuda.current_stream().cuda_stream)
+    for _ in range(3):
+        img.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert same(img.cpu().numpy(), exact)

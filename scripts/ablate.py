@@ -60,6 +60,8 @@ CONTEXT = {
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {
+    # tile order: a tile counts as heavy only if both of its waves had exact-path pixels
+    "heavy2": [("vrt_render.hip", "  if (((old + add) & 0xFF00u) != 0u) {\n", "  if (((old + add) & 0xFF00u) >= 0x200u) {\n")],
     # the tile order also for certified-exact-path launches (CERT 1: glass-heavy volumes, C1)
     "ordcert1": [
         ("vrt_context.cpp", "a.textured || a.cert != 2 ||", "a.textured || a.cert < 1 ||"),

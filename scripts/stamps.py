@@ -67,6 +67,7 @@ def main():
         st = np.zeros((slots * args.wg_waves, 3), dtype=np.uint64)
         assert lib.vrt_debug_stamps(st.ctypes.data, st.size) == 0
         keep = st[:, 0] != 0
+        wave_index = np.nonzero(keep)[0] if args.tile_order else np.arange(len(st))
         if args.tile_order:
             st = st[keep]
             waves = len(st)
@@ -136,7 +137,8 @@ def main():
                 assert lib.vrt_debug_stamps3(st3.ctypes.data, st3.size) == 0
                 st3 = st3[keep] if args.tile_order else st3[:waves]
                 extra["stamps3"] = st3
-            np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st, **extra)
+            np.savez_compressed(os.path.join(args.save, f"stamps_{cfg}.npz"), stamps=st,
+                                wave_index=wave_index, **extra)
     return report
 
 

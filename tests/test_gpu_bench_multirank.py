@@ -1,7 +1,8 @@
 """Rehearsal of bench.py's multi-rank path on a one-GPU box: torch.distributed.run with two ranks
 sharing cuda:0 over gloo (RCCL needs one GPU per rank; the driver's 8-GPU run uses it). Checks the
-JSON contract of rank 0's line for N = 2, weak scaling (the frame is 2 x 1080 rows), the gather of
-RGBA8 parts and the max-over-ranks timing — the code path the scaling runs take."""
+JSON contract of rank 0's line for N = 2, weak scaling (the frame is 2 x 1080 rows), the bands
+kept on their ranks with one gather after the timed region (the default) or the per-frame gather of
+RGBA8 parts (--gather-frames), and the max-over-ranks timing — the code path the scaling runs take."""
 import json
 import os
 import socket
@@ -23,12 +24,13 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("scaling", ["weak", "strong"])
-def test_bench_two_ranks_json(built, scaling):
+@pytest.mark.parametrize("scaling,gather", [("weak", False), ("strong", False), ("weak", True)])
+def test_bench_two_ranks_json(built, scaling, gather):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
            "--backend", "gloo", "--same-device", "--scaling", scaling, "--cpu-seconds", "0"]
+    cmd += ["--gather-frames"] if gather else []
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -44,3 +46,9 @@ def test_bench_two_ranks_json(built, scaling):
     assert out["config"]["frame"].startswith("1920x2160" if scaling == "weak" else "1920x1080")
     assert out["roofline"]["kernel_ms_max_over_ranks"] >= out["roofline"]["kernel_ms"]
     assert out["cpu_baseline"] is None        # rank 0 at N=1 only
+    assert out["verified"] is True
+    if gather:
+        assert out["collect"] is None and "every frame" in out["config"]["parallelism"]
+    else:   # one gather of the last frame after the timed region
+        rows = 2160 if scaling == "weak" else 1080
+        assert out["collect"]["rows"] == rows and out["collect"]["bytes"] == rows * 1920 * 4

@@ -24,7 +24,7 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1):
+def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1, gather=True):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -53,14 +53,21 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
         state["i"] += 1
 
     tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
-                       dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts)
+                       dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts,
+                       gather=gather)
     got = []
     for _ in range(frames):
         f = tiler.frame()
-        if f is not None:
-            got.append(f.clone().numpy())
+        if gather:
+            if f is not None:
+                got.append(f.clone().numpy())
+        else:   # bands stay on their ranks; gather each frame here only to check it
+            tiler.finish()
+            full = tiler.collect()
+            if rank == 0:
+                got.append(full.clone().numpy())
     f = tiler.finish()
-    if f is not None:
+    if gather and f is not None:
         got.append(f.clone().numpy())
     if rank == 0:
         q.put((got, bytes(vox_np)))
@@ -178,3 +185,34 @@ def test_part_spec_and_assembly():
     g = torch.stack([torch.stack([frame[s * world + r::world * parts] for s in range(parts)])
                      for r in range(world)])
     assert torch.equal(assemble_parts(g), frame)
+
+
+@pytest.mark.parametrize("world,parts", [(2, 1), (2, 2), (3, 2)])
+def test_distributed_bands_without_per_frame_gather(built, world, parts):
+    """gather=False (bench.py's multi-rank default): every rank renders and filters its own band
+    in place with no exchange; collect() assembles the frame on rank 0 — the RGBA8 temporal
+    sequence equals the single-process one bit for bit."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h, frames, alpha = 16, 20, 12, 3, 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
+                                              parts, False)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, _ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    hist = np.zeros((h, w, 4), np.uint8)
+    assert len(got) == frames
+    for t in range(frames):
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert np.array_equal(got[t], hist), t

@@ -20,8 +20,14 @@ With one rank and P > 1 parts, every part renders straight into its rows of the 
 rows, which hold the previous frame: no band buffers, no assembly copy (it cost ≈4 % of a C3
 frame as two strided copy kernels per frame).
 
-FrameTiler double-buffers the band (N > 1) so that the gather of frame k overlaps the render of
-frame k+1. Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8 store
+With several ranks the frame is either gathered to rank 0 every frame (gather=True: the display
+of one whole frame on one GPU) or kept distributed (gather=False, bench.py's default for N > 1):
+the per-pixel program has no exchange step, so each rank then renders and filters its band in
+place exactly as a single rank renders its frame, and collect() gathers the bands once when the
+whole frame is wanted (SURVEY §8e's per-frame gather is output delivery, not part of the path: at
+weak scaling every rank's 8.3 MB RGBA8 band would cross xGMI into rank 0 per 0.06 ms frame).
+FrameTiler double-buffers the band (gather=True) so that the gather of frame k overlaps the render
+of frame k+1. Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8 store
 (the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire instead of 16.
 The temporal history is part-local (each part blends its own rows, on its own stream), so it adds
 no exchange and no cross-stream dependency; the previous frame's part buffer IS the history.
@@ -94,16 +100,18 @@ class FrameTiler:
     the CURRENT stream (the HIP kernel through the C-ABI, or the oracle in CPU tests); `prev` holds
     that part's rows of the previous frame (the temporal history; zeros before the first frame;
     it is `out` itself with one buffer: each pixel is read before it is written).
-    frame() renders the next frame; with one rank it returns that frame (for parts > 1 each part
-    renders into its rows of it directly, in place); with several ranks the gather is issued
-    asynchronously and rank 0 returns the PREVIOUS frame, assembled on `self.assembly_stream`
-    (None on the first call and on other ranks), so the gather of frame k overlaps the render of
-    frame k+1. finish() drains the pipeline and returns the last frame on rank 0. A returned
-    frame is valid until the next frame() call; synchronise the device before reading it.
+    frame() renders the next frame; with one rank, or with gather=False, it returns this rank's
+    band of it (the whole frame with one rank; for parts > 1 each part renders into its rows of it
+    directly, in place); with several ranks and gather=True the gather is issued asynchronously
+    and rank 0 returns the PREVIOUS frame, assembled on `self.assembly_stream` (None on the first
+    call and on other ranks), so the gather of frame k overlaps the render of frame k+1. finish()
+    drains the pipeline and returns the last frame (band) on rank 0; collect() (gather=False)
+    assembles the last frame on rank 0 with one gather. A returned frame is valid until the next
+    frame() call; synchronise the device before reading it.
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
-                 channels: int = 4, dtype=torch.float32, parts: int = 1):
+                 channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.group = group
@@ -113,13 +121,16 @@ class FrameTiler:
         self.rows_p = self.specs[0][1]
         self.render_band = render_band
         self.cuda = torch.device(device).type == "cuda"
+        self.gather = gather and self.world > 1
+        self.channels, self.dtype = channels, dtype
         shape = (parts, self.rows_p, width, channels)
-        nbuf = 2 if self.world > 1 else 1
-        # one rank, several parts: the parts render into (and filter in place) the frame itself
-        self.direct = self.world == 1 and parts > 1
+        nbuf = 2 if self.gather else 1
+        # no per-frame gather, several parts: the parts render into (and filter in place) this
+        # rank's band itself (the whole frame with one rank)
+        self.direct = not self.gather and parts > 1
         self.frame_buf = None
         if self.direct:
-            self.frame_buf = torch.zeros((height, width, channels), dtype=dtype, device=device)
+            self.frame_buf = torch.zeros((self.rows, width, channels), dtype=dtype, device=device)
             self.bands = [self.frame_buf.view(shape)]   # same storage (bench's counted launch)
         else:
             self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
@@ -127,9 +138,9 @@ class FrameTiler:
                              if self.cuda and parts > 1 else None)
         self.assembly_stream = None
         self.gathered = None
-        if self.rank == 0 and self.world > 1:
+        if self.rank == 0 and self.gather:
             self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
-        if self.rank == 0 and self.world > 1:
+        if self.rank == 0 and self.gather:
             self.gathered = [torch.empty((self.world,) + shape, dtype=dtype, device=device)
                              for _ in range(nbuf)]
             if self.cuda:
@@ -168,7 +179,8 @@ class FrameTiler:
         return events
 
     def _frame_rows(self, s: int) -> torch.Tensor:
-        """frame_buf rows of this (single) rank's part s: rows s, s + parts, ..."""
+        """frame_buf rows of this rank's part s (direct mode: frame_buf is the rank's band, the
+        whole frame with one rank): band rows s, s + parts, ..."""
         return self.frame_buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
 
     # ---- pipeline --------------------------------------------------------------------------
@@ -178,7 +190,7 @@ class FrameTiler:
         prev = self.bands[(self.k - 1) % nb]
         self.k += 1
         band = self.bands[b]
-        if self.world == 1:
+        if not self.gather:   # one rank, or ranks that keep their bands: no exchange
             self._render_parts(band, prev, None)
             return band[0] if self.parts == 1 else self.frame_buf
         wait_work, self.pending[b] = self.pending[b], None
@@ -216,8 +228,20 @@ class FrameTiler:
         self.assembled[b] = self.assembly_stream.record_event()
         return out
 
-    def finish(self) -> Optional[torch.Tensor]:
+    def collect(self) -> Optional[torch.Tensor]:
+        """Without the per-frame gather, after finish(): one gather of every rank's current band to
+        rank 0, re-interleaved into the whole frame (returned on rank 0, None elsewhere); e.g. to
+        display or check the last frame. Synchronous."""
+        assert not self.gather, "collect() is for gather=False tilers"
+        band = (self.frame_buf if self.direct else self.bands[0][0]).contiguous()
         if self.world == 1:
+            return band
+        glist = ([torch.empty_like(band) for _ in range(self.world)] if self.rank == 0 else None)
+        dist.gather(band, glist, dst=0, group=self.group)
+        return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
+
+    def finish(self) -> Optional[torch.Tensor]:
+        if not self.gather:
             if self.part_streams is not None:
                 cur = torch.cuda.current_stream()
                 for st in self.part_streams:

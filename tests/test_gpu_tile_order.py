@@ -147,3 +147,17 @@ def test_tile_order_graph_capture(renderer):
         g.replay()
         torch.cuda.synchronize()
         assert same(img.cpu().numpy(), exact)
+
+
+def test_tile_order_band_beyond_the_pool(renderer):
+    """A band of more tiles than a pool slot holds (65 536: here 7680 x 4320 = 259 200 tiles in
+    one launch) renders in dispatch order; the frame equals the exact instance's."""
+    n, w, h = 128, 7680, 4320
+    renderer.upload_volume(vrt.build_scene("refraction", n), n)
+    p = vrt.default_params(4, 4)
+    renderer.set_tile_order(True)
+    cam = vrt.make_camera(w, h)
+    exact, _, _ = renderer.render(cam, p, want_hits=False)
+    img = frames(renderer, cam, p, h, w, 2)
+    for k, f in enumerate(img):
+        assert same(f, exact), f"frame {k}"

@@ -60,6 +60,9 @@ CONTEXT = {
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {
+    # bounce stacks without raised wave priority / at priority 1
+    "noprio": [("vrt_render.hip", "    __builtin_amdgcn_s_setprio(kStackPrio);  // bounce stacks: the longest waves of a frame\n", "")],
+    "prio1": [("vrt_render.hip", "constexpr int kStackPrio = 3;", "constexpr int kStackPrio = 1;")],
     # tile order: a tile counts as heavy only if both of its waves had exact-path pixels
     "heavy2": [("vrt_render.hip", "  if (((old + add) & 0xFF00u) != 0u) {\n", "  if (((old + add) & 0xFF00u) >= 0x200u) {\n")],
     # the tile order also for certified-exact-path launches (CERT 1: glass-heavy volumes, C1)

@@ -301,12 +301,12 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
 // slot's old stream (everything enqueued there so far, its last launch with the slot included)
 // and makes this stream wait for that mark on the device, then zeroes the slot on this stream (no
 // heavy tiles yet). No marker is needed per launch: launches on one stream are ordered. Not while
-// the stream is being captured into a graph (a replayed node would reuse one flag set): dispatch
-// order then.
+// the stream is being captured into a graph (a replayed node would reuse one list / counter set):
+// dispatch order then.
 OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
-  // only where it pays: glass in the volume (no bounce stacks otherwise: the first pass would be
-  // `tiles` empty workgroups, C2/C4 +4 %) and certified pixels (glass-heavy volumes, where most
-  // tiles are heavy, keep dispatch order: C1 +8 %)
+  // only where it pays: glass in the volume (without it the order gains nothing: C2 ±0, C4 +5 %,
+  // profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where every tile is
+  // heavy, keep dispatch order: C1 +3.4 %)
   if (!ctx->tile_order || a.tiles == 0 || a.tiles > kOrderMaxTiles || a.textured || a.cert != 2 ||
       !s.has_glass)
     return nullptr;

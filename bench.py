@@ -213,9 +213,6 @@ def main():
     ren = vrt.Renderer(local)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
 
-    evs = []
-    timing = {"on": False}
-
     def launch(row0, rows, step, out, prev, cnt_ptr=0):
         sp = torch.cuda.current_stream(dev).cuda_stream   # the part's stream (FrameTiler)
         # a part may be a row-strided view into the frame (FrameTiler's single-rank mode)
@@ -230,15 +227,7 @@ def main():
                                   pitch=pitch)
 
     def render_band(row0, rows, step, out, prev):
-        e = None
-        if timing["on"]:   # only in the launch-timing pass, never in the timed region
-            cs = torch.cuda.current_stream(dev)
-            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            e[0].record(cs)
         launch(row0, rows, step, out, prev)
-        if e is not None:
-            e[1].record(cs)
-            evs.append(e)
 
     parts = args.parts if frame_h % (world * args.parts) == 0 else 1
     tiler = FrameTiler(w, frame_h, render_band, dev,
@@ -287,16 +276,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     frame_gpu_ms = ev0.elapsed_time(ev1) / args.steps
-    # Launch-timing pass (after the timed region): per-launch events on each part's stream give
-    # the mean duration of one render_kernel launch, the figure rocprofv3 reports per kernel
-    # (the `parts` launches of a frame overlap, so a launch lasts longer than frame_gpu_ms/parts).
-    timing["on"] = True
-    for _ in range(20):
+    # Launch-timing pass (after the timed region, the same FrameTiler path): the mean duration of
+    # one render_kernel launch — what rocprofv3 reports per kernel — from the kernels' own device
+    # start / end timestamps (vrt_set_launch_timing: hipExtLaunchKernelGGL events; the `parts`
+    # launches of a frame overlap, so a launch lasts longer than frame_gpu_ms / parts). Not in the
+    # timed region: the per-launch events cost ~8 % of the frame rate (r02 s17).
+    lt_frames = max(20, min(args.steps, 200))
+    ren.set_launch_timing(lt_frames * parts)
+    for _ in range(lt_frames):
         tiler.frame()
     tiler.finish()
-    torch.cuda.synchronize(dev)
-    timing["on"] = False
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    lt_total, lt_n = ren.launch_timing()
+    ren.set_launch_timing(0)
+    launch_ms = lt_total / max(lt_n, 1)
     t = torch.tensor([elapsed, frame_gpu_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -476,6 +468,9 @@ def main():
                 "bytes_per_launch": int(bytes_per_launch),
                 "bytes_per_frame": own_bytes,
                 "launch_ms": round(launch_ms, 4),
+                "launch_ms_is": ("mean render_kernel duration from the kernels' device start / end "
+                                 "timestamps (hipExtLaunchKernelGGL events, vrt_set_launch_timing) "
+                                 "over a pass of the same frames after the timed region"),
                 "launches_per_frame": parts,
                 "kernel_ms": round(frame_gpu_ms, 4),
                 "kernel_ms_is": (f"GPU time per frame of this rank: {parts} concurrent "

@@ -185,6 +185,16 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode);
  * else 0. */
 int vrt_certified(const vrt_ctx* ctx);
 
+/* ABI v8 (r02): device timestamps of the async band launches (vrt_render_rows*_async,
+ * vrt_render_temporal_rows*_async on the first device): vrt_set_launch_timing(ctx, n) creates
+ * timing events for the next n launches (0: off; it synchronises the first device when replacing
+ * earlier events), each launch then records its kernel's start and end on the device
+ * (hipExtLaunchKernelGGL); vrt_launch_timing waits for the recorded launches, returns the sum of
+ * their kernel durations and their count, and frees the events for the next n launches. This is
+ * the per-kernel duration a profiler reports, measured in the caller's own timed region. */
+int vrt_set_launch_timing(vrt_ctx* ctx, int32_t launches);
+int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
+
 /* ABI v7: heavy-first tile order for stats-free colour-only launches with certified pixels
  * (vrt_certified() == 1) of volumes with glass (DESIGN.md §6 "Tile order"): on = 1 (default),
  * off = 0. Each launch records which of its 16x8 tiles had a pixel on the exact path (glass

@@ -19,7 +19,9 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 step bench 300 python bench.py --config "$CFG"
 export TMPDIR=/tmp
-step prof_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$ROOT/bench.py" --config "$CFG" --steps 20 --warmup 3 --cpu-seconds 0
+# the bench command itself under the kernel trace (its JSON line lands in prof_trace.log): the
+# bench's launch_ms and rocprofv3's mean kernel duration come from the same process
+step prof_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$ROOT/bench.py" --config "$CFG" --cpu-seconds 0
 [ -n "$NO_PMC" ] && exit 0
 step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$ROOT/bench.py" --config "$CFG" --steps 5 --warmup 1 --cpu-seconds 0 --parts 1
 step prof_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$ROOT/bench.py" --config "$CFG" --steps 5 --warmup 1 --cpu-seconds 0 --parts 1

@@ -26,6 +26,12 @@ for name in ("bench.log", "pytest_gpu.log", "smoke.log"):
     if os.path.exists(p):
         with open(p) as f, open(os.path.join(dst, name), "w") as g:
             g.writelines(l for l in f if "amdgpu.ids" not in l)
+pt = os.path.join(src, "prof_trace.log")   # the bench line printed under the kernel trace
+if os.path.exists(pt):
+    lines = [l for l in open(pt) if l.startswith("{")]
+    if lines:
+        with open(os.path.join(dst, "bench_under_rocprof.json"), "w") as g:
+            g.write(lines[-1])
 ks = os.path.join(src, "trace", "run_kernel_stats.csv")
 if os.path.exists(ks):
     shutil.copy(ks, os.path.join(dst, f"{a.config}_kernel_stats.csv"))

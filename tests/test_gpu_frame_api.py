@@ -161,3 +161,27 @@ def test_headless_app_gets_the_bench_frame_time(built, tmp_path):
     print(f"vrt_headless pipelined {app_ms:.4f} ms/frame, synchronous {sync_ms:.4f} ms/frame, "
           f"bench {bench_ms:.4f} ms/frame")
     assert app_ms <= 1.10 * bench_ms, (app_ms, bench_ms)
+
+
+def test_launch_timing(built):
+    """vrt_set_launch_timing / vrt_launch_timing: device start/end timestamps of async band
+    launches (bench.py's launch_ms); launches past the requested count are not recorded."""
+    n, w, h = 64, 320, 180
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("refraction", n), n)
+        cam = vrt.make_camera(w, h)
+        p = vrt.default_params(4, 4)
+        img = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        r.set_launch_timing(2)
+        for _ in range(3):   # the third launch finds no free events
+            r.render_rows_async(cam, p, 0, h, 1, img.data_ptr(), 0, 0, s)
+        total, k = r.launch_timing()
+        assert k == 2 and total > 0.0
+        r.render_rows_async(cam, p, 0, h, 1, img.data_ptr(), 0, 0, s)   # events free again
+        total2, k2 = r.launch_timing()
+        assert k2 == 1 and total2 > 0.0
+        r.set_launch_timing(0)
+        r.render_rows_async(cam, p, 0, h, 1, img.data_ptr(), 0, 0, s)
+        assert r.launch_timing() == (0.0, 0)
+        torch.cuda.synchronize()

@@ -340,6 +340,18 @@ class Renderer:
                     "vrt_render_frame_device")
         return ptr.value, (float(st.kernel_ms) if st is not None else None)
 
+    def set_launch_timing(self, launches: int):
+        """vrt_set_launch_timing: device start/end timestamps for the next `launches` async band
+        launches (0: off)."""
+        self._check(self._lib.vrt_set_launch_timing(self._h, int(launches)), "vrt_set_launch_timing")
+
+    def launch_timing(self):
+        """vrt_launch_timing: (sum of the recorded launches' kernel durations in ms, launches)."""
+        total, n = C.c_double(), C.c_uint64()
+        self._check(self._lib.vrt_launch_timing(self._h, C.byref(total), C.byref(n)),
+                    "vrt_launch_timing")
+        return total.value, n.value
+
     def debug_collectives(self):
         """vrt_debug_collectives: this one-device context takes the multi-GPU path through RCCL
         (one-rank communicator: ncclBroadcast of the volume, ncclGather of the band)."""

@@ -113,6 +113,8 @@ SIGNATURES = {
     "vrt_set_certified": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_certified": (C.c_int, [C.c_void_p]),
     "vrt_set_tile_order": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_set_launch_timing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_launch_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "vrt_render": (
         C.c_int,
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_void_p, C.c_void_p, C.POINTER(Stats)],

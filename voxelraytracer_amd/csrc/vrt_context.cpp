@@ -99,6 +99,10 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
+  // vrt_set_launch_timing: timing events for the async band launches' device start / end
+  // timestamps (2 per launch, created up front), and how many are in use since the last read
+  std::vector<hipEvent_t> lt_ev;
+  size_t lt_used = 0;
   std::vector<uint8_t> atlas_host;      // bytes of the last atlas upload (a params pointer is
                                         // re-uploaded when its bytes differ, not by identity)
   int32_t hist_w = 0, hist_h = 0;       // image size of the resident whole-frame history
@@ -694,6 +698,8 @@ void vrt_destroy(vrt_ctx* c) {
     for (hipEvent_t e : c->ev_consumed)
       if (e) (void)hipEventDestroy(e);
     if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
+    if (!c->lt_ev.empty()) (void)hipDeviceSynchronize();
+    for (hipEvent_t e : c->lt_ev) (void)hipEventDestroy(e);
   }
   for (Shard& s : c->sh) shard_free(s);
   delete c;
@@ -809,6 +815,42 @@ int vrt_set_skip_layout(vrt_ctx* ctx, int32_t octants) {
   return VRT_OK;
 }
 
+int vrt_set_launch_timing(vrt_ctx* ctx, int32_t launches) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (launches < 0 || launches > (1 << 20)) return fail(ctx, VRT_ERR_INVALID, "launches must be in [0, 2^20]");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  if (!ctx->lt_ev.empty()) VRT_HIP(ctx, hipDeviceSynchronize());  // no launch still records into them
+  for (hipEvent_t e : ctx->lt_ev) (void)hipEventDestroy(e);
+  ctx->lt_ev.clear();
+  ctx->lt_used = 0;
+  for (int32_t i = 0; i < 2 * launches; ++i) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return fail(ctx, VRT_ERR_DEVICE, "hipEventCreate (launch timing)");
+    ctx->lt_ev.push_back(e);
+  }
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches) {
+  if (!ctx || !total_ms || !launches) return VRT_ERR_INVALID;
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  double total = 0.0;
+  for (size_t i = 0; i + 1 < ctx->lt_used; i += 2) {
+    VRT_HIP(ctx, hipEventSynchronize(ctx->lt_ev[i + 1]));
+    float ms = 0.0f;
+    VRT_HIP(ctx, hipEventElapsedTime(&ms, ctx->lt_ev[i], ctx->lt_ev[i + 1]));
+    total += ms;
+  }
+  *total_ms = total;
+  *launches = ctx->lt_used / 2;
+  ctx->lt_used = 0;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
   if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
@@ -874,6 +916,14 @@ static int check_band(vrt_ctx* ctx, const vrt_camera* cam, int32_t row0, int32_t
   return VRT_OK;
 }
 
+// The next launch's timestamp events (vrt_set_launch_timing), or none when off / all in use
+void launch_timing_events(vrt_ctx* ctx, hipEvent_t& begin, hipEvent_t& end) {
+  begin = end = nullptr;
+  if (ctx->lt_used + 2 > ctx->lt_ev.size()) return;
+  begin = ctx->lt_ev[ctx->lt_used++];
+  end = ctx->lt_ev[ctx->lt_used++];
+}
+
 int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
                                   int32_t rows, int32_t row_step, int64_t pitch, float* d_out_rgba,
                                   vrt_hit* d_out_hit, uint64_t* d_counters, void* hip_stream) {
@@ -886,8 +936,10 @@ int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt
   Shard& s = ctx->sh[0];
   vrt::KArgs a = make_args(ctx, s, cam, p, row0, rows, row_step);
   a.pitch = int32_t(pitch);
+  hipEvent_t eb, ee;
+  launch_timing_events(ctx, eb, ee);
   launch(ctx, s, a, reinterpret_cast<float4*>(d_out_rgba), d_out_hit,
-         reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream));
+         reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream), eb, ee);
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
 }
@@ -919,8 +971,10 @@ int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, 
   a.prev = d_prev_rgba8;
   a.cur = d_cur_rgba8;
   a.raw = d_raw_rgba8;
+  hipEvent_t eb, ee;
+  launch_timing_events(ctx, eb, ee);
   launch(ctx, s, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
-         static_cast<hipStream_t>(hip_stream));
+         static_cast<hipStream_t>(hip_stream), eb, ee);
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
 }

@@ -60,6 +60,8 @@ CONTEXT = {
 }
 # multi-file experiments: name -> [(file, anchor, replacement), ...]
 MULTI = {
+    # tile order: the second pass in reverse row order (top of the frame first)
+    "pass2rev": [("vrt_render.hip", "  const uint32_t t = L - cap;\n", "  const uint32_t t = a.tiles - 1u - (L - cap);\n")],
     # bounce stacks without raised wave priority / at priority 1
     "noprio": [("vrt_render.hip", "    __builtin_amdgcn_s_setprio(kStackPrio);  // bounce stacks: the longest waves of a frame\n", "")],
     "prio1": [("vrt_render.hip", "constexpr int kStackPrio = 3;", "constexpr int kStackPrio = 1;")],

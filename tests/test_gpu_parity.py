@@ -251,3 +251,19 @@ def test_randomize_direction_bit_exact(renderer):
     got = renderer.debug_randomize(d[:64], p[:64], 0.0, 1.0)
     signs = np.signbit(got[:, 0])
     assert signs.any() and (~signs).any()
+
+
+@pytest.mark.parametrize("scene,n,R,T", [("refraction", 128, 4, 4), ("glass_cube", 128, 1, 2),
+                                         ("terrain", 128, 4, 2), ("terrain", 32, 4, 2)])
+def test_textured_fast_path_equals_exact_instance(renderer, scene, n, R, T):
+    """Stats-free textured frames (exact walks with certified shadow walks from the exact hit
+    points, CERT 1) equal the exact instance's bit for bit, with the reference atlas, at full
+    size; terrain 32^3 has glass walls (main.cpp:233)."""
+    vox = vrt.build_scene(scene, n)
+    renderer.upload_volume(vox, n)
+    cam = vrt.make_camera(1920, 1080)
+    p = vrt.textured_params(vrt.default_params(R, T), ref_atlas())
+    exact, _, _ = renderer.render(cam, p, want_hits=False, counters=True)
+    fast, _, st = renderer.render(cam, p, want_hits=False, counters=False)
+    assert st["kernel_ms"] > 0
+    assert np.array_equal(fast.view(np.uint32), exact.view(np.uint32))

@@ -2102,7 +2102,10 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // stats-free colour-only frames (vrt_set_certified): certified pixels (a.cert 2), certified
   // exact-path rays only (1: the certified primary's registers would slow glass-heavy frames by
   // ~5 %), exact walks only (0)
-  auto kern = a.textured ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
+  // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
+  // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
+  auto kern = a.textured ? (stats ? render_kernel<true, true>
+                                  : (a.cert >= 1 ? render_kernel<false, true, 1> : render_kernel<false, true>))
                          : (stats ? render_kernel<true, false>
                                   : (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true>
                                                             : render_kernel<false, false, 2>)

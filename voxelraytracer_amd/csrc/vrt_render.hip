@@ -1066,12 +1066,18 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     const int nx = cx + (a == 0 ? sx : 0), ny = cy + (a == 1 ? sy : 0), nz = cz + (a == 2 ? sz : 0);
     const uint32_t ntex = path_texel(c, nx, ny, nz, obase);
     const float ga = a == 0 ? gam.x : (a == 1 ? gam.y : gam.z);
-    // near-edge flags per other axis: ahead (crossed within the bound after s1) / behind (before)
+    // near-edge flags per other axis: ahead (crossed within the bound after s1) / behind (before).
+    // A plane behind counts down to -gam_b, not 0: a ray that starts ON a plane (a shadow or
+    // secondary ray from an exact hit point on the hit face) has that plane at parameter 0 up to
+    // rounding, and the exact walk's currentPos stays on it — sampling the voxel beyond it — until
+    // the ray has moved half an ulp of the coordinate off it (r02 s18: a shadow ray from
+    // (33.000008, 127, 37.02) sampled the panel voxel (32, 127, 37) at its first x crossing, and
+    // back.y rounded to just below 0 hid that alternative from the certified walk)
     const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
                ahz = a != 2 && sig.z - s1 < ga + gam.z;
-    const bool bhx = a != 0 && back.x >= 0.0f && s1 - back.x < ga + gam.x;
-    const bool bhy = a != 1 && back.y >= 0.0f && s1 - back.y < ga + gam.y;
-    const bool bhz = a != 2 && back.z >= 0.0f && s1 - back.z < ga + gam.z;
+    const bool bhx = a != 0 && back.x > -gam.x && s1 - back.x < ga + gam.x;
+    const bool bhy = a != 1 && back.y > -gam.y && s1 - back.y < ga + gam.y;
+    const bool bhz = a != 2 && back.z > -gam.z && s1 - back.z < ga + gam.z;
     const bool near = ahx | ahy | ahz | bhx | bhy | bhz;
     const uint32_t nb = ntex & kVoxMask;
     if (cert_event<SHADOW>(nb, medium)) {
@@ -1317,6 +1323,51 @@ __device__ __forceinline__ bool exact_start_cell(const Ctx& c, const f3 P, const
   return wpx == float(cx + (sx > 0)) && wpy == float(cy + (sy > 0)) && wpz == float(cz + (sz > 0));
 }
 
+// Cells the exact walk samples behind its start cell. A start coordinate P_a that is an integer k
+// with D_a < 0 (a shadow or secondary ray from an exact hit point on its face plane) makes the
+// start cell k - 1 on axis a, but until cur_a = P_a + s D_a rounds off k the exact walk samples
+// layer k — beyond the plane — at every crossing of another axis (r02 s18: a shadow ray from
+// (33.000008, 127, 37.02) going -x, -y sampled the panel voxel (32, 127, 37) at its x crossing
+// 8.5e-6 after the start; the certified walk had jumped that crossing). The certified walk cannot
+// see those cells, so they are checked here: every cell of layer k the walk may enter across an
+// axis crossed within 2 ulp(k) / |D_a| (+1e-5) of the start must be a non-event, else unsure.
+template <bool SHADOW>
+__device__ __forceinline__ bool start_layers_clear(const Ctx& c, const f3 P, const f3 D, int cx, int cy,
+                                                   int cz, uint32_t medium) {
+  const float p[3] = {P.x, P.y, P.z}, d[3] = {D.x, D.y, D.z};
+  const int cell[3] = {cx, cy, cz};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    if (!(d[a] < 0.0f) || p[a] != __builtin_floorf(p[a])) continue;
+    const float off = (0x1p-22f * __builtin_fmaxf(__builtin_fabsf(p[a]), 1.0f) + 1e-5f) / __builtin_fabsf(d[a]);
+    int q[3] = {cell[0], cell[1], cell[2]};
+    q[a] += 1;  // layer k
+    bool early[3] = {false, false, false};
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      if (b == a) continue;
+      const float plane = float(cell[b] + (d[b] > 0.0f ? 1 : 0));
+      early[b] = (plane - p[b]) / d[b] < off;  // first crossing of axis b
+    }
+    const int b1 = a == 0 ? 1 : 0, b2 = a == 2 ? 1 : 2;
+    const int s1 = d[b1] > 0.0f ? 1 : -1, s2 = d[b2] > 0.0f ? 1 : -1;
+    int r[3];
+    if (early[b1]) {
+      r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1;
+      if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+    }
+    if (early[b2]) {
+      r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b2] += s2;
+      if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+    }
+    if (early[b1] && early[b2]) {
+      r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1; r[b2] += s2;
+      if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+    }
+  }
+  return true;
+}
+
 // The shadow bit of an exact hit h by a certified walk: the shadow ray starts at the exact hit
 // point h.point with len h.len (GetShadowRay, :191-201), so its start is known exactly, as a
 // primary ray's is (e0 = 0, the exact walk's own start cell). 1 blocked, 0 lit, -1 unsure.
@@ -1324,6 +1375,7 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h) {
   const f3 S = c.sun_n;
   int cx, cy, cz;
   if (!fast_path_ok(S) || !exact_start_cell(c, h.point, S, cx, cy, cz)) return -1;
+  if (!start_layers_clear<true>(c, h.point, S, cx, cy, cz, 0u)) return -1;
   const CertResult s = cert_walk<true>(c, h.point, S, c.sun_rcp, c.max_len - h.len, cx, cy, cz, 0.0f,
                                        mk(0.0f, 0.0f, 0.0f), h.len, 0u);
   return s.res == CERT_UNSURE ? -1 : (s.res == CERT_HIT ? 1 : 0);
@@ -1353,7 +1405,8 @@ __device__ __forceinline__ bool cert_air_segment(const Ctx& c, const Ray& ray, i
 // its walk certifies as a primary's does
 __device__ __forceinline__ bool cert_secondary(const Ctx& c, const Ray& ray, f3& color) {
   int cx, cy, cz;
-  if (ray.voxel != 0u || !fast_path_ok(ray.dir) || !exact_start_cell(c, ray.pos, ray.dir, cx, cy, cz))
+  if (ray.voxel != 0u || !fast_path_ok(ray.dir) || !exact_start_cell(c, ray.pos, ray.dir, cx, cy, cz) ||
+      !start_layers_clear<false>(c, ray.pos, ray.dir, cx, cy, cz, 0u))
     return false;
   return cert_air_segment(c, ray, cx, cy, cz, mk(0.0f, 0.0f, 0.0f), color);
 }
@@ -1479,7 +1532,10 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
   const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
   int cx, cy, cz;
-  if (!exact_start_cell(c, P, D, cx, cy, cz)) { CERT_DIAG(0); return false; }
+  if (!exact_start_cell(c, P, D, cx, cy, cz) || !start_layers_clear<false>(c, P, D, cx, cy, cz, 0u)) {
+    CERT_DIAG(0);
+    return false;
+  }
   // hardware reciprocals (<= 1 ulp): the certified walk only needs its own error bounded
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
   CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f,

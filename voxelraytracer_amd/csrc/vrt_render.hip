@@ -1764,6 +1764,28 @@ __device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px,
   return ray;
 }
 
+// A scratch-stack entry: only reflection rays are stored (exact_pixel), whose medium is air
+// (reflection_ray sets voxel 0), with both depths (<= 16) in one word: 9 dwords instead of 11.
+struct StackRay {
+  f3 pos, dir;
+  float len, energy;
+  uint32_t depths;
+};
+__device__ __forceinline__ StackRay pack_stack_ray(const Ray& r) {
+  return StackRay{r.pos, r.dir, r.len, r.energy, uint32_t(r.rdepth) | (uint32_t(r.tdepth) << 16)};
+}
+__device__ __forceinline__ Ray unpack_stack_ray(const StackRay& e) {
+  Ray r;
+  r.pos = e.pos;
+  r.dir = e.dir;
+  r.len = e.len;
+  r.energy = e.energy;
+  r.voxel = 0;
+  r.rdepth = int32_t(e.depths & 0xffffu);
+  r.tdepth = int32_t(e.depths >> 16);
+  return r;
+}
+
 #ifdef VRT_STAMPS
 // Diagnostic build only: per wave {time after the exact primary trace, after the bounce stacks}
 constexpr int kMaxStampWaves3 = 1 << 18;
@@ -1780,7 +1802,7 @@ template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
-  Ray stack[kMaxStack];
+  StackRay stack[kMaxStack - 1];  // the top entry lives in `ray`
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
   const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
@@ -1798,19 +1820,31 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
     __builtin_amdgcn_s_setprio(kStackPrio);  // bounce stacks: the longest waves of a frame
     Hit h = h0;
     for (;;) {
-      const uint32_t m = mat_id(h.voxel);
+      // The reference pushes the reflection ray, then the refraction ray, then pops the top
+      // (:440-448). The ray pushed last is popped at once, so it goes straight to `ray` and only a
+      // reflection ray under a refraction ray is written to the scratch stack: same rays in the
+      // same order, same STACK_FULL cases (the cap counts the ray held in `ray` as an entry), and
+      // about half the scratch writes of a glass tree.
+      bool push_r = false, push_t = false;
       if (h.found) {
-        if (mat_reflective(m) && ray.rdepth < a.max_refl) {
-          if (sp < cap) stack[sp++] = reflection_ray(c, ray, h);
-          else flags |= VRT_HIT_FLAG_STACK_FULL;
-        }
-        if (mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f) {
-          if (sp < cap) stack[sp++] = refraction_ray<TEX>(c, ray, h, k);
-          else flags |= VRT_HIT_FLAG_STACK_FULL;
-        }
+        const uint32_t m = mat_id(h.voxel);
+        const bool pr = mat_reflective(m) && ray.rdepth < a.max_refl;
+        const bool pt = mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f;
+        push_r = pr && sp < cap;
+        push_t = pt && sp + int(push_r) < cap;
+        if ((pr && !push_r) || (pt && !push_t)) flags |= VRT_HIT_FLAG_STACK_FULL;
       }
-      if (sp == 0) break;
-      ray = stack[--sp];
+      if (push_r && push_t) {
+        stack[sp++] = pack_stack_ray(reflection_ray(c, ray, h));
+        ray = refraction_ray<TEX>(c, ray, h, k);
+      } else if (push_r) {
+        ray = reflection_ray(c, ray, h);
+      } else if (push_t) {
+        ray = refraction_ray<TEX>(c, ray, h, k);
+      } else {
+        if (sp == 0) break;
+        ray = unpack_stack_ray(stack[--sp]);
+      }
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
         bool settled;

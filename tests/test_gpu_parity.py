@@ -71,6 +71,10 @@ CASES = [
     ("glass_cube", 16, 15, 15, 4, 4, dict(pos=(0.25, 0.25, 0.25), rot=(-35.26439, 45.0, 0.0))),
     ("terrain", 32, 121, 121, 4, 2, dict(pos=(0.0, 5.0, 0.0), rot=(-90.0, 0.0, 0.0))),
     ("terrain", 512, 384, 216, 4, 2, {}),
+    # deep bounce trees (the largest stack the ABI accepts, R + T + 1 = 17): the stack order of
+    # reflection rays parked under refraction rays, tdepth-heavy and rdepth-heavy
+    ("glass_cube", 32, 128, 96, 4, 12, dict(pos=(0.5, 1.0, -2.5), rot=(-25.0, 15.0, 0.0))),
+    ("refraction", 64, 128, 72, 12, 4, dict(ray_noise=0.02, refraction_noise=0.02, time=5.0)),
 ]
 
 

@@ -1820,6 +1820,13 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
     __builtin_amdgcn_s_setprio(kStackPrio);  // bounce stacks: the longest waves of a frame
     Hit h = h0;
     for (;;) {
+      // The sun vector and its reciprocal are opaque per iteration (an empty asm on SGPR copies),
+      // so the compiler cannot hoist the per-lane products the loop body forms from them into
+      // VGPRs live across the whole loop: those were spilled per lane on loop entry. Scratch
+      // 832 -> 720 B per lane, WRITE_SIZE per C3 frame 17.2 -> 14.6 MB (DESIGN.md §6 "HBM writes").
+      Ctx lc = c;
+      asm volatile("" : "+s"(lc.sun_n.x), "+s"(lc.sun_n.y), "+s"(lc.sun_n.z), "+s"(lc.sun_rcp.x),
+                   "+s"(lc.sun_rcp.y), "+s"(lc.sun_rcp.z));
       // The reference pushes the reflection ray, then the refraction ray, then pops the top
       // (:440-448). The ray pushed last is popped at once, so it goes straight to `ray` and only a
       // reflection ray under a refraction ray is written to the scratch stack: same rays in the
@@ -1829,18 +1836,18 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       if (h.found) {
         const uint32_t m = mat_id(h.voxel);
         const bool pr = mat_reflective(m) && ray.rdepth < a.max_refl;
-        const bool pt = mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(c, h).w != 1.0f;
+        const bool pt = mat_transparent(m) && ray.tdepth < a.max_transp && get_color<TEX>(lc, h).w != 1.0f;
         push_r = pr && sp < cap;
         push_t = pt && sp + int(push_r) < cap;
         if ((pr && !push_r) || (pt && !push_t)) flags |= VRT_HIT_FLAG_STACK_FULL;
       }
       if (push_r && push_t) {
-        stack[sp++] = pack_stack_ray(reflection_ray(c, ray, h));
-        ray = refraction_ray<TEX>(c, ray, h, k);
+        stack[sp++] = pack_stack_ray(reflection_ray(lc, ray, h));
+        ray = refraction_ray<TEX>(lc, ray, h, k);
       } else if (push_r) {
-        ray = reflection_ray(c, ray, h);
+        ray = reflection_ray(lc, ray, h);
       } else if (push_t) {
-        ray = refraction_ray<TEX>(c, ray, h, k);
+        ray = refraction_ray<TEX>(lc, ray, h, k);
       } else {
         if (sp == 0) break;
         ray = unpack_stack_ray(stack[--sp]);
@@ -1848,15 +1855,15 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
         bool settled;
-        h = march_cert(c, ray, color, settled, k, steps, flags);
+        h = march_cert(lc, ray, color, settled, k, steps, flags);
         if (settled) {
           h.found = false;  // a miss or a hit without secondary rays
           continue;
         }
-        shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
+        shade<STATS, TEX, CSH>(lc, ray, h, color, k, steps, flags);
         continue;
       }
-      h = trace_with_shadow<STATS, TEX, false, CSH>(c, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH>(lc, ray, color, k, steps, flags);
     }
 #ifdef VRT_STAMPS
     {

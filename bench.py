@@ -10,17 +10,25 @@ ray-trace FBO and the temporal filter into the RGB8 history (main.cpp:363-393), 
 kernel epilogue (4 B history read + 4 B write per pixel); --output f32 writes vrt_render's float
 RGBA frame (16 B per pixel).
 
+Frames in flight: at u_Alpha = 1 (the slider default) a frame does not read its history, so
+consecutive frames are independent; the timed frames rotate over --lanes (default 4) lanes, each
+with its own HIP stream and output buffer, so up to four frames are in flight and the next frames'
+waves fill the wave slots one frame's longest (exact-path) waves hold (voxelraytracer_amd/tiles.py;
+scripts/diag/strong_pipe.py). At u_Alpha != 1 frames depend on their history: one lane, two
+interleaved row parts on two streams, filtered in place (the round-2 scheme).
+
 Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
-cyclic row bands (rank r owns rows r, r+N, ...); every rank renders and filters its band in place
-in HBM. The per-pixel program has no exchange step, so the timed frames run with no collective;
-after the timed region rank 0 gathers the last frame's bands over RCCL once (collect()).
---gather-frames gathers every frame to rank 0 inside the timed region instead (display delivery,
-pipelined so the gather of frame k overlaps the render of frame k+1). Default --scaling weak: with
-N ranks the frame is N*H rows of the same view (N-fold vertical sample density), so each rank
-renders exactly the config's W x H pixels; --scaling strong splits the config's frame N ways.
+cyclic row bands (rank r owns rows r, r+N, ...); every rank renders and filters its band in HBM.
+The per-pixel program has no exchange step, so the timed frames run with no collective; after the
+timed region rank 0 gathers the last frame's bands over RCCL once (collect()). --gather-frames
+gathers every frame to rank 0 inside the timed region instead (display delivery, one lane,
+pipelined so the gather of frame k overlaps the render of frame k+1). Default --scaling strong:
+the config's frame (C3: 1920x1080) is split N ways, the reference's one frame per draw
+(main.cpp:325-361) tiled across the GPUs; --scaling weak renders an N-fold taller frame of the same
+view instead (each rank a config-sized band; opt-in, no BASELINE config names that frame).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
-                       [--output rgba8|f32] [--alpha A] [--scaling weak|strong]
+                       [--output rgba8|f32] [--alpha A] [--scaling strong|weak] [--lanes L]
 """
 import argparse
 import json
@@ -30,12 +38,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4). One rank
-# does not depend on it (C3 0.0667 ms/frame at 4 queues, 0.0669 at 16, profiles/r02_s08); with
-# the RCCL and assembly streams of the multi-rank path there are more streams than 4 queues, so
-# ranks of a multi-GPU run raise it (before HIP initialises).
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4): the lanes'
+# streams (4 frames in flight), the main stream and, at N > 1, the RCCL streams need more than 4,
+# or two streams share a queue and serialise; 16 (before HIP initialises). Neutral for one stream
+# pair (C3 0.0667 ms/frame at 4 queues, 0.0669 at 16, profiles/r02_s08).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 CONFIGS = {
     # name: (scene, N, W, H, R, T, description)
@@ -74,9 +81,12 @@ def parse():
     ap.add_argument("--shading", default="color", choices=["color", "textured"],
                     help="color: _COLOR_ONLY materials (SURVEY §8d configs); textured: the "
                          "reference's default build, atlas shading (synthetic 256/128 atlas)")
-    ap.add_argument("--parts", type=int, default=2,
-                    help="interleaved row parts per rank, each on its own HIP stream, so one "
-                         "launch's tail overlaps the next part's launch (tiles.py)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="frames in flight per rank, each on its own stream(s) and output buffer "
+                         "(tiles.py); 0: 4 at alpha 1 (frames independent), else 1")
+    ap.add_argument("--parts", type=int, default=0,
+                    help="interleaved row parts per frame, each on its own HIP stream (tiles.py); "
+                         "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
@@ -86,9 +96,9 @@ def parse():
                     help="N > 1: gather every frame's bands to rank 0 over RCCL inside the timed "
                          "region (display delivery); default: bands stay on their ranks, one "
                          "gather after the timed region")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: N ranks render an N-fold taller frame (each a config-sized band); "
-                         "strong: the config's frame is split N ways")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the config's frame is split N ways (default); weak (opt-in): N "
+                         "ranks render an N-fold taller frame (each a config-sized band)")
     return ap.parse_args()
 
 
@@ -229,10 +239,16 @@ def main():
     def render_band(row0, rows, step, out, prev):
         launch(row0, rows, step, out, prev)
 
-    parts = args.parts if frame_h % (world * args.parts) == 0 else 1
+    lanes = args.lanes or (4 if args.alpha == 1.0 and not args.gather_frames else 1)
+    if args.gather_frames and lanes > 1:
+        raise SystemExit("--gather-frames renders one frame at a time (--lanes 1)")
+    parts = args.parts or (1 if lanes > 1 else 2)
+    parts = parts if frame_h % (world * parts) == 0 else 1
+    # independent frames: at alpha 1 the kernel does not read the history (tiles.py)
     tiler = FrameTiler(w, frame_h, render_band, dev,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
-                       gather=args.gather_frames)
+                       gather=args.gather_frames, lanes=lanes,
+                       independent=rgba8 and args.alpha == 1.0 or not rgba8)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -278,8 +294,8 @@ def main():
     frame_gpu_ms = ev0.elapsed_time(ev1) / args.steps
     # Launch-timing pass (after the timed region, the same FrameTiler path): the mean duration of
     # one render_kernel launch — what rocprofv3 reports per kernel — from the kernels' own device
-    # start / end timestamps (vrt_set_launch_timing: hipExtLaunchKernelGGL events; the `parts`
-    # launches of a frame overlap, so a launch lasts longer than frame_gpu_ms / parts). Not in the
+    # start / end timestamps (vrt_set_launch_timing: hipExtLaunchKernelGGL events; launches of
+    # frames in flight overlap, so a launch lasts longer than frame_gpu_ms / parts). Not in the
     # timed region: the per-launch events cost ~8 % of the frame rate (r02 s17).
     lt_frames = max(20, min(args.steps, 200))
     ren.set_launch_timing(lt_frames * parts)
@@ -295,27 +311,32 @@ def main():
     elapsed, frame_ms_max = t.tolist()
 
     # Check of the timed path (after all timing): the next `verify_frames` frames through the same
-    # FrameTiler (parts on their streams, pitched in place, tile order seeded by the frames before
+    # FrameTiler (lanes and parts on their streams, tile order seeded by the frames before
     # them, certified walks), each against the exact STATS instance (exact walks, counters on)
     # rendering the same rows from a copy of the same history: the stored bytes (or float frame)
     # must be equal. Single rank: the frames and their histories are kept for the oracle check.
     verify = None
     pairs = []   # (history before, frame after) of each verified frame, host copies
+
+    def last_parts():   # this rank's part buffers of the last frame enqueued
+        if tiler.gather:
+            band = tiler.bands[(tiler.k - 1) % 2]
+            return [band[s_] for s_ in range(parts)]
+        return [tiler.part_rows(tiler.last(), s_) for s_ in range(parts)]
+
     if not args.no_verify:
-        nb = len(tiler.bands)
         bad = 0
         total = 0
         vc = torch.zeros_like(cnt)
         for _ in range(max(1, args.verify_frames)):
-            last = tiler.bands[(tiler.k - 1) % nb]
-            prev_parts = [tiler._part_buffers(s_, last, last)[0].clone() for s_ in range(parts)]
-            prev_full = tiler.frame_buf.clone() if world == 1 and tiler.frame_buf is not None else None
+            tiler.finish()
+            prev_parts = [t_.clone() for t_ in last_parts()]   # the next frame's history
+            prev_full = tiler.last().clone() if world == 1 and not tiler.gather else None
             tiler.frame()
             tiler.finish()
             torch.cuda.synchronize(dev)
-            newest = tiler.bands[(tiler.k - 1) % nb]
             for s_, (row0, rows, step) in enumerate(tiler.specs):
-                got = tiler._part_buffers(s_, newest, newest)[0].contiguous()
+                got = last_parts()[s_].contiguous()
                 ref = torch.zeros_like(got)
                 prev_c = prev_parts[s_].contiguous()
                 launch(row0, rows, step, ref, prev_c, vc.data_ptr())   # counters on: STATS instance
@@ -323,7 +344,7 @@ def main():
                 bad += int((got != ref).sum().item())
                 total += got.numel()
             if prev_full is not None:
-                pairs.append((prev_full.cpu().numpy(), tiler.frame_buf.cpu().numpy()))
+                pairs.append((prev_full.cpu().numpy(), tiler.last().cpu().numpy()))
         verify = {"verified": bad == 0, "frames": max(1, args.verify_frames),
                   "mismatched_elements": bad, "elements": total,
                   "against": "exact walks (STATS instance, counters on) on a copy of the same "
@@ -351,15 +372,19 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
-        # Roofline of the dominant kernel, per launch (as rocprofv3 reports it): this rank's
-        # algorithmic bytes of one part launch over the mean launch duration. The algorithmic
-        # bytes are the reference's: 1 B per DDA step of its walk + 2 B per refraction probe + the
-        # pixel bytes; the certified walks read only a few texels per pixel, so this
-        # is a reference-normalised rate, not a bandwidth. What binds the kernel is VALU issue and
-        # dependency latency (valu_issue below); the measured HBM traffic is hbm_frac.
+        # Roofline of the dominant kernel (render_kernel). Algorithmic bytes are the reference's:
+        # 1 B per DDA step of its walk + 2 B per refraction probe + the pixel bytes;
+        # the certified walks read only a few texels per pixel, so this is a reference-normalised
+        # rate, not a bandwidth. What binds the kernel is VALU issue and dependency latency
+        # (valu_issue below); the measured HBM traffic is hbm_frac. Per launch (what rocprofv3
+        # reports per kernel): this rank's bytes of one launch over the mean launch duration. With
+        # frames in flight, launches overlap (launches_in_flight on average), so the GPU's rate is
+        # the per-launch rate times that: this rank's bytes per frame / GPU time per frame.
         own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
         bytes_per_launch = float(np.mean(part_bytes))
-        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        per_launch = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        in_flight = launch_ms * parts / frame_gpu_ms
+        achieved = own_bytes / (frame_gpu_ms * 1e-3) / 1e9
         lib_hash = lib_sha256()
         traffic = traffic_frame = hbm_frac = None
         valu = None
@@ -416,6 +441,10 @@ def main():
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
             "value": round(value, 3),
+            "value_is": ("rays of the reference's ray tree per frame (primary + secondary stack "
+                         "pops + shadow rays, counted by the exact-walk instance) x frames / wall "
+                         "time of the timed frames, all ranks: output-equivalent throughput (the "
+                         "timed certified kernel walks fewer rays and steps for the same image)"),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -443,10 +472,12 @@ def main():
                            % args.alpha) if rgba8 else "float RGBA",
                 "parallelism": ((f"cyclic row bands x{world} + RCCL gather to rank 0 every frame"
                                  if args.gather_frames else
-                                 f"cyclic row bands x{world}, no collective in the timed region "
-                                 "(one RCCL gather of the last frame after it)")
+                                 f"cyclic row bands x{world} ({args.scaling} scaling), no collective "
+                                 "in the timed region (one RCCL gather of the last frame after it)")
                                 if world > 1 else "single GPU, whole frame")
-                               + f", {parts} interleaved row parts on {parts} HIP streams",
+                               + (f", {lanes} frames in flight (lanes)" if lanes > 1 else "")
+                               + f", {parts} interleaved row part{'s' if parts > 1 else ''} per "
+                               f"frame on {lanes * parts} HIP stream{'s' if lanes * parts > 1 else ''}",
                 "rays_per_frame": rays_per_frame,
                 "algorithmic_bytes_per_frame": bytes_per_frame,
             },
@@ -454,8 +485,13 @@ def main():
                 "bound": "valu-issue/latency",
                 "achieved": round(achieved, 2),
                 "achieved_is": ("reference-normalised algorithmic bytes (1 B per DDA step of the "
-                                "reference walk + 2 B per refraction probe + pixel bytes) of one "
-                                "render_kernel launch / its mean duration; not a bandwidth"),
+                                "reference walk + 2 B per refraction probe + pixel bytes) of this "
+                                "rank's frame / GPU time per frame = per-launch rate x launches in "
+                                "flight; not a bandwidth"),
+                "achieved_per_launch": round(per_launch, 2),
+                "achieved_per_launch_is": ("bytes of one render_kernel launch / its mean duration "
+                                           "(launch_ms, as rocprofv3 reports it)"),
+                "launches_in_flight": round(in_flight, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -472,10 +508,11 @@ def main():
                                  "timestamps (hipExtLaunchKernelGGL events, vrt_set_launch_timing) "
                                  "over a pass of the same frames after the timed region"),
                 "launches_per_frame": parts,
+                "lanes": lanes,
                 "kernel_ms": round(frame_gpu_ms, 4),
-                "kernel_ms_is": (f"GPU time per frame of this rank: {parts} concurrent "
-                                 "render_kernel launches (interleaved row parts on separate "
-                                 "streams), HIP events around the K timed frames"),
+                "kernel_ms_is": (f"GPU time per frame of this rank in the steady state ({lanes} "
+                                 f"frame(s) in flight, {parts} launch(es) per frame): HIP events "
+                                 "around the K timed frames on the main stream / K"),
                 "kernel_ms_max_over_ranks": round(frame_ms_max, 4),
                 "valu_issue": valu,
                 "lib_sha256": lib_hash[:16],

@@ -16,8 +16,11 @@
  *   - Images are W*H RGBA float, row 0 = bottom row (GL window convention).
  *   - A context spans one or more GPUs (vrt_create's device mask). Whole-frame entry points
  *     (vrt_render, vrt_render_frame, vrt_render_frame_device) split the frame into cyclic row
- *     bands, one per device, each rendered as two interleaved row parts on two context-owned
- *     streams; the *_async band entry points run on the context's first (root) device.
+ *     bands, one per device, rendered on context-owned streams: frame f on lane f % 4. A frame
+ *     that runs alone (synchronous calls) or reads its history is two interleaved row parts on
+ *     two streams; a device-output frame at u_Alpha = 1 is one launch per band, and up to four
+ *     of them are in flight (ABI v9). The *_async band entry points run on the context's first
+ *     (root) device.
  */
 #ifndef VRT_H
 #define VRT_H
@@ -28,7 +31,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 8
+#define VRT_ABI_VERSION 9
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -203,11 +206,11 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
  * same XCD as before, the last to finish first, so the frame's longest waves start first.
  * Launches on a stream that is being captured into a graph use dispatch order. Every tile is
  * rendered exactly once in any case: images are identical with and without it.
- * ABI v8: the state is a pool allocated by vrt_create (8 slots of 5 x 65536 words + a header:
- * bands up to 65536 tiles, i.e. 4096 x 2048 pixels; larger bands use dispatch order), zeroed on the
- * launch stream when a slot is (re)assigned; reusing a slot on another stream waits for its last
- * launch on the device (hipStreamWaitEvent), not on the host — unless the caller has destroyed
- * that stream, when the device is synchronised once. */
+ * ABI v8: the state is a pool allocated by vrt_create (ABI v9: 16 slots of 5 x 65536 words + a
+ * header: bands up to 65536 tiles, i.e. 4096 x 2048 pixels; larger bands use dispatch order), a
+ * slot per (band, stream), zeroed on the launch stream when it is (re)assigned. Reassigning the
+ * least recently used slot (more than 16 band/stream pairs in use) synchronises the device once
+ * (ABI v9: the old stream is never touched; its owner may have destroyed it). */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
@@ -297,8 +300,9 @@ int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam,
  * context: render, filter against the last filtered frame, copy the new filtered frame to the
  * HOST buffer out_rgba8 (W*H*4 bytes). The history starts black and restarts black when the image
  * size changes. stats may be NULL. Each device renders its row band as two interleaved parts on
- * its two context-owned streams (one launch's tail overlaps the other's) and filters it in
- * place; the bands are copied straight into the host rows (no device-side gather). */
+ * two context-owned streams (one launch's tail overlaps the other's); ABI v9: every device's DMA
+ * engine writes its band straight into its rows of a pinned staging frame owned by the context
+ * (the k copies run in parallel), which is then copied to out_rgba8. */
 int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params, float alpha,
                      uint8_t* out_rgba8, vrt_stats* stats);
 
@@ -308,15 +312,19 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* para
  * (e.g. the texture upload / blit of main.cpp:379-385) sees the frame. The frame stays valid until
  * the fourth later call, which overwrites it only after the work the caller had enqueued on
  * hip_stream before the next call. One device: the frame is rendered straight into that buffer
- * (no copy) and consecutive frames overlap on the GPU; several devices: the bands are gathered to
- * the first one over xGMI by ncclGather (rccl.h) and placed into their rows by strided copies.
+ * (no copy); several devices: the bands are gathered to the first one over xGMI by ncclGather
+ * (rccl.h) and placed into their rows by strided copies. Consecutive frames overlap on the GPU:
+ * at u_Alpha = 1 a frame does not read its history and up to four frames are in flight (ABI v9);
+ * otherwise part q of a frame waits only for part q of the frame before (its history rows).
  * Returns after the launches; stats may be NULL (then no host sync happens; with stats the call
  * waits for the frame). */
 int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
                             float alpha, void* hip_stream, const uint32_t** d_frame,
                             vrt_stats* stats);
 
-/* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history. */
+/* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history of
+ * the next frame. ABI v9: no buffer changes hands (a device-output frame the caller holds keeps
+ * its contents and lifetime). */
 int vrt_history_reset(vrt_ctx* ctx);
 
 /* ---- host-side scene harness (mirrors src/main.cpp; no GPU needed) ----------------------- */

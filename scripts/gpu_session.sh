@@ -2,7 +2,7 @@
 # One gpurun call built from named steps (each under its own time limit; the call stops at the
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
-# steps: tests | smoke | bench[:CFG] | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
+# steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
 #        sq[:CFG] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
@@ -31,6 +31,7 @@ for st in "$@"; do
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench_${arg:-C3} 300 python bench.py --config ${arg:-C3} ;;
+    drv) run drv_${arg:-C3} 300 python bench.py --config ${arg:-C3} --steps 20 --warmup 5 ;;
     ab) run ab 600 python -u scripts/ab.py --rounds 8 --configs ${arg:-C1,C2,C3,C4} ;;
     benchvar)
       for lib in $(libs); do

@@ -107,7 +107,7 @@ def test_frame_device_output(built, devs):
             s.wait_stream(torch.cuda.current_stream())
             ptr, t = r.render_frame_device(cam, vrt.default_params(R, T, time=float(i + 1)), a,
                                            s.cuda_stream, timing=(i == 1))
-            ms = ms or t
+            ms = ms or (t["kernel_ms"] if t else None)
             ptrs.append(ptr)
             if i >= 3:   # frame i-3 is still valid after frame i
                 torch.cuda.current_stream().wait_stream(s)
@@ -117,6 +117,78 @@ def test_frame_device_output(built, devs):
                     assert np.array_equal(got, ref[j]), f"frame {j} read after frame {i}"
         assert ms is not None and ms > 0
         assert len(set(ptrs[:4])) == 4 and ptrs[4] == ptrs[0]
+
+
+@pytest.mark.parametrize("devs", [0, [0, 0]], ids=["k1", "k2"])
+def test_device_frames_mixed_counted_and_alpha(built, devs):
+    """Device-output frames in flight (u_Alpha = 1: one launch per frame on rotating lanes) mixed
+    with counted frames (the exact instance, one launch) and u_Alpha < 1 frames (two parts, each
+    waiting for its history rows on another lane), plus a synchronous frame in between: every
+    frame equals the synchronous sequence (a counted frame after uncounted device
+    frames must be ordered after all of them)."""
+    scene, n, w, h, R, T = "refraction", 128, 320, 181, 4, 4
+    alphas = [1.0, 1.0, 0.5, 1.0, 1.0, 0.5, 0.6, 1.0, 1.0, 1.0, 0.5, 1.0]
+    counted = {2, 4, 9}
+    sync_at = {6}
+    ref = sequence(0, scene, n, w, h, R, T, alphas)
+    with vrt.Renderer(devs) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        cam = vrt.make_camera(w, h)
+        s = torch.cuda.Stream()
+        for i, a in enumerate(alphas):
+            p = vrt.default_params(R, T, time=float(i + 1))
+            if i in sync_at:
+                f, _ = r.render_frame(cam, p, a)
+                assert np.array_equal(f, ref[i]), f"sync frame {i}"
+                continue
+            ptr, st = r.render_frame_device(cam, p, a, s.cuda_stream, counters=i in counted)
+            if i in counted:
+                assert st["pixels"] == w * h
+            torch.cuda.current_stream().wait_stream(s)
+            got = np.empty((h, w, 4), np.uint8)
+            hipcopy(got, ptr)
+            assert np.array_equal(got, ref[i]), f"frame {i}"
+
+
+@pytest.mark.parametrize("alpha", [0.5, 1.0])
+def test_history_reset_keeps_held_frames(built, alpha):
+    """Key F (vrt_history_reset, main.cpp:417-421) between device-output frames: the next frame
+    filters against the last ray-traced frame, and the frames the caller still holds (valid until
+    the fourth later call) keep their contents (the reset used to swap a held ring
+    slot into the raw buffer, which the next frame overwrote)."""
+    scene, n, w, h, R, T = "refraction", 128, 256, 144, 4, 4
+    frames, reset_before = 7, 4
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        cam = vrt.make_camera(w, h)
+        # reference through the band API: raw (quantised) and filtered frames, explicit history
+        hist = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
+        raw_prev = None
+        refs = []
+        cs = torch.cuda.current_stream().cuda_stream
+        for i in range(frames):
+            p = vrt.default_params(R, T, time=float(i + 1))
+            prev = raw_prev if i == reset_before else hist
+            cur = torch.zeros_like(hist)
+            raw = torch.zeros_like(hist)
+            r.render_temporal_rows_async(cam, p, alpha, 0, h, 1, prev.data_ptr(), cur.data_ptr(),
+                                         raw.data_ptr(), stream=cs)
+            torch.cuda.synchronize()
+            refs.append(cur.cpu().numpy())
+            hist, raw_prev = cur, raw
+        s = torch.cuda.Stream()
+        ptrs = []
+        for i in range(frames):
+            if i == reset_before:
+                r.history_reset()
+            ptr, _ = r.render_frame_device(cam, vrt.default_params(R, T, time=float(i + 1)), alpha,
+                                           s.cuda_stream)
+            ptrs.append(ptr)
+            torch.cuda.current_stream().wait_stream(s)
+            for j in range(max(0, i - 3), i + 1):   # every frame still held
+                got = np.empty((h, w, 4), np.uint8)
+                hipcopy(got, ptrs[j])
+                assert np.array_equal(got, refs[j]), f"frame {j} read after frame {i}"
 
 
 def hipcopy(dst: np.ndarray, ptr: int):
@@ -134,8 +206,9 @@ def hipcopy(dst: np.ndarray, ptr: int):
 def test_headless_app_gets_the_bench_frame_time(built, tmp_path):
     """vrt_headless (C++ over the C-ABI) at C3 in its display-path mode (--pipelined:
     vrt_render_frame_device into a device buffer, no per-frame host sync): GPU time per frame within
-    10 % of bench.py's per-frame GPU time of the same workload (both uncounted, certified, two
-    parts), the C++ host with HIP's default hardware-queue count. The synchronous loop
+    10 % of bench.py's per-frame GPU time of the same workload (both uncounted, certified, four
+    frames in flight), the C++ host raising HIP's hardware-queue count itself as INTEGRATION.md
+    asks (no GPU_MAX_HW_QUEUES in its environment). The synchronous loop
     (vrt_render_frame, which waits for each frame as the reference's blocking GL timer query did)
     reports each frame's own GPU time, which includes the frame's tail that consecutive frames
     hide; its frames are identical."""

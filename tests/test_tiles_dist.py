@@ -24,7 +24,8 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1, gather=True):
+def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1, gather=True,
+           lanes=1):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -54,7 +55,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
 
     tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
                        dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts,
-                       gather=gather)
+                       gather=gather, lanes=lanes)
     got = []
     for _ in range(frames):
         f = tiler.frame()
@@ -201,6 +202,83 @@ def test_distributed_bands_without_per_frame_gather(built, world, parts):
     port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
                                               parts, False)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, _ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    hist = np.zeros((h, w, 4), np.uint8)
+    assert len(got) == frames
+    for t in range(frames):
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert np.array_equal(got[t], hist), t
+
+
+@pytest.mark.parametrize("lanes,parts,independent", [(3, 1, False), (2, 2, False), (4, 1, True)])
+def test_single_rank_lanes(built, lanes, parts, independent):
+    """Frames in flight (bench.py's default at alpha 1): frame k renders into lane k % L's buffer
+    and reads its history from the previous lane's. Dependent lanes (alpha 0.5) must give the
+    single-buffer filtered sequence; independent lanes (alpha 1: the history is not read) the
+    quantised frames. Each returned band is the frame, and stays valid for L - 1 more frames."""
+    import oracle
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import FrameTiler
+
+    n, w, h, frames = 16, 20, 12, 6
+    alpha = 1.0 if independent else 0.5
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    state = {"i": 0}
+
+    def render_band(row0, rows, step, out, prev):
+        p = vrt.default_params(1, 2, time=float(state["i"] // parts + 1), ray_noise=0.05)
+        rgba, _, _ = oracle.render(cam, vox, n, p, row0=row0, rows=rows, row_step=step)
+        old = np.full_like(prev.numpy(), 77) if independent else prev.numpy().copy()
+        _, cur = oracle.temporal(rgba, old, alpha)   # alpha 1: independent of the history
+        out.copy_(torch.from_numpy(cur))
+        state["i"] += 1
+
+    tiler = FrameTiler(w, h, render_band, torch.device("cpu"), dtype=torch.uint8, parts=parts,
+                       lanes=lanes, independent=independent)
+    hist = np.zeros((h, w, 4), np.uint8)
+    kept = []
+    for t in range(frames):
+        f = tiler.frame()
+        kept.append((f, tiler.last()))
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert f is tiler.bufs[t % lanes] and kept[-1][1] is f
+        assert np.array_equal(f.numpy(), hist), t
+    assert np.array_equal(tiler.finish().numpy(), hist)
+
+
+def test_lanes_need_kept_bands():
+    from voxelraytracer_amd.tiles import FrameTiler
+
+    with pytest.raises(ValueError):
+        FrameTiler(8, 4, lambda *a: None, torch.device("cpu"), lanes=0)
+
+
+@pytest.mark.parametrize("world,lanes", [(2, 2), (2, 3)])
+def test_distributed_lanes(built, world, lanes):
+    """Several ranks keeping their bands, each with frames in flight (bench.py's multi-GPU
+    default at alpha 1, here with dependent lanes at alpha 0.5): the collected frames equal the
+    single-process sequence."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h, frames, alpha = 16, 20, 12, 4, 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
+                                              1, False, lanes)) for r in range(world)]
     for p in procs:
         p.start()
     got, _ = q.get(timeout=120)

@@ -328,17 +328,25 @@ class Renderer:
         return out, stats
 
     def render_frame_device(self, cam: Camera, params: Params, alpha: float, stream: int = 0,
-                            timing: bool = False):
+                            timing: bool = False, counters: bool = False):
         """vrt_render_frame_device: the next filtered frame for display, on the first device,
         ordered on `stream`. Returns (device pointer of the W*H RGBA8 frame, owned by the context
-        and valid until the fourth later call; kernel_ms or None). timing=True waits for the frame."""
-        st = abi.Stats() if timing else None
+        and valid until the fourth later call; stats dict or None). timing or counters wait for
+        the frame (counters run the exact-walk instance); the dict then holds kernel_ms (and the
+        counters)."""
+        st = abi.Stats() if (timing or counters) else None
+        if st is not None:
+            st.request = abi.VRT_STATS_COUNTERS if counters else 0
         ptr = C.c_void_p()
         self._check(self._lib.vrt_render_frame_device(self._h, C.byref(cam), C.byref(params), alpha,
                                                       stream or None, C.byref(ptr),
                                                       C.byref(st) if st is not None else None),
                     "vrt_render_frame_device")
-        return ptr.value, (float(st.kernel_ms) if st is not None else None)
+        if st is None:
+            return ptr.value, None
+        stats = counters_dict(st.counters)
+        stats["kernel_ms"] = float(st.kernel_ms)
+        return ptr.value, stats
 
     def set_launch_timing(self, launches: int):
         """vrt_set_launch_timing: device start/end timestamps for the next `launches` async band

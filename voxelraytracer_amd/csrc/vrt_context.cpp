@@ -1,16 +1,19 @@
 // vrt_context.cpp — the C-ABI context of include/vrt.h around the kernels of vrt_render.hip.
 //
 // A context spans the devices of its mask. Every device holds a "shard": a
-// replica of the volume in the kernel's packed layout, two context-owned part streams, its row
-// band's history / ray-trace / float buffers, counters and the tile-order pool. Whole-frame entry
-// points split the frame into cyclic row bands (device j renders rows j, j+k, ...; sky and
-// geometry rows balance across devices) and each band into two interleaved row parts, one per
-// part stream, so one launch's last dispatch round overlaps the other's (DESIGN.md §6 "Tail
-// hiding"). The reference's single GL draw (main.cpp:323-361) becomes 2k concurrent launches.
-// The only exchange is the output: host outputs are written by each device straight into its
-// host rows (k PCIe links in parallel, no device hop); the device-output frame is gathered to
-// the first device with ncclGather over xGMI (rccl.h:745). The volume reaches the other devices
-// by ncclBroadcast from the first one.
+// replica of the volume in the kernel's packed layout, kLanes lanes of context-owned streams, its
+// row band's history / ray-trace / float buffers, counters and the tile-order pool. Whole-frame
+// entry points split the frame into cyclic row bands (device j renders rows j, j+k, ...; sky and
+// geometry rows balance across devices). Frame f renders on lane f % kLanes: device-output frames
+// that do not read their history (u_Alpha = 1) are one launch per band and up to kLanes of them are
+// in flight, the next frames' waves filling the slots one frame's longest waves hold; frames that
+// run alone or read their history are two interleaved row parts, whose launches overlap each
+// other's tails (DESIGN.md §6 "Tail hiding", §8 "Frames in flight"). The reference's single GL
+// draw (main.cpp:323-361) becomes k (or 2k) concurrent launches.
+// The only exchange is the output: synchronous host outputs are written by each device's DMA
+// engine straight into its rows of a pinned staging frame (k links in parallel, no device hop);
+// the device-output frame is gathered to the first device with ncclGather over xGMI
+// (rccl.h:745). The volume reaches the other devices by ncclBroadcast from the first one.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -26,9 +29,19 @@
 
 namespace {
 
-constexpr int kParts = 2;              // interleaved row parts per device band
-constexpr int kOrderSlots = 8;         // tile-order buffers per device (band geometry x stream)
-constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 4096 x 4096 pixels
+constexpr int kParts = 2;              // interleaved row parts of a frame that runs alone
+// Whole frames rotate over kLanes lanes: frame f renders on lane f % kLanes (kParts streams and
+// timing events of its own) into history ring slot f % kRing. At u_Alpha = 1 a frame does not read
+// its history, so consecutive device-output frames are independent and up to kLanes of them are in
+// flight: the light waves of the next frames fill the wave slots one frame's exact-path waves hold
+// (C3 0.0618 -> 0.0599 ms per frame on one GPU, C3's band at k = 8 GPUs 0.0416 -> 0.0112 ms;
+// scripts/diag/strong_pipe.py, profiles/r03_pipe). Such frames are one launch (a second part
+// only adds launch overhead once other frames fill the tail); frames that run alone (synchronous
+// calls) or read their history (u_Alpha != 1: part q of frame f waits for part q of frame f - 1)
+// are kParts interleaved parts, whose launches overlap each other's tails.
+constexpr int kLanes = 4;
+constexpr int kOrderSlots = 16;        // tile-order buffers per device (band geometry x stream)
+constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 65536 16x8 tiles (4096 x 2048 pixels)
 constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 2u * vrt::kOrdClasses;  // KArgs::order
 // first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
 // 8160 tiles are heavy)
@@ -40,14 +53,14 @@ constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 
 #endif
 // Filtered frames rotate through kRing buffers: frame f reads ring[(f-1) % kRing] (the temporal
 // history) and writes ring[f % kRing]. A device-output frame (vrt_render_frame_device) is handed
-// to the caller as its ring buffer and stays valid for two more frames with no copy.
+// to the caller as its ring buffer and stays valid until the fourth later call, with no copy.
 constexpr int kRing = 4;
+static_assert(kRing % kLanes == 0, "a ring slot is always written from the same lane");
 
 struct OrderSlot {
   int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
   hipStream_t stream = nullptr;
   uint32_t* d = nullptr;       // kOrderSlotWords words inside the shard's pool
-  hipEvent_t done = nullptr;   // recorded on the slot's stream when the slot is handed over
   bool used = false;
   uint64_t epoch = 0, tick = 0;
 };
@@ -65,17 +78,22 @@ struct Shard {
   // counters
   unsigned long long* d_cnt = nullptr;      // VRT_CNT_COUNT totals of a synchronous render
   unsigned long long* d_cnt_rep = nullptr;  // kCntReplicas x VRT_CNT_COUNT, kept zeroed
-  // streams and events of whole-frame renders
-  hipStream_t part[kParts] = {nullptr, nullptr};
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;  // frame begin / end on part[0] (ordering)
-  hipEvent_t ev_join = nullptr;                      // part[1] done / caller-stream marker
-  hipEvent_t ev_pdone[kParts] = {nullptr, nullptr};  // a part of a device-output frame is done
-  // GPU time of each part launch: recorded when the kernel starts / ends on the device
-  hipEvent_t ev_kbeg[kParts] = {nullptr, nullptr}, ev_kend[kParts] = {nullptr, nullptr};
-  bool timed[kParts] = {false, false};               // parts launched by the last frame
+  // whole-frame lanes: streams, and per lane the events of its last frame's launches
+  hipStream_t ls[kLanes][kParts] = {};
+  hipEvent_t ev_done[kLanes][kParts] = {};
+  int lane_parts[kLanes] = {};       // launches of the lane's last frame (0: none)
+  bool lane_hist[kLanes] = {};       // the lane's last frame read its history ring slot
+  hipStream_t gs = nullptr;          // gather / assembly / host-copy stream
+  hipEvent_t ev_gs = nullptr;        // marker on gs (volume upload ordering, gather done)
+  hipEvent_t ev_band_read[kRing] = {};  // gs has read ring slot s (device-output gather)
+  bool band_read_valid[kRing] = {};
+  // GPU time of each launch of the last synchronous frame: recorded when the kernel starts /
+  // ends on the device
+  hipEvent_t ev_kbeg[kParts] = {}, ev_kend[kParts] = {};
+  bool timed[kParts] = {};
   // this device's row band of the whole-frame buffers (band_cap rows x width)
-  uint32_t* d_ring[kRing] = {};  // filtered bands (history ring)
-  uint32_t* d_raw = nullptr;   // quantised ray-trace band (the rayTrace FBO; key F)
+  uint32_t* d_ring[kRing] = {};      // filtered bands (history ring)
+  uint32_t* d_rawbuf[kRing] = {};    // quantised ray-trace band of frame f (rayTrace FBO; key F)
   size_t hist_pixels = 0;
   float4* d_out = nullptr;     // vrt_render's float band
   vrt_hit* d_hit = nullptr;
@@ -107,15 +125,18 @@ struct vrt_ctx {
                                         // re-uploaded when its bytes differ, not by identity)
   int32_t hist_w = 0, hist_h = 0;       // image size of the resident whole-frame history
   uint64_t fk = 0;                      // frames rendered into the resident history
+  bool raw_is_cur[kRing] = {};          // frame in slot s had u_Alpha = 1: its raw frame = ring[s]
+  bool reset_pending = false;           // vrt_history_reset: the next frame's history is the raw frame
   uint32_t* d_gather = nullptr;         // first device: k x band_cap x width words (ncclGather)
   size_t hist_pixels_gather = 0;
-  uint32_t* d_frames[kRing] = {};  // first device, k > 1: assembled frames
+  uint32_t* d_frames[kRing] = {};       // first device, k > 1: assembled frames
   // caller stream, device-output frames: E_f = ev_consumed[f % kRing], recorded at call f, marks
   // the caller's work enqueued before call f (its consumption of frames <= f - 1)
   hipEvent_t ev_consumed[kRing] = {};
   bool consumed_valid[kRing] = {};
   hipEvent_t ev_gathered = nullptr;     // first device: the last device-output frame is assembled
-  bool gather_pending = false;
+  void* h_stage = nullptr;              // pinned host staging of synchronous frames (k bands in)
+  size_t h_stage_bytes = 0;
   std::string err;
 };
 
@@ -170,18 +191,29 @@ PartRows part_rows(int32_t height, int32_t k, int32_t parts, int32_t j, int32_t 
 
 void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
-  for (void* p : {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats, (void*)s.d_cnt,
-                  (void*)s.d_cnt_rep, (void*)s.d_ring[0], (void*)s.d_ring[1], (void*)s.d_ring[2],
-                  (void*)s.d_ring[3], (void*)s.d_raw, (void*)s.d_out, (void*)s.d_hit,
-                  (void*)s.d_atlas, (void*)s.d_order_pool})
+  std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats,
+                             (void*)s.d_cnt, (void*)s.d_cnt_rep, (void*)s.d_out, (void*)s.d_hit,
+                             (void*)s.d_atlas, (void*)s.d_order_pool};
+  for (int r = 0; r < kRing; ++r) {
+    bufs.push_back(s.d_ring[r]);
+    bufs.push_back(s.d_rawbuf[r]);
+  }
+  for (void* p : bufs)
     if (p) (void)hipFree(p);
-  for (auto& o : s.order)
-    if (o.done) (void)hipEventDestroy(o.done);
-  for (hipEvent_t e : {s.ev_start, s.ev_stop, s.ev_join, s.ev_kbeg[0], s.ev_kbeg[1], s.ev_kend[0], s.ev_kend[1],
-                       s.ev_pdone[0], s.ev_pdone[1]})
+  std::vector<hipEvent_t> evs = {s.ev_gs};
+  for (int q = 0; q < kParts; ++q) {
+    evs.push_back(s.ev_kbeg[q]);
+    evs.push_back(s.ev_kend[q]);
+  }
+  for (int l = 0; l < kLanes; ++l)
+    for (int q = 0; q < kParts; ++q) evs.push_back(s.ev_done[l][q]);
+  for (int r = 0; r < kRing; ++r) evs.push_back(s.ev_band_read[r]);
+  for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
-  for (hipStream_t st : s.part)
-    if (st) (void)hipStreamDestroy(st);
+  for (int l = 0; l < kLanes; ++l)
+    for (int q = 0; q < kParts; ++q)
+      if (s.ls[l][q]) (void)hipStreamDestroy(s.ls[l][q]);
+  if (s.gs) (void)hipStreamDestroy(s.gs);
   s = Shard();
 }
 
@@ -190,27 +222,33 @@ hipError_t shard_init(Shard& s, int device) {
   hipError_t e = hipSetDevice(device);
   const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
   const size_t pool_words = size_t(kOrderSlots) * kOrderSlotWords;
-  for (int p = 0; p < kParts && e == hipSuccess; ++p) e = hipStreamCreateWithFlags(&s.part[p], hipStreamNonBlocking);
   // ordering markers without timestamps (timing events make the command processor stamp and
   // flush around them: ~20 us gaps between the launches of a stream, measured)
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_start, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_stop, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming);
-  for (int p = 0; p < kParts && e == hipSuccess; ++p) {
-    e = hipEventCreateWithFlags(&s.ev_pdone[p], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreate(&s.ev_kbeg[p]);
-    if (e == hipSuccess) e = hipEventCreate(&s.ev_kend[p]);
+  // HIP deals streams to its hardware queues (GPU_MAX_HW_QUEUES, 4 by default) in creation order:
+  // the lanes' first streams first, so that frames in flight land on distinct queues
+  for (int q = 0; q < kParts; ++q)
+    for (int l = 0; l < kLanes && e == hipSuccess; ++l) {
+      e = hipStreamCreateWithFlags(&s.ls[l][q], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_done[l][q], hipEventDisableTiming);
+    }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.gs, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_gs, hipEventDisableTiming);
+  for (int r = 0; r < kRing && e == hipSuccess; ++r)
+    e = hipEventCreateWithFlags(&s.ev_band_read[r], hipEventDisableTiming);
+  for (int q = 0; q < kParts && e == hipSuccess; ++q) {
+    e = hipEventCreate(&s.ev_kbeg[q]);
+    if (e == hipSuccess) e = hipEventCreate(&s.ev_kend[q]);
   }
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt, sizeof(unsigned long long) * VRT_CNT_COUNT);
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt_rep, rep_bytes);
   if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
   if (e == hipSuccess) e = hipMalloc(&s.d_order_pool, pool_words * sizeof(uint32_t));
-  for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) {
-    s.order[i].d = s.d_order_pool + size_t(i) * kOrderSlotWords;
-    e = hipEventCreateWithFlags(&s.order[i].done, hipEventDisableTiming);
-  }
+  for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) s.order[i].d = s.d_order_pool + size_t(i) * kOrderSlotWords;
   return e;
 }
+
+// The stream of the shard's one-at-a-time work (volume upload, passes, broadcast): lane 0's first
+hipStream_t main_stream(const Shard& s) { return s.ls[0][0]; }
 
 int upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t size) {
   if (!rgba || size < 1 || size > 8192 || (size & (size - 1)) != 0)
@@ -301,12 +339,13 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
 }
 
 // The tile-order slot of this launch's band and stream, from the shard's pool (no allocation, no
-// host sync). Reusing the least recently used slot for another band / stream first marks the
-// slot's old stream (everything enqueued there so far, its last launch with the slot included)
-// and makes this stream wait for that mark on the device, then zeroes the slot on this stream (no
-// heavy tiles yet). No marker is needed per launch: launches on one stream are ordered. Not while
-// the stream is being captured into a graph (a replayed node would reuse one list / counter set):
-// dispatch order then.
+// host sync in the steady state). A slot stays with its (band, stream): launches on one stream are
+// ordered, so no marker is needed per launch. Reassigning the least recently used slot to another
+// band or stream (more than kOrderSlots pairs in use) first synchronises the device: the old
+// stream's last launch with the slot may still run, and that stream may already have been
+// destroyed by its owner, so no event is recorded on it. Then the slot is zeroed on this stream
+// (no heavy tiles yet). Not while the stream is being captured into a graph (a replayed node
+// would reuse one list / counter set): dispatch order then.
 OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
   // only where it pays: glass in the volume (without it the order gains nothing: C2 ±0, C4 +5 %,
   // profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where every tile is
@@ -325,14 +364,7 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
     slot = &s.order[0];
     for (auto& o : s.order)
       if (!o.used || (slot->used && o.tick < slot->tick)) slot = &o;
-    if (slot->used && slot->stream != st) {
-      // the old stream may have been destroyed by its owner: then wait for the whole device
-      if (hipEventRecord(slot->done, slot->stream) == hipSuccess) {
-        if (hipStreamWaitEvent(st, slot->done, 0) != hipSuccess) return nullptr;
-      } else if (hipDeviceSynchronize() != hipSuccess) {
-        return nullptr;
-      }
-    }
+    if (slot->used && slot->stream != st && hipDeviceSynchronize() != hipSuccess) return nullptr;
     // zero the list counters, the wave counters and both rank sets (no heavy tiles yet)
     if (hipMemsetAsync(slot->d, 0, (vrt::kOrdHdr + size_t(3) * a.tiles) * sizeof(uint32_t), st) != hipSuccess)
       return nullptr;
@@ -371,6 +403,8 @@ int volume_alloc(vrt_ctx* ctx, Shard& s, int32_t n) {
   if (n < 2 || n > 1024 || (n & (n - 1)) != 0)
     return fail(ctx, VRT_ERR_INVALID, "volume edge must be a power of two in [2, 1024]");
   VRT_HIP(ctx, hipSetDevice(s.device));
+  // frames still in flight on the lanes read the resident volume: an upload is not a hot call
+  VRT_HIP(ctx, hipDeviceSynchronize());
   // octant layout while 8 padded u16 volumes stay addressable by a 32-bit byte offset
   const bool fits = uint64_t(n + 1) * (n + 1) * (n + 1) * 2 * 8 <= (uint64_t(1) << 32);
   const int32_t octants = fits && ctx->layout_req != 1 ? 8 : 1;
@@ -413,20 +447,20 @@ int volume_finish_all(vrt_ctx* ctx) {
   for (Shard& s : ctx->sh) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     const uint64_t vol = uint64_t(s.n) * s.n * s.n;
-    vrt::launch_volume_passes(s.d_vox, s.d_tmp, s.d_vox_pad, uint32_t(s.n), s.octants, s.part[0]);
+    vrt::launch_volume_passes(s.d_vox, s.d_tmp, s.d_vox_pad, uint32_t(s.n), s.octants, main_stream(s));
     // certified walks cannot settle glass pixels (their secondary rays start at the exact hit
     // point) and a glass pixel pays the certified primary walk before the exact path: the
     // automatic mode turns them off when glass makes up more than 1/8 of the non-empty voxels
     if (!s.d_vstats) VRT_HIP(ctx, hipMalloc(&s.d_vstats, 2 * sizeof(unsigned long long)));
-    VRT_HIP(ctx, hipMemsetAsync(s.d_vstats, 0, 2 * sizeof(unsigned long long), s.part[0]));
-    vrt::launch_glass_share(s.d_vox, vol, s.d_vstats, s.part[0]);
+    VRT_HIP(ctx, hipMemsetAsync(s.d_vstats, 0, 2 * sizeof(unsigned long long), main_stream(s)));
+    vrt::launch_glass_share(s.d_vox, vol, s.d_vstats, main_stream(s));
     VRT_HIP(ctx, hipGetLastError());
   }
   for (Shard& s : ctx->sh) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     unsigned long long vs[2] = {0, 0};
-    VRT_HIP(ctx, hipMemcpyAsync(vs, s.d_vstats, sizeof(vs), hipMemcpyDeviceToHost, s.part[0]));
-    VRT_HIP(ctx, hipStreamSynchronize(s.part[0]));
+    VRT_HIP(ctx, hipMemcpyAsync(vs, s.d_vstats, sizeof(vs), hipMemcpyDeviceToHost, main_stream(s)));
+    VRT_HIP(ctx, hipStreamSynchronize(main_stream(s)));
     s.cert_auto = vs[0] * 8 <= vs[1];
     s.has_glass = vs[0] > 0;
   }
@@ -446,7 +480,7 @@ int broadcast_volume(vrt_ctx* ctx) {
     for (size_t j = 0; j < k; ++j) {
       Shard& s = ctx->sh[j];
       (void)hipSetDevice(s.device);
-      const ncclResult_t r = ncclBroadcast(root.d_vox, s.d_vox, bytes, ncclUint8, 0, ctx->comms[j], s.part[0]);
+      const ncclResult_t r = ncclBroadcast(root.d_vox, s.d_vox, bytes, ncclUint8, 0, ctx->comms[j], main_stream(s));
       if (r != ncclSuccess) {
         (void)ncclGroupEnd();
         return nccl_fail(ctx, r, "ncclBroadcast(volume)");
@@ -456,19 +490,19 @@ int broadcast_volume(vrt_ctx* ctx) {
     return VRT_OK;
   }
   VRT_HIP(ctx, hipSetDevice(root.device));
-  VRT_HIP(ctx, hipEventRecord(root.ev_join, root.part[0]));
+  VRT_HIP(ctx, hipEventRecord(root.ev_gs, main_stream(root)));
   for (size_t j = 1; j < k; ++j) {
     Shard& s = ctx->sh[j];
     VRT_HIP(ctx, hipSetDevice(s.device));
-    VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], root.ev_join, 0));
-    VRT_HIP(ctx, hipMemcpyPeerAsync(s.d_vox, s.device, root.d_vox, root.device, bytes, s.part[0]));
+    VRT_HIP(ctx, hipStreamWaitEvent(main_stream(s), root.ev_gs, 0));
+    VRT_HIP(ctx, hipMemcpyPeerAsync(s.d_vox, s.device, root.d_vox, root.device, bytes, main_stream(s)));
   }
   return VRT_OK;
 }
 
 // Whole-frame band buffers of every device for a W x H frame (history black on (re)creation):
-// the ring of filtered bands and the raw band; with several devices, the first device's ring of
-// assembled frames.
+// the ring of filtered bands and the ring of raw bands; with several devices, the first device's
+// ring of assembled frames.
 int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
   if (w == ctx->hist_w && h == ctx->hist_h) return VRT_OK;
   const int32_t k = int32_t(ctx->sh.size());
@@ -477,17 +511,26 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     VRT_HIP(ctx, hipDeviceSynchronize());  // nothing may still read the old buffers
     if (pixels > s.hist_pixels) {
-      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_ring[3], &s.d_raw}) {
-        if (*b) (void)hipFree(*b);
-        *b = nullptr;
-      }
+      for (int r = 0; r < kRing; ++r)
+        for (uint32_t** b : {&s.d_ring[r], &s.d_rawbuf[r]}) {
+          if (*b) (void)hipFree(*b);
+          *b = nullptr;
+        }
       s.hist_pixels = 0;
-      for (uint32_t** b : {&s.d_ring[0], &s.d_ring[1], &s.d_ring[2], &s.d_ring[3], &s.d_raw})
-        if (hipMalloc(b, pixels * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
+      for (int r = 0; r < kRing; ++r)
+        for (uint32_t** b : {&s.d_ring[r], &s.d_rawbuf[r]})
+          if (hipMalloc(b, pixels * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc history buffers");
       s.hist_pixels = pixels;
     }
-    for (uint32_t* b : {s.d_ring[0], s.d_ring[1], s.d_ring[2], s.d_ring[3], s.d_raw})
-      VRT_HIP(ctx, hipMemset(b, 0, pixels * 4));
+    for (int r = 0; r < kRing; ++r) {
+      VRT_HIP(ctx, hipMemset(s.d_ring[r], 0, pixels * 4));
+      VRT_HIP(ctx, hipMemset(s.d_rawbuf[r], 0, pixels * 4));
+      s.band_read_valid[r] = false;
+    }
+    for (int l = 0; l < kLanes; ++l) {
+      s.lane_parts[l] = 0;
+      s.lane_hist[l] = false;
+    }
   }
   if (k > 1 || ctx->coll1) {
     VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
@@ -500,86 +543,122 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
   ctx->hist_w = w;
   ctx->hist_h = h;
   ctx->fk = 0;
-  ctx->gather_pending = false;
+  ctx->reset_pending = false;
+  for (bool& v : ctx->raw_is_cur) v = false;
   for (bool& v : ctx->consumed_valid) v = false;
   return VRT_OK;
 }
 
-// Launch one whole frame on every device: band j as kParts interleaved parts on the part streams
-// (or, when counting or writing hit records, one exact-instance launch on part[0]), bracketed by
-// ev_start / ev_stop on part[0] with part[1] joined. rgba8: the temporal path from the history
-// ring[(fk-1) % kRing] into ring[fk % kRing] + d_raw (frame fk); else the float band into d_out
-// (+ d_hit). wait_consumed: every part first waits for the caller's consumption of the ring slot
-// it overwrites (device-output frames, one device).
-// pipelined (one device, uncounted): no cross-part ordering at all — each part stream depends
-// only on its own previous frame (disjoint rows), so frame k+1's parts fill frame k's tail.
-// timing: device timestamps of every part kernel's start and end (vrt_stats.kernel_ms); only
-// when the caller asked for stats, since timing events cost latency between launches.
+// st waits for every launch of lane l's last frame except the one on st itself (stream order)
+int wait_lane(vrt_ctx* ctx, Shard& s, int l, hipStream_t st) {
+  for (int r = 0; r < s.lane_parts[l]; ++r)
+    if (s.ls[l][r] != st) VRT_HIP(ctx, hipStreamWaitEvent(st, s.ev_done[l][r], 0));
+  return VRT_OK;
+}
+
+// Launch one whole frame on every device, on lane g = fk % kLanes: band j as nparts launches on
+// the lane's streams — one exact-instance launch when counting or writing hit records; one launch
+// when `overlap` (device-output frames, which overlap each other) and the frame does not read its
+// history; else kParts interleaved parts, whose launches fill each other's tails. rgba8: the
+// temporal path from the history (ring[(fk-1) % kRing], or after vrt_history_reset the last raw
+// frame) into ring[fk % kRing] (+ the raw band when u_Alpha != 1: at u_Alpha = 1 the filtered
+// frame is the quantised frame); else the float band into d_out (+ d_hit). Every launch records
+// its lane's done event; cross-lane ordering only where buffers are shared:
+//  - the lane's previous frame had another layout: its launches on the other streams (same slot);
+//  - the frame reads its history (u_Alpha != 1): frame fk-1's launches (its slot, other lane);
+//  - frame fk-3 read this slot as its history: its launches (WAR);
+//  - a device-output gather of frame fk-4 read this slot: its gather stream;
+//  - wait_consumed: the caller's consumption of the device-output frame in this slot.
+// timing: device timestamps of every launch (vrt_stats.kernel_ms; synchronous calls only).
 int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, bool rgba8,
-                 bool hits, bool counting, bool timing, bool pipelined = false,
-                 hipEvent_t wait_consumed = nullptr) {
+                 bool hits, bool counting, bool timing, bool overlap, hipEvent_t wait_consumed = nullptr) {
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
+  const uint64_t f = ctx->fk;
+  const int g = int(f % kLanes), slot = int(f % kRing), pslot = int((f + kRing - 1) % kRing);
+  // the kernel reads the history iff u_Alpha != 1 (store_pixel, vrt_render.hip)
+  const bool hist = rgba8 && alpha != 1.0f;
+  const bool single = counting || hits;  // one counter replica set: one counted launch
+  const int nparts = single || (overlap && !hist) ? 1 : kParts;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
     VRT_HIP(ctx, hipSetDevice(s.device));
-    if (ctx->gather_pending && j > 0)  // the last device-output frame still reads this band
-      VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], ctx->ev_gathered, 0));
-    if (counting)
-      VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.part[0]));
-    if (!pipelined) VRT_HIP(ctx, hipEventRecord(s.ev_start, s.part[0]));
-    s.timed[0] = s.timed[1] = false;
+    for (int q = 0; q < kParts; ++q) s.timed[q] = false;
     const int32_t hb = band_rows(h, k, j);
-    if (hb > 0) {
-      const bool single = counting || hits;  // one counter replica set: one counted launch
-      const int32_t nparts = single ? 1 : kParts;
-      if (!single && !pipelined) VRT_HIP(ctx, hipStreamWaitEvent(s.part[1], s.ev_start, 0));
-      if (wait_consumed)
-        for (int32_t q = 0; q < nparts; ++q) VRT_HIP(ctx, hipStreamWaitEvent(s.part[q], wait_consumed, 0));
-      for (int32_t q = 0; q < nparts; ++q) {
-        const PartRows pr = single ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
-        if (pr.rows == 0) continue;
-        vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
-        a.pitch = int32_t(int64_t(w) * (single ? 1 : kParts));
-        const size_t off = size_t(pr.band_row0) * size_t(w);
-        s.timed[q] = timing;
-        hipEvent_t kb = timing ? s.ev_kbeg[q] : nullptr, ke = timing ? s.ev_kend[q] : nullptr;
-        if (rgba8) {
-          a.alpha = alpha;
-          a.prev = s.d_ring[(ctx->fk + kRing - 1) % kRing] + off;
-          a.cur = s.d_ring[ctx->fk % kRing] + off;
-          a.raw = s.d_raw + off;
-          launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.part[q], kb, ke);
-        } else {
-          launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
-                 s.part[q], kb, ke);
-        }
-        VRT_HIP(ctx, hipGetLastError());
-      }
-      if (!single && !pipelined) {
-        VRT_HIP(ctx, hipEventRecord(s.ev_join, s.part[1]));
-        VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
-      }
+    if (hb == 0) {
+      s.lane_parts[g] = 0;
+      s.lane_hist[g] = false;
+      continue;
     }
-    if (!pipelined) VRT_HIP(ctx, hipEventRecord(s.ev_stop, s.part[0]));
+    int st;
+    for (int q = 0; q < nparts; ++q) {
+      hipStream_t sq = s.ls[g][q];
+      if (s.lane_parts[g] != nparts && (st = wait_lane(ctx, s, g, sq)) != VRT_OK) return st;
+      if (rgba8 && f > 0) {
+        const int pg = int((f - 1) % kLanes);
+        if (hist) {  // part q's history rows: frame f-1's launch with the same rows, or all of them
+          if (s.lane_parts[pg] == nparts) VRT_HIP(ctx, hipStreamWaitEvent(sq, s.ev_done[pg][q], 0));
+          else if ((st = wait_lane(ctx, s, pg, sq)) != VRT_OK) return st;
+        }
+        const int rg = int((f + kLanes - 3) % kLanes);
+        if (f >= 3 && s.lane_hist[rg] && (st = wait_lane(ctx, s, rg, sq)) != VRT_OK) return st;
+      }
+      if (rgba8 && s.band_read_valid[slot]) VRT_HIP(ctx, hipStreamWaitEvent(sq, s.ev_band_read[slot], 0));
+      if (wait_consumed) VRT_HIP(ctx, hipStreamWaitEvent(sq, wait_consumed, 0));
+    }
+    if (rgba8) s.band_read_valid[slot] = false;
+    if (counting)
+      VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.ls[g][0]));
+    const uint32_t* hsrc = ctx->reset_pending && !ctx->raw_is_cur[pslot] ? s.d_rawbuf[pslot] : s.d_ring[pslot];
+    for (int q = 0; q < nparts; ++q) {
+      const PartRows pr = nparts == 1 ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
+      if (pr.rows == 0) {
+        VRT_HIP(ctx, hipEventRecord(s.ev_done[g][q], s.ls[g][q]));
+        continue;
+      }
+      vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
+      a.pitch = int32_t(int64_t(w) * nparts);
+      const size_t off = size_t(pr.band_row0) * size_t(w);
+      s.timed[q] = timing;
+      hipEvent_t kb = timing ? s.ev_kbeg[q] : nullptr, ke = timing ? s.ev_kend[q] : nullptr;
+      if (rgba8) {
+        a.alpha = alpha;
+        a.prev = hsrc + off;
+        a.cur = s.d_ring[slot] + off;
+        a.raw = hist ? s.d_rawbuf[slot] + off : nullptr;
+        launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.ls[g][q], kb, ke);
+      } else {
+        launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
+               s.ls[g][q], kb, ke);
+      }
+      VRT_HIP(ctx, hipGetLastError());
+      VRT_HIP(ctx, hipEventRecord(s.ev_done[g][q], s.ls[g][q]));
+    }
+    s.lane_parts[g] = nparts;
+    s.lane_hist[g] = hist;
   }
-  ctx->gather_pending = false;
+  if (rgba8) {
+    ctx->raw_is_cur[slot] = !hist;
+    ctx->reset_pending = false;
+  }
   return VRT_OK;
 }
 
 // Wait for every device, then fill stats: kernel_ms = the slowest device's span from its first
-// part kernel's start to its last part kernel's end (device timestamps: the GPU time of the
-// frame, as GL_TIME_ELAPSED measured the draw); counters summed.
+// launch's start to its last launch's end (device timestamps: the GPU time of the frame, as
+// GL_TIME_ELAPSED measured the draw); counters summed.
 int finish_frame(vrt_ctx* ctx, vrt_stats* stats, bool counting) {
   float ms_max = 0.0f;
   unsigned long long tot[VRT_CNT_COUNT] = {0};
   for (Shard& s : ctx->sh) {
     VRT_HIP(ctx, hipSetDevice(s.device));
-    for (hipStream_t st : s.part) VRT_HIP(ctx, hipStreamSynchronize(st));
+    for (int l = 0; l < kLanes; ++l)
+      for (int q = 0; q < kParts; ++q) VRT_HIP(ctx, hipStreamSynchronize(s.ls[l][q]));
+    VRT_HIP(ctx, hipStreamSynchronize(s.gs));
     if (stats) {
       int first = -1;
       for (int q = 0; q < kParts; ++q)
         if (s.timed[q] && first < 0) first = q;
-      if (first >= 0) {  // times relative to the first part's start (may be negative)
+      if (first >= 0) {  // times relative to the first launch's start (may be negative)
         float lo = 0.0f, hi = 0.0f;
         for (int q = 0; q < kParts; ++q) {
           if (!s.timed[q]) continue;
@@ -606,19 +685,35 @@ int finish_frame(vrt_ctx* ctx, vrt_stats* stats, bool counting) {
   return VRT_OK;
 }
 
-// Band j's rows (band row r = frame row j + r*k) to the host frame: one strided copy per device
-// on its own PCIe link.
-int copy_bands_to_host(vrt_ctx* ctx, int32_t w, int32_t h, const void* const* bands, size_t elem,
-                       void* host) {
+// Pinned host staging of synchronous frames, at least `bytes` (portable: every device's DMA
+// engine writes it directly, so the k band copies run in parallel)
+int ensure_stage(vrt_ctx* ctx, size_t bytes) {
+  if (ctx->h_stage_bytes >= bytes) return VRT_OK;
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  ctx->h_stage = nullptr;
+  ctx->h_stage_bytes = 0;
+  if (hipHostMalloc(&ctx->h_stage, bytes, hipHostMallocPortable) != hipSuccess)
+    return fail(ctx, VRT_ERR_OOM, "hipHostMalloc staging");
+  ctx->h_stage_bytes = bytes;
+  return VRT_OK;
+}
+
+// Band j's rows (band row r = frame row j + r*k) into their frame rows of the pinned staging
+// buffer at byte offset stage_off: one strided DMA per device on its own link, after every launch
+// of the frame on lane g. The caller copies the staged frame out after finish_frame.
+int stage_bands(vrt_ctx* ctx, int g, int32_t w, int32_t h, const void* const* bands, size_t elem,
+                size_t stage_off) {
   const int32_t k = int32_t(ctx->sh.size());
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
     const int32_t hb = band_rows(h, k, j);
     if (hb == 0) continue;
     VRT_HIP(ctx, hipSetDevice(s.device));
+    int st = wait_lane(ctx, s, g, s.ls[g][0]);
+    if (st != VRT_OK) return st;
     const size_t row = size_t(w) * elem;
-    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(host) + size_t(j) * row, size_t(k) * row, bands[j], row,
-                                  row, size_t(hb), hipMemcpyDeviceToHost, s.part[0]));
+    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(ctx->h_stage) + stage_off + size_t(j) * row, size_t(k) * row,
+                                  bands[j], row, row, size_t(hb), hipMemcpyDeviceToHost, s.ls[g][0]));
   }
   return VRT_OK;
 }
@@ -698,6 +793,7 @@ void vrt_destroy(vrt_ctx* c) {
     for (hipEvent_t e : c->ev_consumed)
       if (e) (void)hipEventDestroy(e);
     if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (!c->lt_ev.empty()) (void)hipDeviceSynchronize();
     for (hipEvent_t e : c->lt_ev) (void)hipEventDestroy(e);
   }
@@ -737,7 +833,7 @@ int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
   Shard& root = ctx->sh[0];
   const size_t bytes = size_t(vol->n) * vol->n * vol->n;
   VRT_HIP(ctx, hipSetDevice(root.device));
-  VRT_HIP(ctx, hipMemcpyAsync(root.d_vox, vol->voxels, bytes, hipMemcpyHostToDevice, root.part[0]));
+  VRT_HIP(ctx, hipMemcpyAsync(root.d_vox, vol->voxels, bytes, hipMemcpyHostToDevice, main_stream(root)));
   if ((st = broadcast_volume(ctx)) != VRT_OK) return st;
   return volume_finish_all(ctx);
 }
@@ -754,8 +850,8 @@ int vrt_upload_volume_device(vrt_ctx* ctx, const uint8_t* d_voxels, int32_t n, v
   // ordered after the caller's work on hip_stream (which produced d_voxels)
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   VRT_HIP(ctx, hipMemcpyAsync(root.d_vox, d_voxels, bytes, hipMemcpyDeviceToDevice, s));
-  VRT_HIP(ctx, hipEventRecord(root.ev_join, s));
-  VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], root.ev_join, 0));
+  VRT_HIP(ctx, hipEventRecord(root.ev_gs, s));
+  VRT_HIP(ctx, hipStreamWaitEvent(main_stream(root), root.ev_gs, 0));
   if ((st = broadcast_volume(ctx)) != VRT_OK) return st;
   return volume_finish_all(ctx);
 }
@@ -780,14 +876,14 @@ int vrt_build_scene_device(vrt_ctx* ctx, int32_t scene, int32_t n, uint32_t seed
     if (!noise.empty()) {
       // d_tmp (>= 2 N^3 bytes >= 4 N^2) is free until the distance passes
       VRT_HIP(ctx, hipMemcpyAsync(s.d_tmp, noise.data(), noise.size() * sizeof(float),
-                                  hipMemcpyHostToDevice, s.part[0]));
+                                  hipMemcpyHostToDevice, main_stream(s)));
       d_noise = reinterpret_cast<const float*>(s.d_tmp);
     }
     if (&s == &ctx->sh[0] && cs) {  // ordered after the caller's prior work on its stream
-      VRT_HIP(ctx, hipEventRecord(s.ev_join, cs));
-      VRT_HIP(ctx, hipStreamWaitEvent(s.part[0], s.ev_join, 0));
+      VRT_HIP(ctx, hipEventRecord(s.ev_gs, cs));
+      VRT_HIP(ctx, hipStreamWaitEvent(main_stream(s), s.ev_gs, 0));
     }
-    vrt::launch_build_scene(s.d_vox, scene, uint32_t(n), d_noise, s.part[0]);
+    vrt::launch_build_scene(s.d_vox, scene, uint32_t(n), d_noise, main_stream(s));
     VRT_HIP(ctx, hipGetLastError());
   }
   return volume_finish_all(ctx);
@@ -998,13 +1094,17 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, f
   if (!out_rgba8) return fail(ctx, VRT_ERR_INVALID, "null output");
   DeviceGuard guard;
   if ((st = ensure_history(ctx, cam->width, cam->height)) != VRT_OK) return st;
+  const size_t bytes = size_t(cam->width) * size_t(cam->height) * 4;
+  if ((st = ensure_stage(ctx, bytes)) != VRT_OK) return st;
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
-  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr)) != VRT_OK) return st;
+  const int g = int(ctx->fk % kLanes), slot = int(ctx->fk % kRing);
+  if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, false)) != VRT_OK) return st;
   std::vector<const void*> bands;
-  for (Shard& s : ctx->sh) bands.push_back(s.d_ring[ctx->fk % kRing]);
+  for (Shard& s : ctx->sh) bands.push_back(s.d_ring[slot]);
   ctx->fk++;
-  if ((st = copy_bands_to_host(ctx, cam->width, cam->height, bands.data(), 4, out_rgba8)) != VRT_OK) return st;
+  if ((st = stage_bands(ctx, g, cam->width, cam->height, bands.data(), 4, 0)) != VRT_OK) return st;
   if ((st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  std::memcpy(out_rgba8, ctx->h_stage, bytes);
   ctx->err.clear();
   return VRT_OK;
 }
@@ -1022,31 +1122,27 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   Shard& root = ctx->sh[0];
   hipStream_t cs = static_cast<hipStream_t>(hip_stream);
   const uint64_t f = ctx->fk;
-  const int slot = int(f % kRing), prev_slot = int((f + kRing - 1) % kRing);
+  const int slot = int(f % kRing), g = int(f % kLanes);
   VRT_HIP(ctx, hipSetDevice(root.device));
   // E_f: whatever the caller enqueued on its stream so far (its consumption of frames <= f - 1)
   VRT_HIP(ctx, hipEventRecord(ctx->ev_consumed[slot], cs));
   ctx->consumed_valid[slot] = true;
-  // Frame f overwrites frame f - kRing's buffer, which must follow E_{f-kRing+1}. Waiting every
-  // kRing - 1 frames on E_{f-1} covers it by stream order: the last such wait before frame f was at
-  // a frame g >= f - kRing + 2 on E_{g-1}, g - 1 >= f - kRing + 1 (one marker per kRing - 1 frames
-  // per part stream instead of one per frame: -8 % per frame at C3, profiles/r02_s08)
+  // Frame f overwrites the buffer handed out at frame f - kRing, which the caller's work before
+  // call f - kRing + 1 consumed: E_{f-kRing+1}. No wait when the host sees it done already.
   hipEvent_t reuse = nullptr;
-  if (f >= 2 && f % (kRing - 1) == 0 && ctx->consumed_valid[prev_slot]) reuse = ctx->ev_consumed[prev_slot];
+  if (f >= kRing) {
+    const int rs = int((f - kRing + 1) % kRing);
+    if (ctx->consumed_valid[rs] && hipEventQuery(ctx->ev_consumed[rs]) != hipSuccess) reuse = ctx->ev_consumed[rs];
+  }
   if (k == 1 && !ctx->coll1) {
-    // one device: the frame is rendered straight into the ring slot handed to the caller, as two
-    // pipelined parts — no part waits for the other (disjoint rows), so consecutive frames overlap
-    // as in the bench's FrameTiler; only the slot's consumption three frames ago is waited for.
-    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, !counting, reuse)) !=
-        VRT_OK)
+    // one device: the frame is rendered straight into the ring slot handed to the caller; up to
+    // kLanes frames in flight (u_Alpha = 1: independent frames)
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true, reuse)) != VRT_OK)
       return st;
-    for (int q = 0; q < kParts; ++q) {
-      VRT_HIP(ctx, hipEventRecord(root.ev_pdone[q], root.part[q]));
-      VRT_HIP(ctx, hipStreamWaitEvent(cs, root.ev_pdone[q], 0));
-    }
+    for (int q = 0; q < root.lane_parts[g]; ++q) VRT_HIP(ctx, hipStreamWaitEvent(cs, root.ev_done[g][q], 0));
     *d_frame = root.d_ring[slot];
   } else {
-    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr)) != VRT_OK) return st;
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true)) != VRT_OK) return st;
     const int32_t cap = band_cap(h, k);
     const size_t row = size_t(w) * 4;
     const uint32_t* src[64];
@@ -1060,35 +1156,53 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
         if (hipMalloc(&ctx->d_gather, need * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc gather");
         ctx->hist_pixels_gather = need;
       }
+      for (int32_t j = 0; j < k; ++j) {  // each device's gather stream after its band's launches
+        Shard& s = ctx->sh[j];
+        VRT_HIP(ctx, hipSetDevice(s.device));
+        if ((st = wait_lane(ctx, s, g, s.gs)) != VRT_OK) return st;
+      }
       VRT_NCCL(ctx, ncclGroupStart());
       for (int32_t j = 0; j < k; ++j) {
         Shard& s = ctx->sh[j];
         (void)hipSetDevice(s.device);
         const ncclResult_t r = ncclGather(s.d_ring[slot], j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
-                                          ncclUint8, 0, ctx->comms[j], s.part[0]);
+                                          ncclUint8, 0, ctx->comms[j], s.gs);
         if (r != ncclSuccess) {
           (void)ncclGroupEnd();
           return nccl_fail(ctx, r, "ncclGather(bands)");
         }
       }
       VRT_NCCL(ctx, ncclGroupEnd());
+      for (int32_t j = 0; j < k; ++j) {  // the band's next writer (frame f + kRing) waits for this
+        Shard& s = ctx->sh[j];
+        VRT_HIP(ctx, hipSetDevice(s.device));
+        VRT_HIP(ctx, hipEventRecord(s.ev_band_read[slot], s.gs));
+        s.band_read_valid[slot] = true;
+      }
       for (int32_t j = 0; j < k; ++j) src[j] = ctx->d_gather + size_t(j) * cap * w;
-    } else {  // a device repeats: copy the bands device to device
-      for (int32_t j = 1; j < k; ++j) VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], ctx->sh[j].ev_stop, 0));
+    } else {  // a device repeats: copy the bands device to device on the first device's stream
+      VRT_HIP(ctx, hipSetDevice(root.device));
+      for (int32_t j = 0; j < k; ++j)
+        for (int q = 0; q < ctx->sh[j].lane_parts[g]; ++q)
+          VRT_HIP(ctx, hipStreamWaitEvent(root.gs, ctx->sh[j].ev_done[g][q], 0));
       for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_ring[slot];
     }
     VRT_HIP(ctx, hipSetDevice(root.device));
-    if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.part[0], reuse, 0));
+    if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.gs, reuse, 0));
     uint32_t* out = ctx->d_frames[slot];
     for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
       const int32_t hb = band_rows(h, k, j);
       if (hb > 0)
         VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + size_t(j) * row, size_t(k) * row, src[j], row,
-                                      row, size_t(hb), hipMemcpyDeviceToDevice, root.part[0]));
+                                      row, size_t(hb), hipMemcpyDeviceToDevice, root.gs));
     }
-    VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.part[0]));
+    if (!ctx->distinct)
+      for (int32_t j = 0; j < k; ++j) {  // same physical device: the bands were read here
+        VRT_HIP(ctx, hipEventRecord(ctx->sh[j].ev_band_read[slot], root.gs));
+        ctx->sh[j].band_read_valid[slot] = true;
+      }
+    VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.gs));
     VRT_HIP(ctx, hipStreamWaitEvent(cs, ctx->ev_gathered, 0));
-    ctx->gather_pending = !ctx->distinct;  // the next frame's other devices wait for the copies
     *d_frame = out;
   }
   ctx->fk++;
@@ -1122,8 +1236,11 @@ int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size) {
 
 int vrt_history_reset(vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
-  // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer)
-  for (Shard& s : ctx->sh) std::swap(s.d_ring[(ctx->fk + kRing - 1) % kRing], s.d_raw);
+  // key F (main.cpp:417-421): std::swap(lastFrameBuffer, rayTraceFrameBuffer) — the next frame
+  // filters against the last ray-traced frame. No buffer changes hands: the next frame reads its
+  // history from the last frame's raw band (its filtered band when u_Alpha was 1, where the two
+  // are equal), so a device-output frame the caller still holds stays untouched.
+  ctx->reset_pending = ctx->fk > 0;
   ctx->err.clear();
   return VRT_OK;
 }
@@ -1151,19 +1268,24 @@ int vrt_render(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float* 
       return fail(ctx, VRT_ERR_OOM, "hipMalloc frame buffers");
     s.out_pixels = pixels;
   }
+  const size_t frame_px = size_t(cam->width) * size_t(cam->height);
+  const size_t fbytes = frame_px * sizeof(float4), hbytes = out_hit ? frame_px * sizeof(vrt_hit) : 0;
+  if ((st = ensure_stage(ctx, fbytes + hbytes)) != VRT_OK) return st;
   const bool counting = stats && (stats->request & VRT_STATS_COUNTERS);
-  if ((st = launch_frame(ctx, cam, p, 1.0f, false, out_hit != nullptr, counting, stats != nullptr)) != VRT_OK) return st;
+  const int g = int(ctx->fk % kLanes);
+  if ((st = launch_frame(ctx, cam, p, 1.0f, false, out_hit != nullptr, counting, stats != nullptr, false)) != VRT_OK)
+    return st;
   std::vector<const void*> bands, hbands;
   for (Shard& s : ctx->sh) {
     bands.push_back(s.d_out);
     hbands.push_back(s.d_hit);
   }
-  if ((st = copy_bands_to_host(ctx, cam->width, cam->height, bands.data(), sizeof(float4), out_rgba)) != VRT_OK)
-    return st;
-  if (out_hit &&
-      (st = copy_bands_to_host(ctx, cam->width, cam->height, hbands.data(), sizeof(vrt_hit), out_hit)) != VRT_OK)
+  if ((st = stage_bands(ctx, g, cam->width, cam->height, bands.data(), sizeof(float4), 0)) != VRT_OK) return st;
+  if (out_hit && (st = stage_bands(ctx, g, cam->width, cam->height, hbands.data(), sizeof(vrt_hit), fbytes)) != VRT_OK)
     return st;
   if ((st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+  std::memcpy(out_rgba, ctx->h_stage, fbytes);
+  if (out_hit) std::memcpy(out_hit, static_cast<const char*>(ctx->h_stage) + fbytes, hbytes);
   ctx->err.clear();
   return VRT_OK;
 }

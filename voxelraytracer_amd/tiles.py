@@ -1,36 +1,34 @@
-"""Framebuffer tiling across the GPUs of one node.
+"""Framebuffer tiling across the GPUs of one node, and frames in flight.
 
 The per-pixel program has no halo and no inter-ray exchange, so a frame splits into row bands,
 one per rank (one process per GPU). Bands are cyclic — rank r owns rows r, r+N, r+2N, ... — so
 every rank gets the same mix of cheap sky rows and expensive geometry rows. Each rank renders its
-band into HBM; the only exchange is one gather of the bands to rank 0 per frame (RCCL over xGMI
-with the "nccl" backend; gloo on CPU for tests), after which rank 0 re-interleaves the bands into
-the frame. The volume is replicated once per GPU (broadcast_volume).
+band into HBM. The volume is replicated once per GPU (broadcast_volume). The only exchange is the
+output: either one gather of the bands to rank 0 per frame (gather=True: RCCL over xGMI with the
+"nccl" backend, gloo on CPU for tests; rank 0 re-interleaves), or none — the bands stay on their
+ranks (gather=False, bench.py's default for N > 1) and collect() gathers one frame when the whole
+frame is wanted (SURVEY §8e's gather is output delivery, not part of the per-pixel path).
 
-Within a rank the band is rendered as P interleaved parts on P HIP streams (default P = 1; the
-bench uses 2): global part q = s*N + r owns frame rows q, q + N*P, q + 2*N*P, ... . One launch's
-last dispatch round leaves wave slots idle while its final waves finish; a second stream's launch
-fills them, so consecutive frames' parts overlap their tails (measured: C3 0.241 -> 0.220 ms per
-frame with P = 2, scripts/streams_exp.py). Ordering uses events only: a part stream waits for the
-gather that last read its buffer, the gather waits for every part of its frame — a part never
-waits for another part, so the overlap is real.
+Within a rank the band is rendered as P interleaved parts (global part q = s*N + r owns frame
+rows q, q + N*P, ...), each on its own HIP stream, and — without the per-frame gather — L frames
+may be in flight at once ("lanes"): frame k renders on lane k % L (P streams and an output buffer
+of its own). A frame's last dispatch round leaves wave slots idle while its longest waves (the
+exact-path and glass pixels, tens of microseconds) finish; the next frames' launches on the other
+lanes fill them. At u_Alpha = 1 (the slider default, res/guis/header.xml:20) a frame does not read
+its history (the RGB8 blend is the identity, tests/test_temporal_oracle.py), so consecutive frames
+are independent (independent=True: no ordering between lanes at all). Otherwise part s of frame k
+waits for part s of frame k-1 (its history rows) with one event. Measured on one MI355X
+(scripts/diag/strong_pipe.py, profiles/r03_pipe/): C3's band at k = 8 GPUs takes 0.0416 ms per frame
+with one lane of two parts and 0.0112 ms with four lanes of one part; the whole 1080p frame 0.0599 ms.
 
-With one rank and P > 1 parts, every part renders straight into its rows of the frame buffer
-(a row-strided view; the renderer's row pitch, ABI v4) and filters them in place against the same
-rows, which hold the previous frame: no band buffers, no assembly copy (it cost ≈4 % of a C3
-frame as two strided copy kernels per frame).
+With one lane every part renders straight into its rows of the band buffer (a row-strided view;
+the renderer's row pitch, ABI v4) and filters them in place against the same rows, which hold the
+previous frame: no band buffers, no assembly copy. With several lanes a part reads its history
+from the previous lane's buffer and writes its own.
 
-With several ranks the frame is either gathered to rank 0 every frame (gather=True: the display
-of one whole frame on one GPU) or kept distributed (gather=False, bench.py's default for N > 1):
-the per-pixel program has no exchange step, so each rank then renders and filters its band in
-place exactly as a single rank renders its frame, and collect() gathers the bands once when the
-whole frame is wanted (SURVEY §8e's per-frame gather is output delivery, not part of the path: at
-weak scaling every rank's 8.3 MB RGBA8 band would cross xGMI into rank 0 per 0.06 ms frame).
-FrameTiler double-buffers the band (gather=True) so that the gather of frame k overlaps the render
-of frame k+1. Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8 store
-(the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire instead of 16.
-The temporal history is part-local (each part blends its own rows, on its own stream), so it adds
-no exchange and no cross-stream dependency; the previous frame's part buffer IS the history.
+gather=True double-buffers the band so that the gather of frame k overlaps the render of frame
+k+1 (one lane only). Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8
+store (the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire.
 """
 from __future__ import annotations
 
@@ -93,25 +91,28 @@ def broadcast_volume(vox: torch.Tensor, src: int = 0, group=None) -> torch.Tenso
 
 
 class FrameTiler:
-    """Renders a sequence of frames across `world` ranks, `parts` streams per rank.
+    """Renders a sequence of frames across `world` ranks, `parts` streams per lane, `lanes`
+    frames in flight per rank.
 
     render_band(row0, rows, row_step, out, prev) must enqueue the render of one part into `out`
-    ([rows, W, channels] of `dtype` on `device`; possibly a row-strided view, see row_pitch) on
-    the CURRENT stream (the HIP kernel through the C-ABI, or the oracle in CPU tests); `prev` holds
-    that part's rows of the previous frame (the temporal history; zeros before the first frame;
-    it is `out` itself with one buffer: each pixel is read before it is written).
-    frame() renders the next frame; with one rank, or with gather=False, it returns this rank's
-    band of it (the whole frame with one rank; for parts > 1 each part renders into its rows of it
-    directly, in place); with several ranks and gather=True the gather is issued asynchronously
-    and rank 0 returns the PREVIOUS frame, assembled on `self.assembly_stream` (None on the first
-    call and on other ranks), so the gather of frame k overlaps the render of frame k+1. finish()
-    drains the pipeline and returns the last frame (band) on rank 0; collect() (gather=False)
-    assembles the last frame on rank 0 with one gather. A returned frame is valid until the next
-    frame() call; synchronise the device before reading it.
+    ([rows, W, channels] of `dtype` on `device`; a row-strided view, see row_pitch) on the CURRENT
+    stream (the HIP kernel through the C-ABI, or the oracle in CPU tests); `prev` holds that
+    part's rows of the previous frame (the temporal history; zeros before the first frame; with
+    one lane it is `out` itself: each pixel is read before it is written).
+    frame() enqueues the next frame; with gather=False (or one rank) it returns this rank's band
+    of it ([rows, W, C], the whole frame with one rank); with several ranks and gather=True the
+    gather is issued asynchronously and rank 0 returns the PREVIOUS frame, assembled on
+    `self.assembly_stream` (None on the first call and on other ranks). finish() makes the current
+    stream wait for every frame enqueued so far and returns the last frame (band) on rank 0 (the
+    last band elsewhere with gather=False); collect() (gather=False) assembles the last frame on
+    rank 0 with one gather. A returned band stays valid until `lanes` more frames are enqueued;
+    synchronise the device before reading it. independent=True declares that render_band does
+    not read `prev` (u_Alpha = 1): frames on different lanes are then not ordered at all.
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
-                 channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True):
+                 channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
+                 lanes: int = 1, independent: bool = False):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.group = group
@@ -122,79 +123,99 @@ class FrameTiler:
         self.render_band = render_band
         self.cuda = torch.device(device).type == "cuda"
         self.gather = gather and self.world > 1
+        if lanes < 1 or (self.gather and lanes > 1):
+            raise ValueError("lanes >= 1; frames in flight keep their bands on the ranks "
+                             "(gather=False)")
+        self.lanes, self.independent = lanes, independent
         self.channels, self.dtype = channels, dtype
         shape = (parts, self.rows_p, width, channels)
-        nbuf = 2 if self.gather else 1
-        # no per-frame gather, several parts: the parts render into (and filter in place) this
-        # rank's band itself (the whole frame with one rank)
-        self.direct = not self.gather and parts > 1
-        self.frame_buf = None
-        if self.direct:
-            self.frame_buf = torch.zeros((self.rows, width, channels), dtype=dtype, device=device)
-            self.bands = [self.frame_buf.view(shape)]   # same storage (bench's counted launch)
+        self.bufs = None
+        self.bands = None
+        if not self.gather:
+            # this rank's band per lane; part s renders band rows s, s + parts, ... in place
+            self.bufs = [torch.zeros((self.rows, width, channels), dtype=dtype, device=device)
+                         for _ in range(lanes)]
         else:
-            self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
-        self.part_streams = ([torch.cuda.Stream(device=device) for _ in range(parts)]
-                             if self.cuda and parts > 1 else None)
+            self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(2)]
+        self.part_streams = ([[torch.cuda.Stream(device=device) for _ in range(parts)]
+                              for _ in range(lanes)]
+                             if self.cuda and (parts > 1 or lanes > 1) else None)
+        self.part_done = [[None] * parts for _ in range(lanes)]   # dependent lanes: frame events
+        self.fresh = True   # the streams must first wait for the current stream's work
         self.assembly_stream = None
         self.gathered = None
+        self.frame_buf = None
         if self.rank == 0 and self.gather:
             self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
-        if self.rank == 0 and self.gather:
             self.gathered = [torch.empty((self.world,) + shape, dtype=dtype, device=device)
-                             for _ in range(nbuf)]
+                             for _ in range(2)]
             if self.cuda:
                 self.assembly_stream = torch.cuda.Stream(device=device)
-        self.pending = [None] * nbuf    # gather that still reads bands[b]
-        self.assembled = [None] * nbuf  # rank 0: assembly that still reads gathered[b] / bands[b]
+        self.pending = [None, None]     # gather that still reads bands[b]
+        self.assembled = [None, None]   # rank 0: assembly that still reads gathered[b]
         self.prev = None                # rank 0: buffer index of the frame awaiting assembly
         self.k = 0
 
     # ---- helpers ---------------------------------------------------------------------------
+    def part_rows(self, buf: torch.Tensor, s: int) -> torch.Tensor:
+        """Part s's rows of a band buffer [rows, W, C] (band rows s, s + parts, ...)."""
+        return buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
+
+    def last(self) -> torch.Tensor:
+        """This rank's band buffer of the last frame enqueued (gather=False)."""
+        return self.bufs[(self.k - 1) % self.lanes]
+
     def _part_buffers(self, s: int, band: torch.Tensor, prev: torch.Tensor):
-        """(out, prev) of part s: its rows of the frame (in place) in direct mode, else its slot
-        of the band buffers."""
-        if self.direct:
-            rows = self._frame_rows(s)
-            return rows, rows
+        """(out, prev) of part s: its rows of the lane buffers, or its slot of the gather bands."""
+        if not self.gather:
+            return self.part_rows(band, s), self.part_rows(prev, s)
         return band[s], prev[s]
 
-    def _render_parts(self, band: torch.Tensor, prev: torch.Tensor, wait_work):
-        """Enqueue every part (each waits for `wait_work`, the gather that last read its buffer).
-        Returns the events that mark the parts' completion (CUDA, parts > 1)."""
+    def _render_parts(self, lane: int, band: torch.Tensor, prev: torch.Tensor, wait_work):
+        """Enqueue every part of the next frame on `lane` (each first waits for `wait_work`, the
+        gather that last read its buffer). Returns the parts' completion events (CUDA streams)."""
         if self.part_streams is None:
             if wait_work is not None:
                 wait_work.wait()
             for s, (row0, rows, step) in enumerate(self.specs):
                 self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
             return None
+        cur = torch.cuda.current_stream()
+        if self.fresh:
+            for ln in self.part_streams:
+                for st in ln:
+                    st.wait_stream(cur)
+            self.fresh = False
+        dep = self.lanes > 1 and not self.independent
+        prev_lane = (lane - 1) % self.lanes
         events = []
         for s, (row0, rows, step) in enumerate(self.specs):
-            st = self.part_streams[s]
+            st = self.part_streams[lane][s]
             with torch.cuda.stream(st):
                 if wait_work is not None:
                     wait_work.wait()
+                if dep and self.part_done[prev_lane][s] is not None:
+                    st.wait_event(self.part_done[prev_lane][s])   # the history rows of part s
                 self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
-                events.append(st.record_event())
+                ev = st.record_event() if (dep or self.gather) else None
+                self.part_done[lane][s] = ev
+                events.append(ev)
         return events
-
-    def _frame_rows(self, s: int) -> torch.Tensor:
-        """frame_buf rows of this rank's part s (direct mode: frame_buf is the rank's band, the
-        whole frame with one rank): band rows s, s + parts, ..."""
-        return self.frame_buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
 
     # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
-        nb = len(self.bands)
-        b = self.k % nb
-        prev = self.bands[(self.k - 1) % nb]
+        if not self.gather:   # one rank, or ranks that keep their bands: no exchange
+            lane = self.k % self.lanes
+            band, prev = self.bufs[lane], self.bufs[(self.k - 1) % self.lanes]
+            self.k += 1
+            self._render_parts(lane, band, prev, None)
+            return band
+        b = self.k % 2
+        prev = self.bands[(self.k - 1) % 2]
         self.k += 1
         band = self.bands[b]
-        if not self.gather:   # one rank, or ranks that keep their bands: no exchange
-            self._render_parts(band, prev, None)
-            return band[0] if self.parts == 1 else self.frame_buf
         wait_work, self.pending[b] = self.pending[b], None
-        events = self._render_parts(band, prev, wait_work)
+        events = self._render_parts(0, band, prev, wait_work)
         cur = torch.cuda.current_stream() if self.cuda else None
         if events is not None:   # the gather (issued from the current stream) needs every part
             for e in events:
@@ -229,11 +250,11 @@ class FrameTiler:
         return out
 
     def collect(self) -> Optional[torch.Tensor]:
-        """Without the per-frame gather, after finish(): one gather of every rank's current band to
-        rank 0, re-interleaved into the whole frame (returned on rank 0, None elsewhere); e.g. to
-        display or check the last frame. Synchronous."""
+        """Without the per-frame gather, after finish(): one gather of every rank's band of the
+        last frame to rank 0, re-interleaved into the whole frame (returned on rank 0, None
+        elsewhere); e.g. to display or check the last frame. Synchronous."""
         assert not self.gather, "collect() is for gather=False tilers"
-        band = (self.frame_buf if self.direct else self.bands[0][0]).contiguous()
+        band = self.last().contiguous()
         if self.world == 1:
             return band
         glist = ([torch.empty_like(band) for _ in range(self.world)] if self.rank == 0 else None)
@@ -241,20 +262,22 @@ class FrameTiler:
         return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
 
     def finish(self) -> Optional[torch.Tensor]:
+        cur = torch.cuda.current_stream() if self.cuda else None
         if not self.gather:
-            if self.part_streams is not None:
-                cur = torch.cuda.current_stream()
-                for st in self.part_streams:
+            for ln in self.part_streams or ():
+                for st in ln:
                     cur.wait_stream(st)
-            return self.bands[0][0] if self.parts == 1 else self.frame_buf
+            self.fresh = True
+            return self.last()
         out = self._assemble_prev() if self.rank == 0 else None
         for i, w in enumerate(self.pending):
             if w is not None:
                 w.wait()
                 self.pending[i] = None
-        cur = torch.cuda.current_stream() if self.cuda else None
-        for st in self.part_streams or ():
-            cur.wait_stream(st)
+        for ln in self.part_streams or ():
+            for st in ln:
+                cur.wait_stream(st)
         if self.assembly_stream is not None:
             cur.wait_stream(self.assembly_stream)
+        self.fresh = True
         return out

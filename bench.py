@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
+    ap.add_argument("--rehearse-ranks", type=int, default=1,
+                    help="one GPU, one process: time only rank 0's band of a K-way strong split "
+                         "(what each GPU of a K-GPU run renders per frame; rays counted over the "
+                         "whole frame); a diagnostic of the scaling path, labelled as such")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
     ap.add_argument("--gather-frames", action="store_true",
@@ -243,31 +247,50 @@ def main():
     def render_band(row0, rows, step, out, prev):
         launch(row0, rows, step, out, prev)
 
+    def launch_ptrs(row0, rows, step, out_ptr, prev_ptr, pitch, sp):
+        # the lean form (FrameTiler's precomputed launches): one ctypes call per part launch
+        if rgba8:
+            ren.render_temporal_rows_async(cam, params, args.alpha, row0, rows, step, prev_ptr,
+                                           out_ptr, 0, 0, 0, sp, pitch=pitch)
+        else:
+            ren.render_rows_async(cam, params, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch)
+
     lanes = args.lanes or (4 if args.alpha == 1.0 and not args.gather_frames else 1)
     if args.gather_frames and lanes > 1:
         raise SystemExit("--gather-frames renders one frame at a time (--lanes 1)")
     parts = args.parts or (1 if lanes > 1 else 2)
-    parts = parts if frame_h % (world * parts) == 0 else 1
+    parts = parts if frame_h % (max(world, args.rehearse_ranks) * parts) == 0 else 1
     # independent frames: at alpha 1 the kernel does not read the history (tiles.py)
-    tiler = FrameTiler(w, frame_h, render_band, dev,
+    rehearse = args.rehearse_ranks if world == 1 and args.rehearse_ranks > 1 else 0
+    if rehearse and (args.gather_frames or args.scaling != "strong"):
+        raise SystemExit("--rehearse-ranks rehearses the strong split without per-frame gathers")
+    tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None, rank=0 if rehearse else None,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
                        gather=args.gather_frames, lanes=lanes,
-                       independent=rgba8 and args.alpha == 1.0 or not rgba8)
+                       independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
     cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device=dev)
     part_bytes = []
     own = None
-    for (row0, rows, step) in tiler.specs:
+    count_specs = tiler.specs
+    if rehearse:   # the whole frame's rays: every rank's parts of the rehearsed split
+        from voxelraytracer_amd.tiles import part_spec
+        count_specs = [part_spec(r_, rehearse, s_, parts, frame_h) for r_ in range(rehearse)
+                       for s_ in range(parts)]
+    own_cnt = torch.zeros_like(cnt)
+    for i_, (row0, rows, step) in enumerate(count_specs):
         pc = torch.zeros_like(cnt)
         scratch = torch.zeros((rows, w, 4), dtype=torch.uint8 if rgba8 else torch.float32, device=dev)
         launch(row0, rows, step, scratch, scratch, pc.data_ptr())
         torch.cuda.synchronize(dev)
         pcd = vrt.counters_dict(pc.cpu().tolist())
-        part_bytes.append(vrt.algorithmic_bytes(pcd, 8 if rgba8 else 16))
         cnt += pc
-    own = vrt.counters_dict(cnt.cpu().tolist())
+        if i_ < parts:   # this rank's own parts (rank 0's when rehearsing)
+            part_bytes.append(vrt.algorithmic_bytes(pcd, 8 if rgba8 else 16))
+            own_cnt += pc
+    own = vrt.counters_dict(own_cnt.cpu().tolist())
     if world > 1:
         dist.all_reduce(cnt)
     counters = vrt.counters_dict(cnt.cpu().tolist())
@@ -493,7 +516,10 @@ def main():
                                  if args.gather_frames else
                                  f"cyclic row bands x{world} ({args.scaling} scaling), no collective "
                                  "in the timed region (one RCCL gather of the last frame after it)")
-                                if world > 1 else "single GPU, whole frame")
+                                if world > 1 else
+                                (f"REHEARSAL on one GPU: only rank 0's band of a {rehearse}-way strong "
+                                 "split is rendered and timed; rays counted over the whole frame"
+                                 if rehearse else "single GPU, whole frame"))
                                + (f", {lanes} frames in flight (lanes)" if lanes > 1 else "")
                                + f", {parts} interleaved row part{'s' if parts > 1 else ''} per "
                                f"frame on {lanes * parts} HIP stream{'s' if lanes * parts > 1 else ''}",

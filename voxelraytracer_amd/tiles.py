@@ -108,13 +108,23 @@ class FrameTiler:
     rank 0 with one gather. A returned band stays valid until `lanes` more frames are enqueued;
     synchronise the device before reading it. independent=True declares that render_band does
     not read `prev` (u_Alpha = 1): frames on different lanes are then not ordered at all.
+    launch (optional, CUDA): the lean form of render_band, launch(row0, rows, row_step,
+    out_ptr, prev_ptr, pitch, stream_handle) with device pointers, the row pitch in pixels and the
+    part's HIP stream; frames whose lanes need no event ordering (one lane, or independent) then
+    enqueue from precomputed arguments with no torch stream switches or tensor views (~4 us per
+    launch on the host instead of ~20: a band of a k-GPU split at k = 8 renders in ~11 us).
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
                  channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
-                 lanes: int = 1, independent: bool = False):
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+                 lanes: int = 1, independent: bool = False, launch: Optional[Callable] = None,
+                 world: Optional[int] = None, rank: Optional[int] = None):
+        # world / rank: override the process group's (one process rehearsing rank `rank` of a
+        # `world`-way split on one GPU; no exchange may then be requested)
+        self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
+        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
+        if world is not None and gather:
+            raise ValueError("a rehearsed split keeps its band (gather=False)")
         self.group = group
         self.width, self.height, self.parts = width, height, parts
         self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
@@ -151,6 +161,19 @@ class FrameTiler:
                              for _ in range(2)]
             if self.cuda:
                 self.assembly_stream = torch.cuda.Stream(device=device)
+        self.plan = None   # lean launches: per lane, per part (row0, rows, step, out, prev, pitch, stream)
+        if (launch is not None and not self.gather and self.part_streams is not None
+                and (lanes == 1 or independent)):
+            self.launch = launch
+            self.plan = []
+            for g in range(lanes):
+                out_b, prev_b = self.bufs[g], self.bufs[(g - 1) % lanes]
+                row = []
+                for q, (row0, rows, step) in enumerate(self.specs):
+                    o, pv = self.part_rows(out_b, q), self.part_rows(prev_b, q)
+                    row.append((row0, rows, step, o.data_ptr(), pv.data_ptr(), row_pitch(o),
+                                self.part_streams[g][q].cuda_stream))
+                self.plan.append(row)
         self.pending = [None, None]     # gather that still reads bands[b]
         self.assembled = [None, None]   # rank 0: assembly that still reads gathered[b]
         self.prev = None                # rank 0: buffer index of the frame awaiting assembly
@@ -204,6 +227,18 @@ class FrameTiler:
 
     # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
+        if self.plan is not None:   # lean launches from precomputed arguments
+            lane = self.k % self.lanes
+            self.k += 1
+            if self.fresh:
+                cur = torch.cuda.current_stream()
+                for ln in self.part_streams:
+                    for st in ln:
+                        st.wait_stream(cur)
+                self.fresh = False
+            for args in self.plan[lane]:
+                self.launch(*args)
+            return self.bufs[lane]
         if not self.gather:   # one rank, or ranks that keep their bands: no exchange
             lane = self.k % self.lanes
             band, prev = self.bufs[lane], self.bufs[(self.k - 1) % self.lanes]

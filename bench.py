@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--parts", type=int, default=0,
                     help="interleaved row parts per frame, each on its own HIP stream (tiles.py); "
                          "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
+    ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1],
+                    help="1: pixels the certified walks cannot settle are rendered by a second, "
+                         "compacted exact pass (vrt_set_exact_pass); 0: in their own lanes")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
@@ -229,6 +232,7 @@ def main():
     vox_dev = torch.from_numpy(vox_host).to(dev)
     broadcast_volume(vox_dev)
     ren = vrt.Renderer(local)
+    ren.set_exact_pass(bool(args.exact_pass))
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
 
     def launch(row0, rows, step, out, prev, cnt_ptr=0):

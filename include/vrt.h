@@ -213,6 +213,15 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
  * (ABI v9: the old stream is never touched; its owner may have destroyed it). */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
+/* ABI v9: deferred exact pass for stats-free launches with certified pixels (vrt_certified() == 1):
+ * on = 1 (default): the certified pass renders the pixels its certified walks settle and records,
+ * per wave, the lane mask of the others (glass hits, near-edge walks); a second kernel on the same
+ * stream renders those with the exact path, compacted into dense waves. off = 0: the exact path
+ * runs in the pixel's own lane, with the heavy-first tile order (vrt_set_tile_order). Bands over
+ * 65536 tiles, and launches on a stream being captured into a graph, use the in-lane path. Images
+ * are identical either way. */
+int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
+
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
  * pairs, out = n float3. Synchronous. */
 int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,

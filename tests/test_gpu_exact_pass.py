@@ -1,0 +1,98 @@
+"""GPU: the deferred exact pass (vrt_set_exact_pass, ABI v9). A certified pass renders the pixels
+its certified walks settle and records, per wave, the lane mask of the others; a second kernel
+renders those with the exact path, compacted into dense waves (ballot masks, a popcount scan
+across the wave, binary search + select-bit per lane: no atomics). Images must be bit-identical
+to the in-lane fallback and to the exact STATS instance, frame after frame, on scenes where many
+pixels defer (glass cube: most pixels; random sparse volumes with every byte; near-edge cameras)
+and with the temporal filter reading its history (alpha 0.5), including bands (row steps),
+pitched output and band heights that leave partial tiles."""
+import numpy as np
+import pytest
+import torch
+
+import voxelraytracer_amd as vrt
+
+pytestmark = pytest.mark.gpu
+
+
+def frames(r, cam, n_frames, R, T, alpha, row0, rows, step, w, exact_pass, counters=False, **kw):
+    r.set_exact_pass(exact_pass)
+    hist = torch.zeros((rows, w, 4), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
+    out = []
+    for t in range(n_frames):
+        p = vrt.default_params(R, T, time=float(t + 1), **kw)
+        r.render_temporal_rows_async(cam, p, alpha, row0, rows, step, hist.data_ptr(), hist.data_ptr(),
+                                     d_counters=cnt.data_ptr() if counters else 0,
+                                     stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        out.append(hist.cpu().numpy().copy())
+    return out
+
+
+def random_volume(n, seed, density=0.02):
+    rng = np.random.default_rng(seed)
+    v = np.zeros(n ** 3, np.uint8)
+    idx = rng.choice(n ** 3, int(density * n ** 3), replace=False)
+    v[idx] = rng.integers(1, 6, len(idx))
+    return v
+
+
+CASES = [
+    ("refraction", 128, 480, 270, 4, 4, 0, 270, 1, {}),
+    ("glass_cube", 64, 320, 180, 1, 2, 0, 180, 1, {}),
+    ("terrain", 128, 384, 216, 4, 2, 1, 53, 4, dict(ray_noise=0.02)),
+    ("random", 32, 256, 150, 4, 4, 0, 150, 1, {}),
+    ("random", 64, 200, 99, 2, 3, 2, 33, 3, dict(reflection_noise=0.01)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}{c[1]}_{c[2]}x{c[3]}" for c in CASES])
+def test_exact_pass_is_bit_identical(built, case):
+    scene, n, w, h, R, T, row0, rows, step, kw = case
+    vox = random_volume(n, n) if scene == "random" else vrt.build_scene(scene, n)
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vox, n)
+        r.set_certified(1)   # certified pixels also on glass-heavy volumes: many deferred pixels
+        cam = vrt.make_camera(w, h)
+        a = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, True, **kw)
+        b = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, False, **kw)
+        ref = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, True, counters=True, **kw)
+    for k in range(3):
+        assert np.array_equal(a[k], ref[k]), f"exact pass, frame {k}"
+        assert np.array_equal(b[k], ref[k]), f"in-lane, frame {k}"
+
+
+def test_exact_pass_lattice_cameras(built):
+    """Cameras on lattice points and diagonals (exact ties: many near-edge, deferred pixels)."""
+    n, w, h = 64, 160, 90
+    vox = vrt.build_scene("refraction", n)
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vox, n)
+        for pos, rot in [((0.0, 0.0, 0.0), (-45.0, -45.0, 0.0)), ((1.0, 2.0, -3.0), (0.0, 0.0, 0.0)),
+                         ((-2.5, 0.5, 1.5), (-35.26439, 45.0, 0.0))]:
+            cam = vrt.make_camera(w, h, pos=pos, rot=rot)
+            a = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, True)
+            ref = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, True, counters=True)
+            assert np.array_equal(a[0], ref[0]), pos
+
+
+def test_exact_pass_toggled_between_frames(built):
+    """The exact pass switched on and off between frames on one stream: the deferred-pixel list's
+    counter sets are reset whenever the slot's previous launch was not a deferred one."""
+    n, w, h = 128, 320, 180
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("refraction", n), n)
+        cam = vrt.make_camera(w, h)
+        hist = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
+        ref = torch.zeros_like(hist)
+        cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        for t, on in enumerate([True, False, True, True, False, False, True, True, True]):
+            p = vrt.default_params(4, 4, time=float(t + 1), ray_noise=0.01 * (t % 2))
+            r.set_exact_pass(on)
+            r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, hist.data_ptr(), hist.data_ptr(), stream=s)
+            r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, ref.data_ptr(), ref.data_ptr(),
+                                         d_counters=cnt.data_ptr(), stream=s)
+            torch.cuda.synchronize()
+            assert torch.equal(hist, ref), f"frame {t} (exact pass {on})"

@@ -250,6 +250,10 @@ class Renderer:
         """Heavy-first tile order for stats-free launches (default on; images are identical)."""
         self._check(self._lib.vrt_set_tile_order(self._h, 1 if on else 0), "vrt_set_tile_order")
 
+    def set_exact_pass(self, on: bool):
+        """Deferred exact pass for certified launches (default on; images are identical)."""
+        self._check(self._lib.vrt_set_exact_pass(self._h, 1 if on else 0), "vrt_set_exact_pass")
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 

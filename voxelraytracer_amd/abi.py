@@ -113,6 +113,7 @@ SIGNATURES = {
     "vrt_set_certified": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_certified": (C.c_int, [C.c_void_p]),
     "vrt_set_tile_order": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_set_exact_pass": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_set_launch_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_launch_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "vrt_render": (

@@ -43,6 +43,10 @@ constexpr int kLanes = 4;
 constexpr int kOrderSlots = 16;        // tile-order buffers per device (band geometry x stream)
 constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 65536 16x8 tiles (4096 x 2048 pixels)
 constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 2u * vrt::kOrdClasses;  // KArgs::order
+// KArgs::defer: two sets of segment counters, then the list: a pixel per word, 8 segments of
+// ceil(tiles / 8) tiles' pixels each
+constexpr size_t kDeferSegWords = size_t(kOrderMaxTiles) / vrt::kOrdClasses * vrt::kWgThreads;
+constexpr size_t kDeferSlotWords = vrt::kDeferHdr + vrt::kOrdClasses * kDeferSegWords;
 // first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
 // 8160 tiles are heavy)
 #if defined(VRT_ORD_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
@@ -67,6 +71,8 @@ struct OrderSlot {
   uint32_t* d = nullptr;       // kOrderSlotWords words inside the shard's pool
   bool used = false;
   uint64_t epoch = 0, tick = 0;
+  uint64_t defer_epoch = 0;    // deferred-pass launches since the slot's counters were zeroed
+  bool last_defer = false;     // the slot's last launch was a deferred-pass launch
 };
 
 struct Shard {
@@ -105,8 +111,9 @@ struct Shard {
   // textured mode's atlas (RGBA8 words)
   uint32_t* d_atlas = nullptr;
   int32_t atlas_size = 0;
-  // heavy-first tile order
+  // heavy-first tile order, and the deferred exact pass's per-wave masks (same slots)
   uint32_t* d_order_pool = nullptr;
+  uint32_t* d_defer_pool = nullptr;
   OrderSlot order[kOrderSlots];
   uint64_t order_tick = 0;
 };
@@ -121,6 +128,7 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
+  bool exact_pass = true;               // vrt_set_exact_pass
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
   // timestamps (2 per launch, created up front), and how many are in use since the last read
   std::vector<hipEvent_t> lt_ev;
@@ -197,7 +205,7 @@ void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
   std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats,
                              (void*)s.d_cnt, (void*)s.d_cnt_rep, (void*)s.d_out, (void*)s.d_hit,
-                             (void*)s.d_atlas, (void*)s.d_order_pool};
+                             (void*)s.d_atlas, (void*)s.d_order_pool, (void*)s.d_defer_pool};
   for (int r = 0; r < kRing; ++r) {
     bufs.push_back(s.d_ring[r]);
     bufs.push_back(s.d_rawbuf[r]);
@@ -247,6 +255,8 @@ hipError_t shard_init(Shard& s, int device) {
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt_rep, rep_bytes);
   if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
   if (e == hipSuccess) e = hipMalloc(&s.d_order_pool, pool_words * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipMalloc(&s.d_defer_pool, size_t(kOrderSlots) * kDeferSlotWords * sizeof(uint32_t));
   for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) s.order[i].d = s.d_order_pool + size_t(i) * kOrderSlotWords;
   return e;
 }
@@ -339,6 +349,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
   a.order = nullptr;
   a.ord_r = a.ord_w = a.ctr_r = a.ctr_w = a.ctr_z = a.ord_q = 0;
+  a.defer = nullptr;
+  a.defer_e = a.defer_seg = 0;
   return a;
 }
 
@@ -350,13 +362,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
 // destroyed by its owner, so no event is recorded on it. Then the slot is zeroed on this stream
 // (no heavy tiles yet). Not while the stream is being captured into a graph (a replayed node
 // would reuse one list / counter set): dispatch order then.
-OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
-  // only where it pays: glass in the volume (without it the order gains nothing: C2 ±0, C4 +5 %,
-  // profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where every tile is
-  // heavy, keep dispatch order: C1 +3.4 %)
-  if (!ctx->tile_order || a.tiles == 0 || a.tiles > kOrderMaxTiles || a.textured || a.cert != 2 ||
-      !s.has_glass)
-    return nullptr;
+OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
+  if (a.tiles == 0 || a.tiles > kOrderMaxTiles) return nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
   OrderSlot* slot = nullptr;
@@ -378,9 +385,38 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
     slot->row_step = a.row_step;
     slot->stream = st;
     slot->epoch = 0;
+    slot->last_defer = false;
     slot->used = true;
   }
   slot->tick = ++s.order_tick;
+  return slot;
+}
+
+// Per-launch state of a stats-free launch from its slot: the deferred exact pass's mask buffer
+// (certified colour-only launches, vrt_set_exact_pass), else the heavy-first tile order.
+void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
+  const bool defer = ctx->exact_pass && !a.textured && a.cert == 2;
+  // the tile order only where it pays: glass in the volume (without it the order gains nothing:
+  // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
+  // every tile is heavy, keep dispatch order: C1 +3.4 %)
+  const bool order = !defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass;
+  if (!defer && !order) return;
+  OrderSlot* slot = acquire_slot(s, a, st);
+  if (!slot) return;
+  if (defer) {  // both counter sets zeroed whenever the slot's previous launch was not one
+    uint32_t* d = s.d_defer_pool + size_t(slot - s.order) * kDeferSlotWords;
+    if (!slot->last_defer) {
+      if (hipMemsetAsync(d, 0, vrt::kDeferHdr * sizeof(uint32_t), st) != hipSuccess) return;
+      slot->defer_epoch = 0;
+    }
+    a.defer = d;
+    a.defer_e = uint32_t(slot->defer_epoch & 1u);
+    a.defer_seg = uint32_t((a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * uint32_t(vrt::kWgThreads);
+    slot->defer_epoch++;
+    slot->last_defer = true;
+    return;
+  }
+  slot->last_defer = false;
   a.order = slot->d;
   a.ord_r = uint32_t(slot->epoch & 1u);
   a.ord_w = a.ord_r ^ 1u;
@@ -389,7 +425,6 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
   a.ctr_z = (a.ctr_r + 2u) % 3u;
   a.ord_q = (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
   slot->epoch++;
-  return slot;
 }
 
 // One band launch on `st` (heavy-first tile order for uncounted launches), then, when counting,
@@ -398,7 +433,7 @@ OrderSlot* tile_order_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStre
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
             hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr) {
   const bool stats = hit || cnt;
-  if (!stats) tile_order_begin(ctx, s, a, st);
+  if (!stats) launch_state_begin(ctx, s, a, st);
   vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
 }
@@ -957,6 +992,14 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
   if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
   ctx->tile_order = on != 0;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0 or 1");
+  ctx->exact_pass = on != 0;
   ctx->err.clear();
   return VRT_OK;
 }

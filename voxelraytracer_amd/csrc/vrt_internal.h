@@ -45,6 +45,15 @@ struct KArgs {
   // slots per class (grid = 8 * ord_q + tiles)
   uint32_t* order;
   uint32_t tiles_x, tiles, ord_r, ord_w, ctr_r, ctr_w, ctr_z, ord_q;
+  // deferred exact pass (stats-free certified launches, vrt_set_exact_pass): nullptr = the exact
+  // path runs in the certified pixel's own lane; else the certified pass appends the pixels that
+  // need the exact path to a list (one atomic per wave with such pixels, on one of kOrdClasses
+  // segment counters by workgroup % 8) and the exact pass renders them 64 to a wave. defer: the
+  // launch slot's words (2 counter sets, then the list); defer_e: the counter set of this launch
+  // (the exact pass zeroes the other one for the next launch on the stream); defer_seg: list
+  // words per segment (a segment holds at most ceil(tiles / 8) tiles' pixels)
+  uint32_t* defer;
+  uint32_t defer_e, defer_seg;
 };
 
 // Waves per workgroup, each rendering an 8x8 pixel tile. Two (a 16x8 tile): a finished
@@ -67,6 +76,8 @@ constexpr int kCntReplicas = 256;           // counter replicas (per-wave atomic
 constexpr uint32_t kOrdClasses = 8;         // tile-order lists: tile % 8 (the XCD of its slot)
 constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 256-byte line each)
 constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
+constexpr uint32_t kDeferHdr = 2 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 counter sets
+constexpr uint32_t kDeferGridDiv = 32;      // exact-pass workgroups per certified-pass waves (grid size)
 
 // ---- launches (vrt_render.hip); all asynchronous on `s` ------------------------------------
 

@@ -1899,8 +1899,11 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // arithmetic is the same source in both instances. TEX: textured mode (!_COLOR_ONLY).
 // CERT (stats-free colour-only instances): 0 exact walks only, 1 certified walks for the exact
 // path's shadow and air-medium secondary rays, 2 also whole pixels first.
-template <bool STATS, bool TEX, int CERT = 0, bool ORD = false>
-__global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
+// DEFER (certified instances): pixels that need the exact path are not rendered here; their lane
+// mask per wave goes to a.defer and exact_pass_kernel renders them compacted (see there).
+// (The certified pass without the exact path fits 64 VGPRs with no scratch: 8 waves per SIMD.)
+template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false>
+__global__ void __launch_bounds__(kWgThreads, DEFER ? 8 : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
@@ -1923,6 +1926,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
   const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
   bool heavy = false;  // this lane took the exact path (tile order: the tile runs long next frame)
+  bool deferred = false;  // DEFER: this lane's pixel is left to the exact pass
 
   Counters k;
 #pragma unroll
@@ -1955,7 +1959,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       g_stamps2[wave_lin][1] = n_exact;
     }
 #endif
-    if (need_exact) {
+    if constexpr (DEFER) {
+      deferred = need_exact;
+    } else if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
       heavy = true;
       (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
@@ -1970,7 +1976,24 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       hr.flags = flags;
       hits[o] = hr;
     }
-    store_pixel(a, out, o, color);
+    if (!deferred) store_pixel(a, out, o, color);
+  }
+  if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
+    const unsigned long long m = __ballot(deferred);
+    if (m != 0ull) {
+      const uint32_t seg = blockIdx.x % kOrdClasses;
+      uint32_t base = 0;
+      if (lane_id() == uint32_t(__builtin_ctzll(m)))
+        base = atomicAdd(a.defer + (a.defer_e * kOrdClasses + seg) * kOrdCtrStride,
+                         uint32_t(__builtin_popcountll(m)));
+      base = uint32_t(__builtin_amdgcn_readlane(int(base), int(__builtin_ctzll(m))));
+      if (deferred) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        const uint32_t l3 = lane_id();  // the pixel re-derived (not kept live across the walks)
+        a.defer[kDeferHdr + seg * a.defer_seg + base + rank] =
+            (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
+      }
+    }
   }
 
   if constexpr (ORD) {
@@ -1997,6 +2020,82 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) render_kernel(KArgs
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
       if (lane_id() == 0 && v) atomicAdd(slot + q, v);
     }
+  }
+}
+
+// The r-th (from 0) set bit of m (r < popcount(m)): binary search on popcounts
+__device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r) {
+  uint32_t pos = 0;
+  uint32_t lo = uint32_t(m);
+  const uint32_t nlo = uint32_t(__builtin_popcount(lo));
+  uint32_t w = lo;
+  if (r >= nlo) {
+    r -= nlo;
+    pos = 32;
+    w = uint32_t(m >> 32);
+  }
+#pragma unroll
+  for (uint32_t half = 16; half > 0; half >>= 1) {
+    const uint32_t low = w & ((1u << half) - 1u);
+    const uint32_t n = uint32_t(__builtin_popcount(low));
+    if (r >= n) {
+      r -= n;
+      pos += half;
+      w >>= half;
+    } else {
+      w = low;
+    }
+  }
+  return pos;
+}
+
+// The deferred exact pass: the pixels a certified pass (render_kernel<..., DEFER>) appended to
+// its list, rendered with the exact path 64 to a wave — the certified pass's waves end with their
+// certified pixels, and the exact walks that would each have held a sparse wave of them run
+// densely here (the north_star's __ballot compaction of live rays). Batch b is list entries
+// [64 b, 64 b + 64) over the segments in order; batches b, b + gridDim.x, ... per workgroup.
+// Every deferred pixel is rendered exactly once, with the same exact path and epilogue as the
+// in-lane fallback, so images are identical. Workgroup 0 zeroes the other counter set for the
+// next launch on the stream (none of this launch's kernels reads it).
+template <bool TEX, int CERT>
+__global__ void __launch_bounds__(64, VRT_MIN_WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
+                                                                     float4* __restrict__ out) {
+  const uint32_t lane = lane_id();
+  const uint32_t* ctr = a.defer + a.defer_e * kOrdClasses * kOrdCtrStride;
+  if (blockIdx.x == 0 && lane < kOrdClasses) a.defer[((a.defer_e ^ 1u) * kOrdClasses + lane) * kOrdCtrStride] = 0u;
+  uint32_t n[kOrdClasses], total = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kOrdClasses; ++q) {
+    n[q] = ctr[q * kOrdCtrStride];
+    total += n[q];
+  }
+  if (blockIdx.x * 64u >= total) return;
+  Ctx c;
+  init_ctx(c, a, vox);
+  __shared__ float4 ax_tab[64 * 3];
+  c.ax = &ax_tab[lane * kAxLane];
+  for (uint32_t base = blockIdx.x * 64u; base < total; base += gridDim.x * 64u) {
+    uint32_t idx = base + lane;
+    if (idx >= total) continue;
+    uint32_t seg = 0;
+#pragma unroll
+    for (uint32_t q = 0; q + 1u < kOrdClasses; ++q) {
+      const bool past = seg == q && idx >= n[q];
+      idx -= past ? n[q] : 0u;
+      seg += past ? 1u : 0u;
+    }
+    const uint32_t e = a.defer[kDeferHdr + seg * a.defer_seg + idx];
+    const int px = int(e & 0xFFFFu), li = int(e >> 16);
+    const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
+    Counters k;
+#pragma unroll
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
+    uint32_t steps = 0, flags = 0;
+    int32_t hit_vidx = -1;
+    float hit_len = 0.0f;
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
   }
 }
 
@@ -2201,6 +2300,22 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // ~5 %), exact walks only (0)
   // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
   // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
+  if (a.defer && !stats && !a.textured && a.cert == 2) {
+    // certified pass, then the exact pass over the pixels it deferred (no tile order: the
+    // certified pass has no long waves)
+    const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+    if (ev_begin)
+      hipExtLaunchKernelGGL((render_kernel<false, false, 2, false, true>), g1, dim3(kWgThreads), 0, s, ev_begin,
+                            nullptr, 0, a, vox, out, hit, cnt_rep);
+    else
+      hipLaunchKernelGGL((render_kernel<false, false, 2, false, true>), g1, dim3(kWgThreads), 0, s, a, vox, out, hit,
+                         cnt_rep);
+    if (ev_end)
+      hipExtLaunchKernelGGL((exact_pass_kernel<false, 2>), g2, dim3(64), 0, s, nullptr, ev_end, 0, a, vox, out);
+    else
+      hipLaunchKernelGGL((exact_pass_kernel<false, 2>), g2, dim3(64), 0, s, a, vox, out);
+    return;
+  }
   auto kern = a.textured ? (stats ? render_kernel<true, true>
                                   : (a.cert >= 1 ? render_kernel<false, true, 1> : render_kernel<false, true>))
                          : (stats ? render_kernel<true, false>

@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1],
                     help="1: pixels the certified walks cannot settle are rendered by a second, "
                          "compacted exact pass (vrt_set_exact_pass); 0: in their own lanes")
+    ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
+                    help="certified pixels (vrt_set_certified): 0 automatic, 1 always, -1 never")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
@@ -233,6 +235,7 @@ def main():
     broadcast_volume(vox_dev)
     ren = vrt.Renderer(local)
     ren.set_exact_pass(bool(args.exact_pass))
+    ren.set_certified(args.certified)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
 
     def launch(row0, rows, step, out, prev, cnt_ptr=0):

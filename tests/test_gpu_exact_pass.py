@@ -96,3 +96,49 @@ def test_exact_pass_toggled_between_frames(built):
                                          d_counters=cnt.data_ptr(), stream=s)
             torch.cuda.synchronize()
             assert torch.equal(hist, ref), f"frame {t} (exact pass {on})"
+
+
+def ref_atlas():
+    """The reference's own textures (res/textures/*128.png) in the ABI atlas layout."""
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "atlas", "atlas_ref128.npz")
+    return np.load(path, allow_pickle=False)["atlas"]
+
+
+TEX_CASES = [
+    ("refraction", 128, 480, 270, 4, 4, "ref"),
+    ("terrain", 128, 384, 216, 4, 2, "ref"),
+    ("glass_cube", 64, 320, 180, 1, 2, "synthetic"),
+    ("refraction", 64, 256, 144, 2, 2, "synthetic"),
+]
+
+
+@pytest.mark.parametrize("case", TEX_CASES, ids=[f"{c[0]}{c[1]}_{c[6]}" for c in TEX_CASES])
+def test_textured_certified_pixels_bit_identical(built, case):
+    """Textured frames (the reference's default build, voxel.glsl:6) with certified pixels: the
+    texel of a certified hit is certified from the hit's error interval on its face plane
+    (cert_texel), the rest is deferred to the exact pass. Identical to the exact instance and to
+    the in-lane path (exact primaries), frame after frame at alpha 0.5."""
+    scene, n, w, h, R, T, which = case
+    atlas = ref_atlas() if which == "ref" else vrt.make_atlas()
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        r.set_certified(1)
+        cam = vrt.make_camera(w, h)
+        out = {}
+        for mode, ep, counters in (("defer", True, False), ("inlane", False, False), ("exact", True, True)):
+            r.set_exact_pass(ep)
+            hist = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
+            cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
+            seq = []
+            for t in range(3):
+                p = vrt.textured_params(vrt.default_params(R, T, time=float(t + 1)), atlas)
+                r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, hist.data_ptr(), hist.data_ptr(),
+                                             d_counters=cnt.data_ptr() if counters else 0,
+                                             stream=torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                seq.append(hist.cpu().numpy().copy())
+            out[mode] = seq
+    for t in range(3):
+        assert np.array_equal(out["defer"][t], out["exact"][t]), f"deferred, frame {t}"
+        assert np.array_equal(out["inlane"][t], out["exact"][t]), f"in-lane, frame {t}"

@@ -395,7 +395,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
 // Per-launch state of a stats-free launch from its slot: the deferred exact pass's mask buffer
 // (certified colour-only launches, vrt_set_exact_pass), else the heavy-first tile order.
 void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
-  const bool defer = ctx->exact_pass && !a.textured && a.cert == 2;
+  const bool defer = ctx->exact_pass && a.cert == 2;
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
   // every tile is heavy, keep dispatch order: C1 +3.4 %)

@@ -1201,9 +1201,10 @@ __device__ __forceinline__ Hit cert_hit_record(const Ray& ray, const CertResult&
 // TraceWithShadow's colour update (voxel.glsl:395-418) for a certified hit of `ray`: the shadow
 // bit by a certified shadow walk from the hit, unless it cannot change the brightness (lit ==
 // ambient). false: unsure (colour untouched).
+template <bool TEX = false>
 __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, const CertResult& h,
-                                               const Hit& hh, f3& color) {
-  const float lit = lit_brightness<false>(hh, c.sun_n, ray.dir);
+                                               const Hit& hh, f3& color, float4 col = float4()) {
+  const float lit = lit_brightness<TEX>(hh, c.sun_n, ray.dir);
   float brightness = kAmbient;
   if (lit != kAmbient) {  // otherwise in shadow or not, the brightness is the ambient term
     const f3 S = c.sun_n;
@@ -1227,7 +1228,10 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
   } else {
     CERT_DIAG(4);
   }
-  apply_hit_color<false>(c, hh, ray.energy, brightness, color);
+  if (!TEX) col = get_color<false>(c, hh);  // textured: the certified texel (cert_texel)
+  color.x = mixf(color.x, col.x * col.w * brightness, ray.energy);
+  color.y = mixf(color.y, col.y * col.w * brightness, ray.energy);
+  color.z = mixf(color.z, col.z * col.w * brightness, ray.energy);
   return true;
 }
 
@@ -1528,6 +1532,52 @@ __device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Coun
 // written only when the pixel certifies. false when any walk or any derived value could differ
 // from the exact path's, or the hit is glass (its secondary rays start at the exact hit point):
 // the pixel then takes the exact path.
+// Textured mode: the texel GetColor (voxel.glsl:174-182) reads at the exact hit point, from the
+// certified hit. The exact hit point is currentPos of the exact walk's hit step; on each face axis
+// it lies within delta = eu |D_b| + the roundings of both points' pos + s dir of the certified
+// point (eu bounds the exact walk's parameter there, cert_gamma). get_color's texel index is a
+// composition of correctly rounded monotone operations of the coordinate (frac by floor, + texX,
+// x ts, / S, floor(. x S)), so if both ends of [p - delta, p + delta] lie in the same voxel and give
+// the same texel, every point between does: the exact texel is that one. false: unsure.
+__device__ __forceinline__ bool texel_pair(const Ctx& c, float p, float d, uint32_t slot, bool flip, uint32_t& t) {
+  const float lo = p - d, hi = p + d;
+  if (__builtin_floorf(lo) != __builtin_floorf(hi)) return false;
+  auto idx = [&](float q) {
+    const float f = q - floorf(q);
+    if (!flip) {  // tx = ((fx + texX) * ts) / S, u = tx
+      const float u = ((f + float(slot)) * c.atlas_fts) / c.atlas_fs;
+      return cvt_flr(u * c.atlas_fs) & c.atlas_mask;
+    }
+    const float ty = (((1.0f - f) + float(slot)) * c.atlas_fts) / c.atlas_fs;  // v = 1 - ty
+    return cvt_flr((1.0f - ty) * c.atlas_fs) & c.atlas_mask;
+  };
+  t = idx(lo);
+  return t == idx(hi);
+}
+
+__device__ __forceinline__ bool cert_texel(const Ctx& c, const Ray& ray, const CertResult& h, const Hit& hh,
+                                           float4& col) {
+  const uint32_t m = mat_id(h.byte);
+  const float px = hh.axis == 0 ? hh.point.z : hh.point.x;  // intersectionAxis[a][1]
+  const float py = hh.axis == 2 ? hh.point.y : (hh.axis == 1 ? hh.point.z : hh.point.y);  // [a][2]
+  const float dx = hh.axis == 0 ? ray.dir.z : ray.dir.x;
+  const float dy = hh.axis == 2 ? ray.dir.y : (hh.axis == 1 ? ray.dir.z : ray.dir.y);
+  const float px0 = hh.axis == 0 ? ray.pos.z : ray.pos.x;
+  const float py0 = hh.axis == 2 ? ray.pos.y : (hh.axis == 1 ? ray.pos.z : ray.pos.y);
+  // eu along the ray, plus 2 ulp-scale roundings of each point's P + s D (both points), doubled
+  const float ex = h.eu * __builtin_fabsf(dx) +
+                   0x1p-21f * (__builtin_fabsf(px0) + __builtin_fabsf(h.u * dx) + __builtin_fabsf(px) + 1.0f);
+  const float ey = h.eu * __builtin_fabsf(dy) +
+                   0x1p-21f * (__builtin_fabsf(py0) + __builtin_fabsf(h.u * dy) + __builtin_fabsf(py) + 1.0f);
+  uint32_t i, j;
+  if (!texel_pair(c, px, ex, mat_tex_x(m), false, i) || !texel_pair(c, py, ey, mat_tex_y(m), true, j)) return false;
+  const uint32_t t = c.atlas[j * (c.atlas_mask + 1u) + i];
+  col = make_float4(float(t & 0xFFu) / 255.0f, float((t >> 8) & 0xFFu) / 255.0f,
+                    float((t >> 16) & 0xFFu) / 255.0f, float(t >> 24) / 255.0f);
+  return true;
+}
+
+template <bool TEX = false>
 __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out) {
   const f3 P = ray0.pos, D = ray0.dir;
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
@@ -1557,7 +1607,10 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
     CERT_DIAG(3);
     return false;
   }
-  if (!cert_shade_hit(c, ray0, h, cert_hit_record(ray0, h), color)) return false;
+  const Hit hh = cert_hit_record(ray0, h);
+  float4 col = float4();
+  if (TEX && !cert_texel(c, ray0, h, hh, col)) return false;
+  if (!cert_shade_hit<TEX>(c, ray0, h, hh, color, col)) return false;
   color_out = color;
   return true;
 }
@@ -1950,7 +2003,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? 8 : VRT_MIN_WAVES) render_
     // colour in LDS, or storing certified pixels before the exact path and re-deriving the
     // primary ray there, was 4-6 % slower.
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    const bool need_exact = CERT < 2 || !cert_pixel(c, ray, color);
+    const bool need_exact = CERT < 2 || !cert_pixel<TEX>(c, ray, color);
 #ifdef VRT_STAMPS
     const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
     const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
@@ -2300,20 +2353,20 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // ~5 %), exact walks only (0)
   // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
   // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
-  if (a.defer && !stats && !a.textured && a.cert == 2) {
+  if (a.defer && !stats && a.cert == 2) {
     // certified pass, then the exact pass over the pixels it deferred (no tile order: the
     // certified pass has no long waves)
     const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+    auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
+    auto k2 = a.textured ? exact_pass_kernel<true, 1> : exact_pass_kernel<false, 2>;
     if (ev_begin)
-      hipExtLaunchKernelGGL((render_kernel<false, false, 2, false, true>), g1, dim3(kWgThreads), 0, s, ev_begin,
-                            nullptr, 0, a, vox, out, hit, cnt_rep);
+      hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);
     else
-      hipLaunchKernelGGL((render_kernel<false, false, 2, false, true>), g1, dim3(kWgThreads), 0, s, a, vox, out, hit,
-                         cnt_rep);
+      hipLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, a, vox, out, hit, cnt_rep);
     if (ev_end)
-      hipExtLaunchKernelGGL((exact_pass_kernel<false, 2>), g2, dim3(64), 0, s, nullptr, ev_end, 0, a, vox, out);
+      hipExtLaunchKernelGGL(k2, g2, dim3(64), 0, s, nullptr, ev_end, 0, a, vox, out);
     else
-      hipLaunchKernelGGL((exact_pass_kernel<false, 2>), g2, dim3(64), 0, s, a, vox, out);
+      hipLaunchKernelGGL(k2, g2, dim3(64), 0, s, a, vox, out);
     return;
   }
   auto kern = a.textured ? (stats ? render_kernel<true, true>

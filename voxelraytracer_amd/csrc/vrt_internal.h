@@ -77,7 +77,16 @@ constexpr uint32_t kOrdClasses = 8;         // tile-order lists: tile % 8 (the X
 constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 256-byte line each)
 constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
 constexpr uint32_t kDeferHdr = 2 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 counter sets
-constexpr uint32_t kDeferGridDiv = 32;      // exact-pass workgroups per certified-pass waves (grid size)
+#if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEFER_GRID_DIV is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_DEFER_GRID_DIV
+#define VRT_DEFER_GRID_DIV 8
+#endif
+// certified-pass waves per exact-pass workgroup (the exact pass's grid; a workgroup loops over the
+// batches beyond it): 8 covers textured frames' deferred pixels in one batch per workgroup (textured
+// C3 0.0843 -> 0.0713 ms against 32; 4 no better; profiles/r03_s11, r03_s12)
+constexpr uint32_t kDeferGridDiv = VRT_DEFER_GRID_DIV;
 
 // ---- launches (vrt_render.hip); all asynchronous on `s` ------------------------------------
 

@@ -1954,9 +1954,20 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // path's shadow and air-medium secondary rays, 2 also whole pixels first.
 // DEFER (certified instances): pixels that need the exact path are not rendered here; their lane
 // mask per wave goes to a.defer and exact_pass_kernel renders them compacted (see there).
-// (The certified pass without the exact path fits 64 VGPRs with no scratch: 8 waves per SIMD.)
+// The certified pass without the exact path fits 64 VGPRs (8 waves per SIMD) with 8 bytes of
+// scratch, but runs faster at 7 (72 VGPRs, no spills): C3 0.0464 -> 0.0447, C4 0.1751 -> 0.1605,
+// textured C3 -4 % (profiles/r03_s11, r03_s12); 6 is slower again.
+#if (defined(VRT_DEFER_WAVES) || defined(VRT_EXACT_WAVES)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEFER_WAVES / VRT_EXACT_WAVES are A/B knobs of make variant builds"
+#endif
+#ifndef VRT_DEFER_WAVES
+#define VRT_DEFER_WAVES 7
+#endif
+#ifndef VRT_EXACT_WAVES
+#define VRT_EXACT_WAVES VRT_MIN_WAVES
+#endif
 template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false>
-__global__ void __launch_bounds__(kWgThreads, DEFER ? 8 : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
+__global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
@@ -2111,7 +2122,7 @@ __device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r)
 // in-lane fallback, so images are identical. Workgroup 0 zeroes the other counter set for the
 // next launch on the stream (none of this launch's kernels reads it).
 template <bool TEX, int CERT>
-__global__ void __launch_bounds__(64, VRT_MIN_WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
+__global__ void __launch_bounds__(64, VRT_EXACT_WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t lane = lane_id();
   const uint32_t* ctr = a.defer + a.defer_e * kOrdClasses * kOrdCtrStride;

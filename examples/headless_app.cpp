@@ -21,6 +21,7 @@
 //   - Utils::Screenshot of the last frame (key F1, :424-428) -> a binary PPM (--ppm), and the raw
 //     RGBA8 frame (--raw, row 0 = bottom) for tests
 // Build: make app (-> build/vrt_headless). Usage: build/vrt_headless --help
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -44,7 +45,7 @@ struct Options {
   std::string atlas_raw;       // textured mode: raw RGBA8 atlas file (size^2 * 4 bytes)
   int atlas_size = 256, atlas_tile = 128;
   std::string ppm, raw;
-  bool quiet = false, counters = false, pipelined = false;
+  bool quiet = false, counters = false, pipelined = false, caller_stream = false;
   uint32_t device_mask = 1;  // bit i = HIP device i
   int warmup = 0;            // frames excluded from the reported mean
 };
@@ -55,7 +56,7 @@ void usage() {
       "             [--bounces R T] [--alpha A] [--ray-noise x] [--reflection-noise x]\n"
       "             [--refraction-noise x] [--day-night SECONDS_PER_FRAME] [--reset-at K]\n"
       "             [--atlas-raw FILE --atlas-size S --atlas-tile T] [--ppm FILE] [--raw FILE]\n"
-      "             [--device-mask M] [--counters] [--warmup K] [--pipelined] [--quiet]");
+      "             [--device-mask M] [--counters] [--warmup K] [--pipelined [--caller-stream]] [--quiet]");
 }
 
 bool parse(int argc, char** argv, Options& o) {
@@ -90,6 +91,7 @@ bool parse(int argc, char** argv, Options& o) {
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--counters") o.counters = true;
     else if (a == "--pipelined") o.pipelined = true;
+    else if (a == "--caller-stream") o.caller_stream = true;
     else if (a == "--device-mask") o.device_mask = uint32_t(std::strtoul(next(a.c_str()), nullptr, 0));
     else if (a == "--warmup") o.warmup = std::atoi(next("--warmup"));
     else if (a == "--help" || a == "-h") return false;
@@ -191,6 +193,11 @@ int main(int argc, char** argv) {
   float time_of_day = 0.9f * day_time;  // "Make day" (main.cpp:577)
   std::vector<uint8_t> frame(size_t(o.width) * o.height * 4);
   if (o.pipelined) {  // display path: device frames, no per-frame host sync
+    // Default: no caller stream (ABI v9) — each frame is consumed on the stream that produced it
+    // (vrt_frame_stream), the display path with no ordering packet between streams; time per
+    // frame = wall time of the timed frames between two device synchronisations (GPU-bound).
+    // --caller-stream: the frames are ordered on this host's own stream instead (each frame makes
+    // it wait), timed with hipEvents on it.
     const uint32_t* d_frame = nullptr;
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -200,12 +207,21 @@ int main(int argc, char** argv) {
       vrt_destroy(rt);
       return 1;
     }
+    hipStream_t cs = o.caller_stream ? s : nullptr;
+    auto t0 = std::chrono::steady_clock::now();
     for (int f = 0; f < o.frames && status == 0; ++f) {
-      if (f == o.warmup) (void)hipEventRecord(e0, s);
+      if (f == o.warmup) {
+        if (cs) {
+          (void)hipEventRecord(e0, s);
+        } else {
+          if (hipDeviceSynchronize() != hipSuccess) status = 1;
+          t0 = std::chrono::steady_clock::now();
+        }
+      }
       if (f == o.reset_at) vrt_history_reset(rt);
       p.time = float(f + 1);
       vrt_sun_dir(time_of_day, day_time, p.sun_dir);
-      if (vrt_render_frame_device(rt, &cam, &p, o.alpha, s, &d_frame, nullptr) != VRT_OK) {
+      if (vrt_render_frame_device(rt, &cam, &p, o.alpha, cs, &d_frame, nullptr) != VRT_OK) {
         std::fprintf(stderr, "vrt_render_frame_device: %s\n", vrt_last_error(rt));
         status = 1;
       }
@@ -214,16 +230,24 @@ int main(int argc, char** argv) {
         while (time_of_day > day_time) time_of_day -= day_time;
       }
     }
-    (void)hipEventRecord(e1, s);
-    if (status == 0 && hipMemcpyAsync(frame.data(), d_frame, frame.size(), hipMemcpyDeviceToHost, s) != hipSuccess)
-      status = 1;
-    if (hipStreamSynchronize(s) != hipSuccess) status = 1;
     float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (cs) {
+      (void)hipEventRecord(e1, s);
+    } else if (status == 0) {
+      if (hipDeviceSynchronize() != hipSuccess) status = 1;
+      ms = float(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    // the last frame to the host on the stream it is consumed on
+    hipStream_t consume = cs ? cs : static_cast<hipStream_t>(vrt_frame_stream(rt));
+    if (status == 0 && hipMemcpyAsync(frame.data(), d_frame, frame.size(), hipMemcpyDeviceToHost, consume) != hipSuccess)
+      status = 1;
+    if (hipStreamSynchronize(consume) != hipSuccess) status = 1;
+    if (cs) (void)hipEventElapsedTime(&ms, e0, e1);
     const int timed = o.frames - o.warmup;
     if (status == 0 && timed > 0)
-      std::printf("pipelined: timed %d frames (after %d warm-up) on %d device(s): mean %.4f ms GPU time per frame\n",
-                  timed, o.warmup, vrt_device_count(rt), ms / timed);
+      std::printf("pipelined (%s): timed %d frames (after %d warm-up) on %d device(s): mean %.4f ms per frame\n",
+                  cs ? "caller stream, GPU time" : "frame streams, wall time", timed, o.warmup,
+                  vrt_device_count(rt), ms / timed);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipStreamDestroy(s);

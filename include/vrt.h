@@ -214,12 +214,14 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* ABI v9: deferred exact pass for stats-free launches with certified pixels (vrt_certified() == 1):
- * on = 1 (default): the certified pass renders the pixels its certified walks settle and records,
- * per wave, the lane mask of the others (glass hits, near-edge walks); a second kernel on the same
- * stream renders those with the exact path, compacted into dense waves. off = 0: the exact path
- * runs in the pixel's own lane, with the heavy-first tile order (vrt_set_tile_order). Bands over
- * 65536 tiles, and launches on a stream being captured into a graph, use the in-lane path. Images
- * are identical either way. */
+ * on = 1 (default): the certified pass renders the pixels its certified walks settle and appends
+ * the others (glass hits, near-edge walks, textured hits near a texel edge) to a list; a second
+ * kernel on the same stream renders those with the exact path, 64 to a wave. It pays when other
+ * work overlaps the exact pass: the async band entry points and the device-output frames (frames
+ * in flight) use it; the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the
+ * in-lane path. off = 0: the exact path runs in the pixel's own lane, with the heavy-first tile
+ * order (vrt_set_tile_order). Bands over 65536 tiles, and launches on a stream being captured into a
+ * graph, use the in-lane path. Images are identical either way. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
@@ -326,10 +328,20 @@ int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* para
  * at u_Alpha = 1 a frame does not read its history and up to four frames are in flight (ABI v9);
  * otherwise part q of a frame waits only for part q of the frame before (its history rows).
  * Returns after the launches; stats may be NULL (then no host sync happens; with stats the call
- * waits for the frame). */
+ * waits for the frame).
+ * ABI v9: hip_stream = NULL orders nothing with the caller's streams. The caller then consumes the
+ * frame on the stream that produced it (vrt_frame_stream, right after the call): work enqueued
+ * there runs after the frame and before the frame that next reuses its buffer (the eighth later
+ * call), so no ordering packet crosses streams (with a caller stream, each frame's wait costs
+ * ~0.01-0.02 ms of GPU throughput at C3); the host blocks only when it is eight
+ * frames ahead of the GPU. */
 int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params,
                             float alpha, void* hip_stream, const uint32_t** d_frame,
                             vrt_stats* stats);
+
+/* ABI v9: the HIP stream (hipStream_t) that rendered (or, with several devices, assembled) the last
+ * device-output frame of a hip_stream = NULL call, on the first device; NULL before one. */
+void* vrt_frame_stream(const vrt_ctx* ctx);
 
 /* "Clear framebuffer" (key F, main.cpp:417-421): the last ray-traced frame becomes the history of
  * the next frame. ABI v9: no buffer changes hands (a device-output frame the caller holds keeps

@@ -120,8 +120,9 @@ def test_frame_device_output(built, devs):
         assert len(set(ptrs)) == len(ptrs)   # ring of eight slots
 
 
-@pytest.mark.parametrize("devs", [0, [0, 0]], ids=["k1", "k2"])
-def test_device_frames_mixed_counted_and_alpha(built, devs):
+@pytest.mark.parametrize("devs,null_stream", [(0, False), ([0, 0], False), (0, True), ([0, 0], True)],
+                         ids=["k1", "k2", "k1-frame-stream", "k2-frame-stream"])
+def test_device_frames_mixed_counted_and_alpha(built, devs, null_stream):
     """Device-output frames in flight (u_Alpha = 1: one launch per frame on rotating lanes) mixed
     with counted frames (the exact instance, one launch) and u_Alpha < 1 frames (two parts, each
     waiting for its history rows on another lane), plus a synchronous frame in between: every
@@ -142,12 +143,18 @@ def test_device_frames_mixed_counted_and_alpha(built, devs):
                 f, _ = r.render_frame(cam, p, a)
                 assert np.array_equal(f, ref[i]), f"sync frame {i}"
                 continue
-            ptr, st = r.render_frame_device(cam, p, a, s.cuda_stream, counters=i in counted)
+            ptr, st = r.render_frame_device(cam, p, a, 0 if null_stream else s.cuda_stream,
+                                            counters=i in counted)
             if i in counted:
                 assert st["pixels"] == w * h
-            torch.cuda.current_stream().wait_stream(s)
             got = np.empty((h, w, 4), np.uint8)
-            hipcopy(got, ptr)
+            if null_stream:   # consumed on the frame's own stream (vrt_frame_stream)
+                fs = r.frame_stream()
+                assert fs
+                hipcopy_on(got, ptr, fs)
+            else:
+                torch.cuda.current_stream().wait_stream(s)
+                hipcopy(got, ptr)
             assert np.array_equal(got, ref[i]), f"frame {i}"
 
 
@@ -192,6 +199,20 @@ def test_history_reset_keeps_held_frames(built, alpha):
                 assert np.array_equal(got, refs[j]), f"frame {j} read after frame {i}"
 
 
+def hipcopy_on(dst: np.ndarray, ptr: int, stream_handle: int):
+    """Device -> host copy of a raw device pointer enqueued on a raw HIP stream (the frame's own
+    stream), then a wait for that stream."""
+    class View:
+        __cuda_array_interface__ = {"shape": dst.shape, "typestr": "|u1", "data": (ptr, False),
+                                    "version": 3}
+
+    ext = torch.cuda.ExternalStream(stream_handle)
+    with torch.cuda.stream(ext):
+        t = torch.as_tensor(View(), device="cuda").to("cpu", non_blocking=False)
+    ext.synchronize()
+    dst[...] = t.numpy()
+
+
 def hipcopy(dst: np.ndarray, ptr: int):
     """Device -> host copy of a raw device pointer, viewed as a torch tensor through
     __cuda_array_interface__."""
@@ -206,8 +227,9 @@ def hipcopy(dst: np.ndarray, ptr: int):
 
 def test_headless_app_gets_the_bench_frame_time(built, tmp_path):
     """vrt_headless (C++ over the C-ABI) at C3 in its display-path mode (--pipelined:
-    vrt_render_frame_device into a device buffer, no per-frame host sync): GPU time per frame within
-    10 % of bench.py's per-frame GPU time of the same workload (both uncounted, certified, four
+    vrt_render_frame_device with no caller stream, each frame consumed on the stream that produced
+    it, no per-frame host sync): time per frame within 10 % of bench.py's per-frame GPU time of the
+    same workload; the caller-stream form (--caller-stream) renders the same frames (both uncounted, certified, four
     frames in flight), the C++ host raising HIP's hardware-queue count itself as INTEGRATION.md
     asks (no GPU_MAX_HW_QUEUES in its environment). The synchronous loop
     (vrt_render_frame, which waits for each frame as the reference's blocking GL timer query did)
@@ -217,11 +239,16 @@ def test_headless_app_gets_the_bench_frame_time(built, tmp_path):
     env.pop("GPU_MAX_HW_QUEUES", None)
     base = [APP, "--scene", "refraction", "--n", "128", "--size", "1920x1080", "--bounces", "4", "4",
             "--frames", "400", "--warmup", "200", "--quiet"]
-    raw_p, raw_s = tmp_path / "p.rgba", tmp_path / "s.rgba"
+    raw_p, raw_s, raw_c = tmp_path / "p.rgba", tmp_path / "s.rgba", tmp_path / "c.rgba"
     r = subprocess.run(base + ["--pipelined", "--raw", str(raw_p)], capture_output=True, text=True,
                        timeout=180, env=env)
     assert r.returncode == 0, r.stderr
     app_ms = float(re.search(r"mean ([0-9.]+) ms", r.stdout).group(1))
+    rc = subprocess.run(base + ["--pipelined", "--caller-stream", "--raw", str(raw_c)], capture_output=True,
+                        text=True, timeout=180, env=env)
+    assert rc.returncode == 0, rc.stderr
+    caller_ms = float(re.search(r"mean ([0-9.]+) ms", rc.stdout).group(1))
+    assert raw_c.read_bytes() == raw_p.read_bytes()
     r2 = subprocess.run(base + ["--raw", str(raw_s)], capture_output=True, text=True, timeout=180, env=env)
     assert r2.returncode == 0, r2.stderr
     sync_ms = float(re.search(r"mean ([0-9.]+) ms", r2.stdout).group(1))
@@ -232,8 +259,8 @@ def test_headless_app_gets_the_bench_frame_time(built, tmp_path):
     assert b.returncode == 0, b.stderr[-2000:]
     out = json.loads([l for l in b.stdout.splitlines() if l.startswith("{")][-1])
     bench_ms = out["roofline"]["kernel_ms"]
-    print(f"vrt_headless pipelined {app_ms:.4f} ms/frame, synchronous {sync_ms:.4f} ms/frame, "
-          f"bench {bench_ms:.4f} ms/frame")
+    print(f"vrt_headless pipelined {app_ms:.4f} ms/frame (frame streams), {caller_ms:.4f} ms/frame "
+          f"(caller stream), synchronous {sync_ms:.4f} ms/frame, bench {bench_ms:.4f} ms/frame")
     assert app_ms <= 1.10 * bench_ms, (app_ms, bench_ms)
 
 

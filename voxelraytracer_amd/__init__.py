@@ -352,6 +352,11 @@ class Renderer:
         stats["kernel_ms"] = float(st.kernel_ms)
         return ptr.value, stats
 
+    def frame_stream(self) -> int:
+        """vrt_frame_stream: the HIP stream that produced the last device frame of a stream = 0
+        (NULL) render_frame_device call; consume that frame there."""
+        return self._lib.vrt_frame_stream(self._h) or 0
+
     def set_launch_timing(self, launches: int):
         """vrt_set_launch_timing: device start/end timestamps for the next `launches` async band
         launches (0: off)."""

@@ -160,6 +160,7 @@ SIGNATURES = {
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_void_p,
          C.POINTER(C.c_void_p), C.POINTER(Stats)],
     ),
+    "vrt_frame_stream": (C.c_void_p, [C.c_void_p]),
     "vrt_history_reset": (C.c_int, [C.c_void_p]),
     "vrt_upload_atlas": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
     "vrt_debug_randomize": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_float,

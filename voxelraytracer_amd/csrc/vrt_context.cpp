@@ -49,6 +49,10 @@ constexpr size_t kDeferSegWords = size_t(kOrderMaxTiles) / vrt::kOrdClasses * vr
 constexpr size_t kDeferSlotWords = vrt::kDeferHdr + vrt::kOrdClasses * kDeferSegWords;
 // first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
 // 8160 tiles are heavy)
+#if (defined(VRT_DEV_NOQUERY) || defined(VRT_DEV_NOCONSUME) || defined(VRT_DEV_NOCSWAIT)) && \
+    !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEV_* are diagnostic knobs of make variant builds"
+#endif
 #if defined(VRT_ORD_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_ORD_DIV is an A/B knob of make variant builds"
 #endif
@@ -147,6 +151,12 @@ struct vrt_ctx {
   hipEvent_t ev_consumed[kRing] = {};
   bool consumed_valid[kRing] = {};
   hipEvent_t ev_gathered = nullptr;     // first device: the last device-output frame is assembled
+  // device-output frames with no caller stream (vrt_frame_stream): the stream that rendered (or
+  // assembled) the last frame, and per ring slot the end of the frame rendered into it (host
+  // back-pressure: at most kRing frames ahead)
+  hipStream_t frame_stream = nullptr;
+  hipEvent_t ev_slot[kRing] = {};
+  bool slot_valid[kRing] = {};
   void* h_stage = nullptr;              // pinned host staging of synchronous frames (k bands in)
   size_t h_stage_bytes = 0;
   std::string err;
@@ -394,8 +404,11 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
 
 // Per-launch state of a stats-free launch from its slot: the deferred exact pass's mask buffer
 // (certified colour-only launches, vrt_set_exact_pass), else the heavy-first tile order.
-void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st) {
-  const bool defer = ctx->exact_pass && a.cert == 2;
+// allow_defer: false for frames that run alone (synchronous calls): there the exact pass's
+// latency after the certified pass is the frame's (C3 0.198 vs 0.076 ms per synchronous frame),
+// while frames in flight hide it
+void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
+  const bool defer = allow_defer && ctx->exact_pass && a.cert == 2;
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
   // every tile is heavy, keep dispatch order: C1 +3.4 %)
@@ -431,9 +444,9 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
 // the fold of the counter replicas into `cnt` (accumulating). ev_begin / ev_end: optional device
 // timestamps of the kernel's start and end.
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
-            hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr) {
+            hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr, bool allow_defer = true) {
   const bool stats = hit || cnt;
-  if (!stats) launch_state_begin(ctx, s, a, st);
+  if (!stats) launch_state_begin(ctx, s, a, st, allow_defer);
   vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
 }
@@ -583,6 +596,8 @@ int ensure_history(vrt_ctx* ctx, int32_t w, int32_t h) {
   ctx->reset_pending = false;
   for (bool& v : ctx->raw_is_cur) v = false;
   for (bool& v : ctx->consumed_valid) v = false;
+  for (bool& v : ctx->slot_valid) v = false;
+  ctx->frame_stream = nullptr;
   return VRT_OK;
 }
 
@@ -609,14 +624,16 @@ int wait_lane(vrt_ctx* ctx, Shard& s, int l, hipStream_t st) {
 //  - wait_consumed: the caller's consumption of the device-output frame in this slot.
 // timing: device timestamps of every launch (vrt_stats.kernel_ms; synchronous calls only).
 int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha, bool rgba8,
-                 bool hits, bool counting, bool timing, bool overlap, hipEvent_t wait_consumed = nullptr) {
+                 bool hits, bool counting, bool timing, bool overlap, hipEvent_t wait_consumed = nullptr,
+                 bool one_part = false) {
   const int32_t k = int32_t(ctx->sh.size()), w = cam->width, h = cam->height;
   const uint64_t f = ctx->fk;
   const int g = int(f % kLanes), slot = int(f % kRing), pslot = int((f + kRing - 1) % kRing);
   // the kernel reads the history iff u_Alpha != 1 (store_pixel, vrt_render.hip)
   const bool hist = rgba8 && alpha != 1.0f;
   const bool single = counting || hits;  // one counter replica set: one counted launch
-  const int nparts = single || (overlap && !hist) ? 1 : kParts;
+  // one_part: device-output frames consumed on their own stream (vrt_frame_stream)
+  const int nparts = single || one_part || (overlap && !hist) ? 1 : kParts;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
     VRT_HIP(ctx, hipSetDevice(s.device));
@@ -662,10 +679,10 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
         a.prev = hsrc + off;
         a.cur = s.d_ring[slot] + off;
         a.raw = hist ? s.d_rawbuf[slot] + off : nullptr;
-        launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.ls[g][q], kb, ke);
+        launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.ls[g][q], kb, ke, overlap);
       } else {
         launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
-               s.ls[g][q], kb, ke);
+               s.ls[g][q], kb, ke, overlap);
       }
       VRT_HIP(ctx, hipGetLastError());
       VRT_HIP(ctx, hipEventRecord(s.ev_done[g][q], s.ls[g][q]));
@@ -758,6 +775,78 @@ int stage_bands(vrt_ctx* ctx, int g, int32_t w, int32_t h, const void* const* ba
   return VRT_OK;
 }
 
+// Several devices (or the one-device RCCL rehearsal): frame f's bands (launched on lane g) to the
+// first device — ncclGather over xGMI on every device's gather stream, or device-to-device copies
+// when a device repeats — then placed into their rows of d_frames[slot] on the first device's
+// gather stream (after `reuse`, the caller's consumption of that buffer, when given); ev_gathered
+// marks the assembled frame.
+int gather_frame(vrt_ctx* ctx, int32_t w, int32_t h, int slot, int g, hipEvent_t reuse, const uint32_t** d_frame) {
+  const int32_t k = int32_t(ctx->sh.size());
+  Shard& root = ctx->sh[0];
+  int st;
+  const int32_t cap = band_cap(h, k);
+  const size_t row = size_t(w) * 4;
+  const uint32_t* src[64];
+  if (ctx->distinct) {  // RCCL gather of the equal-size bands to the first device over xGMI
+    if (!ctx->d_gather || size_t(k) * size_t(cap) * size_t(w) > ctx->hist_pixels_gather) {
+      VRT_HIP(ctx, hipDeviceSynchronize());
+      if (ctx->d_gather) (void)hipFree(ctx->d_gather);
+      ctx->d_gather = nullptr;
+      ctx->hist_pixels_gather = 0;
+      const size_t need = size_t(k) * size_t(cap) * size_t(w);
+      if (hipMalloc(&ctx->d_gather, need * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc gather");
+      ctx->hist_pixels_gather = need;
+    }
+    for (int32_t j = 0; j < k; ++j) {  // each device's gather stream after its band's launches
+      Shard& s = ctx->sh[j];
+      VRT_HIP(ctx, hipSetDevice(s.device));
+      if ((st = wait_lane(ctx, s, g, s.gs)) != VRT_OK) return st;
+    }
+    VRT_NCCL(ctx, ncclGroupStart());
+    for (int32_t j = 0; j < k; ++j) {
+      Shard& s = ctx->sh[j];
+      (void)hipSetDevice(s.device);
+      const ncclResult_t r = ncclGather(s.d_ring[slot], j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
+                                        ncclUint8, 0, ctx->comms[j], s.gs);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(ctx, r, "ncclGather(bands)");
+      }
+    }
+    VRT_NCCL(ctx, ncclGroupEnd());
+    for (int32_t j = 0; j < k; ++j) {  // the band's next writer (frame f + kRing) waits for this
+      Shard& s = ctx->sh[j];
+      VRT_HIP(ctx, hipSetDevice(s.device));
+      VRT_HIP(ctx, hipEventRecord(s.ev_band_read[slot], s.gs));
+      s.band_read_valid[slot] = true;
+    }
+    for (int32_t j = 0; j < k; ++j) src[j] = ctx->d_gather + size_t(j) * cap * w;
+  } else {  // a device repeats: copy the bands device to device on the first device's stream
+    VRT_HIP(ctx, hipSetDevice(root.device));
+    for (int32_t j = 0; j < k; ++j)
+      for (int q = 0; q < ctx->sh[j].lane_parts[g]; ++q)
+        VRT_HIP(ctx, hipStreamWaitEvent(root.gs, ctx->sh[j].ev_done[g][q], 0));
+    for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_ring[slot];
+  }
+  VRT_HIP(ctx, hipSetDevice(root.device));
+  if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.gs, reuse, 0));
+  uint32_t* out = ctx->d_frames[slot];
+  for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
+    const int32_t hb = band_rows(h, k, j);
+    if (hb > 0)
+      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + size_t(j) * row, size_t(k) * row, src[j], row,
+                                    row, size_t(hb), hipMemcpyDeviceToDevice, root.gs));
+  }
+  if (!ctx->distinct)
+    for (int32_t j = 0; j < k; ++j) {  // same physical device: the bands were read here
+      VRT_HIP(ctx, hipEventRecord(ctx->sh[j].ev_band_read[slot], root.gs));
+      ctx->sh[j].band_read_valid[slot] = true;
+    }
+  VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.gs));
+  *d_frame = out;
+  return VRT_OK;
+}
+
 int create(const std::vector<int>& devs, vrt_ctx** out) {
   if (!out) return VRT_ERR_INVALID;
   *out = nullptr;
@@ -781,6 +870,8 @@ int create(const std::vector<int>& devs, vrt_ctx** out) {
       hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming) != hipSuccess ||
       [&] {
         for (hipEvent_t& e : c->ev_consumed)
+          if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
+        for (hipEvent_t& e : c->ev_slot)
           if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return true;
         return false;
       }()) {
@@ -832,6 +923,8 @@ void vrt_destroy(vrt_ctx* c) {
     for (uint32_t* f : c->d_frames)
       if (f) (void)hipFree(f);
     for (hipEvent_t e : c->ev_consumed)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_slot)
       if (e) (void)hipEventDestroy(e);
     if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -1173,92 +1266,73 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   const uint64_t f = ctx->fk;
   const int slot = int(f % kRing), g = int(f % kLanes);
   VRT_HIP(ctx, hipSetDevice(root.device));
+  if (!cs) {
+    // no caller stream (ABI v9): the caller consumes each frame on the stream that produced it
+    // (vrt_frame_stream), which renders the frame that next reuses its buffer, kRing frames later,
+    // after that consumption: no ordering packet between streams. One launch per band (so that one
+    // stream holds the whole frame), and the host stays at most kRing frames ahead.
+    if (ctx->slot_valid[slot] && hipEventQuery(ctx->ev_slot[slot]) != hipSuccess)
+      VRT_HIP(ctx, hipEventSynchronize(ctx->ev_slot[slot]));
+    if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true, nullptr, true)) !=
+        VRT_OK)
+      return st;
+    if (k == 1 && !ctx->coll1) {
+      ctx->frame_stream = root.ls[g][0];
+      *d_frame = root.d_ring[slot];
+    } else {
+      if ((st = gather_frame(ctx, w, h, slot, g, nullptr, d_frame)) != VRT_OK) return st;
+      ctx->frame_stream = root.gs;
+    }
+    VRT_HIP(ctx, hipSetDevice(root.device));
+    VRT_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->frame_stream));
+    ctx->slot_valid[slot] = true;
+    ctx->fk++;
+    if (stats && (st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
+    ctx->err.clear();
+    return VRT_OK;
+  }
   // E_f: whatever the caller enqueued on its stream so far (its consumption of frames <= f - 1)
   VRT_HIP(ctx, hipEventRecord(ctx->ev_consumed[slot], cs));
   ctx->consumed_valid[slot] = true;
   // Frame f overwrites the buffer handed out at frame f - kRing, which the caller's work before
-  // call f - kRing + 1 consumed: E_{f-kRing+1}. No wait when the host sees it done already.
+  // call f - kRing + 1 consumed: E_{f-kRing+1}. The host waits for it when it is not done yet
+  // (the caller's stream is more than kRing - 1 frames behind): a swapchain's back-pressure, with
+  // no ordering packet on the GPU. (Waiting for it on the lane's stream cost 0.016 ms per C3 frame:
+  // the cross-queue wait packets stalled the lanes; scripts/diag/devframe_ab.py, profiles/r03_s14.)
   hipEvent_t reuse = nullptr;
   if (f >= kRing) {
     const int rs = int((f - kRing + 1) % kRing);
-    if (ctx->consumed_valid[rs] && hipEventQuery(ctx->ev_consumed[rs]) != hipSuccess) reuse = ctx->ev_consumed[rs];
+#if defined(VRT_DEV_NOQUERY)  // diagnostic builds: the wait on the GPU (the r03 s13 scheme) / none (unsafe)
+    if (ctx->consumed_valid[rs]) reuse = ctx->ev_consumed[rs];
+#elif defined(VRT_DEV_NOCONSUME)
+    (void)rs;
+#else
+    if (ctx->consumed_valid[rs] && hipEventQuery(ctx->ev_consumed[rs]) != hipSuccess)
+      VRT_HIP(ctx, hipEventSynchronize(ctx->ev_consumed[rs]));
+#endif
   }
   if (k == 1 && !ctx->coll1) {
     // one device: the frame is rendered straight into the ring slot handed to the caller; up to
     // kLanes frames in flight (u_Alpha = 1: independent frames)
     if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true, reuse)) != VRT_OK)
       return st;
+#ifndef VRT_DEV_NOCSWAIT  // diagnostic builds only: the caller's stream not ordered after the frame (unsafe)
     for (int q = 0; q < root.lane_parts[g]; ++q) VRT_HIP(ctx, hipStreamWaitEvent(cs, root.ev_done[g][q], 0));
+#endif
     *d_frame = root.d_ring[slot];
   } else {
     if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true)) != VRT_OK) return st;
-    const int32_t cap = band_cap(h, k);
-    const size_t row = size_t(w) * 4;
-    const uint32_t* src[64];
-    if (ctx->distinct) {  // RCCL gather of the equal-size bands to the first device over xGMI
-      if (!ctx->d_gather || size_t(k) * size_t(cap) * size_t(w) > ctx->hist_pixels_gather) {
-        VRT_HIP(ctx, hipDeviceSynchronize());
-        if (ctx->d_gather) (void)hipFree(ctx->d_gather);
-        ctx->d_gather = nullptr;
-        ctx->hist_pixels_gather = 0;
-        const size_t need = size_t(k) * size_t(cap) * size_t(w);
-        if (hipMalloc(&ctx->d_gather, need * 4) != hipSuccess) return fail(ctx, VRT_ERR_OOM, "hipMalloc gather");
-        ctx->hist_pixels_gather = need;
-      }
-      for (int32_t j = 0; j < k; ++j) {  // each device's gather stream after its band's launches
-        Shard& s = ctx->sh[j];
-        VRT_HIP(ctx, hipSetDevice(s.device));
-        if ((st = wait_lane(ctx, s, g, s.gs)) != VRT_OK) return st;
-      }
-      VRT_NCCL(ctx, ncclGroupStart());
-      for (int32_t j = 0; j < k; ++j) {
-        Shard& s = ctx->sh[j];
-        (void)hipSetDevice(s.device);
-        const ncclResult_t r = ncclGather(s.d_ring[slot], j == 0 ? ctx->d_gather : nullptr, size_t(cap) * row,
-                                          ncclUint8, 0, ctx->comms[j], s.gs);
-        if (r != ncclSuccess) {
-          (void)ncclGroupEnd();
-          return nccl_fail(ctx, r, "ncclGather(bands)");
-        }
-      }
-      VRT_NCCL(ctx, ncclGroupEnd());
-      for (int32_t j = 0; j < k; ++j) {  // the band's next writer (frame f + kRing) waits for this
-        Shard& s = ctx->sh[j];
-        VRT_HIP(ctx, hipSetDevice(s.device));
-        VRT_HIP(ctx, hipEventRecord(s.ev_band_read[slot], s.gs));
-        s.band_read_valid[slot] = true;
-      }
-      for (int32_t j = 0; j < k; ++j) src[j] = ctx->d_gather + size_t(j) * cap * w;
-    } else {  // a device repeats: copy the bands device to device on the first device's stream
-      VRT_HIP(ctx, hipSetDevice(root.device));
-      for (int32_t j = 0; j < k; ++j)
-        for (int q = 0; q < ctx->sh[j].lane_parts[g]; ++q)
-          VRT_HIP(ctx, hipStreamWaitEvent(root.gs, ctx->sh[j].ev_done[g][q], 0));
-      for (int32_t j = 0; j < k; ++j) src[j] = ctx->sh[j].d_ring[slot];
-    }
+    if ((st = gather_frame(ctx, w, h, slot, g, reuse, d_frame)) != VRT_OK) return st;
     VRT_HIP(ctx, hipSetDevice(root.device));
-    if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.gs, reuse, 0));
-    uint32_t* out = ctx->d_frames[slot];
-    for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
-      const int32_t hb = band_rows(h, k, j);
-      if (hb > 0)
-        VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + size_t(j) * row, size_t(k) * row, src[j], row,
-                                      row, size_t(hb), hipMemcpyDeviceToDevice, root.gs));
-    }
-    if (!ctx->distinct)
-      for (int32_t j = 0; j < k; ++j) {  // same physical device: the bands were read here
-        VRT_HIP(ctx, hipEventRecord(ctx->sh[j].ev_band_read[slot], root.gs));
-        ctx->sh[j].band_read_valid[slot] = true;
-      }
-    VRT_HIP(ctx, hipEventRecord(ctx->ev_gathered, root.gs));
     VRT_HIP(ctx, hipStreamWaitEvent(cs, ctx->ev_gathered, 0));
-    *d_frame = out;
   }
   ctx->fk++;
   if (stats && (st = finish_frame(ctx, stats, counting)) != VRT_OK) return st;
   ctx->err.clear();
   return VRT_OK;
 }
+
+void* vrt_frame_stream(const vrt_ctx* ctx) { return ctx ? static_cast<void*>(ctx->frame_stream) : nullptr; }
 
 int vrt_debug_collectives(vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;

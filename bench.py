@@ -91,9 +91,10 @@ def parse():
     ap.add_argument("--parts", type=int, default=0,
                     help="interleaved row parts per frame, each on its own HIP stream (tiles.py); "
                          "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
-    ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1],
-                    help="1: pixels the certified walks cannot settle are rendered by a second, "
-                         "compacted exact pass (vrt_set_exact_pass); 0: in their own lanes")
+    ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1, 2],
+                    help="pixels the certified walks cannot settle rendered by a second, compacted "
+                         "exact pass (vrt_set_exact_pass): 1 automatic (launches of >= 2 rounds of "
+                         "resident waves), 2 always, 0 never (in their own lanes)")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
                     help="certified pixels (vrt_set_certified): 0 automatic, 1 always, -1 never")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -234,7 +235,7 @@ def main():
     vox_dev = torch.from_numpy(vox_host).to(dev)
     broadcast_volume(vox_dev)
     ren = vrt.Renderer(local)
-    ren.set_exact_pass(bool(args.exact_pass))
+    ren.set_exact_pass(args.exact_pass)
     ren.set_certified(args.certified)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
 

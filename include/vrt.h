@@ -214,12 +214,14 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
 /* ABI v9: deferred exact pass for stats-free launches with certified pixels (vrt_certified() == 1):
- * on = 1 (default): the certified pass renders the pixels its certified walks settle and appends
+ * on = 1 (default, automatic) or 2 (always, whatever the band size: tests and A/B timing): the
+ * certified pass renders the pixels its certified walks settle and appends
  * the others (glass hits, near-edge walks, textured hits near a texel edge) to a list; a second
  * kernel on the same stream renders those with the exact path, 64 to a wave. It pays when other
- * work overlaps the exact pass: the async band entry points and the device-output frames (frames
- * in flight) use it; the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the
- * in-lane path. off = 0: the exact path runs in the pixel's own lane, with the heavy-first tile
+ * work overlaps the exact pass and the launch is large: the async band entry points and the
+ * device-output frames (frames in flight) use it for bands of at least two rounds of resident
+ * waves (CUs x 4 x 7 x 2 waves: 14336, e.g. 1920 x 960 pixels, on MI355X); smaller bands and the
+ * synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path. off = 0: the exact path runs in the pixel's own lane, with the heavy-first tile
  * order (vrt_set_tile_order). Bands over 65536 tiles, and launches on a stream being captured into a
  * graph, use the in-lane path. Images are identical either way. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);

@@ -55,9 +55,9 @@ def test_exact_pass_is_bit_identical(built, case):
         r.upload_volume(vox, n)
         r.set_certified(1)   # certified pixels also on glass-heavy volumes: many deferred pixels
         cam = vrt.make_camera(w, h)
-        a = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, True, **kw)
-        b = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, False, **kw)
-        ref = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, True, counters=True, **kw)
+        a = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 2, **kw)   # deferred, any size
+        b = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 0, **kw)
+        ref = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 2, counters=True, **kw)
     for k in range(3):
         assert np.array_equal(a[k], ref[k]), f"exact pass, frame {k}"
         assert np.array_equal(b[k], ref[k]), f"in-lane, frame {k}"
@@ -72,8 +72,8 @@ def test_exact_pass_lattice_cameras(built):
         for pos, rot in [((0.0, 0.0, 0.0), (-45.0, -45.0, 0.0)), ((1.0, 2.0, -3.0), (0.0, 0.0, 0.0)),
                          ((-2.5, 0.5, 1.5), (-35.26439, 45.0, 0.0))]:
             cam = vrt.make_camera(w, h, pos=pos, rot=rot)
-            a = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, True)
-            ref = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, True, counters=True)
+            a = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, 2)
+            ref = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, 2, counters=True)
             assert np.array_equal(a[0], ref[0]), pos
 
 
@@ -88,7 +88,7 @@ def test_exact_pass_toggled_between_frames(built):
         ref = torch.zeros_like(hist)
         cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
         s = torch.cuda.current_stream().cuda_stream
-        for t, on in enumerate([True, False, True, True, False, False, True, True, True]):
+        for t, on in enumerate([2, 0, 2, 2, 0, 0, 2, 1, 2]):
             p = vrt.default_params(4, 4, time=float(t + 1), ray_noise=0.01 * (t % 2))
             r.set_exact_pass(on)
             r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, hist.data_ptr(), hist.data_ptr(), stream=s)
@@ -126,7 +126,7 @@ def test_textured_certified_pixels_bit_identical(built, case):
         r.set_certified(1)
         cam = vrt.make_camera(w, h)
         out = {}
-        for mode, ep, counters in (("defer", True, False), ("inlane", False, False), ("exact", True, True)):
+        for mode, ep, counters in (("defer", 2, False), ("inlane", 0, False), ("exact", 2, True)):
             r.set_exact_pass(ep)
             hist = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
             cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")

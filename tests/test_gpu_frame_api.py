@@ -135,6 +135,7 @@ def test_device_frames_mixed_counted_and_alpha(built, devs, null_stream):
     ref = sequence(0, scene, n, w, h, R, T, alphas)
     with vrt.Renderer(devs) as r:
         r.upload_volume(vrt.build_scene(scene, n), n)
+        r.set_exact_pass(2)   # deferred exact passes at this small size too (automatic: in-lane)
         cam = vrt.make_camera(w, h)
         s = torch.cuda.Stream()
         for i, a in enumerate(alphas):

@@ -250,9 +250,10 @@ class Renderer:
         """Heavy-first tile order for stats-free launches (default on; images are identical)."""
         self._check(self._lib.vrt_set_tile_order(self._h, 1 if on else 0), "vrt_set_tile_order")
 
-    def set_exact_pass(self, on: bool):
-        """Deferred exact pass for certified launches (default on; images are identical)."""
-        self._check(self._lib.vrt_set_exact_pass(self._h, 1 if on else 0), "vrt_set_exact_pass")
+    def set_exact_pass(self, mode):
+        """Deferred exact pass for certified launches: 0/False off, 1/True automatic (default:
+        bands of at least two rounds of resident waves), 2 always. Images are identical."""
+        self._check(self._lib.vrt_set_exact_pass(self._h, int(mode)), "vrt_set_exact_pass")
 
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0

@@ -81,6 +81,7 @@ struct OrderSlot {
 
 struct Shard {
   int device = 0;
+  uint32_t wave_slots = 7168;  // resident waves of the certified pass: CUs x 4 SIMDs x 7
   // volume: canonical N^3, distance scratch, the kernel's packed octant volumes
   uint8_t* d_vox = nullptr;
   uint8_t* d_tmp = nullptr;
@@ -132,7 +133,7 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
-  bool exact_pass = true;               // vrt_set_exact_pass
+  int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 always
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
   // timestamps (2 per launch, created up front), and how many are in use since the last read
   std::vector<hipEvent_t> lt_ev;
@@ -242,6 +243,10 @@ void shard_free(Shard& s) {
 hipError_t shard_init(Shard& s, int device) {
   s.device = device;
   hipError_t e = hipSetDevice(device);
+  int cus = 0;
+  if (e == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      cus > 0)
+    s.wave_slots = uint32_t(cus) * 4u * 7u;
   const size_t rep_bytes = sizeof(unsigned long long) * vrt::kCntReplicas * VRT_CNT_COUNT;
   const size_t pool_words = size_t(kOrderSlots) * kOrderSlotWords;
   // ordering markers without timestamps (timing events make the command processor stamp and
@@ -406,9 +411,15 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
 // (certified colour-only launches, vrt_set_exact_pass), else the heavy-first tile order.
 // allow_defer: false for frames that run alone (synchronous calls): there the exact pass's
 // latency after the certified pass is the frame's (C3 0.198 vs 0.076 ms per synchronous frame),
-// while frames in flight hide it
+// while frames in flight hide it. The deferral also needs a launch of at least two rounds of the
+// certified pass's resident waves: on smaller bands the exact pass's latency (its longest waves
+// are the glass pixels' bounce stacks) follows a short certified pass on the same stream and
+// bounds the band's frame rate (C3's band at k = 4 / 8 GPUs: 0.025 / 0.0235 ms per frame deferred,
+// 0.0155 / 0.0114 in-lane; the whole frame: 0.0445 deferred, 0.060 in-lane; C4's band at k = 8,
+// 16 200 waves: 0.0281 deferred, 0.0297 in-lane; profiles/r03_s18, r03_s19).
 void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
-  const bool defer = allow_defer && ctx->exact_pass && a.cert == 2;
+  const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 &&
+                     (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
   // every tile is heavy, keep dispatch order: C1 +3.4 %)
@@ -1091,8 +1102,8 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
 
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
-  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0 or 1");
-  ctx->exact_pass = on != 0;
+  if (on < 0 || on > 2) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0, 1 or 2");
+  ctx->exact_pass = on;
   ctx->err.clear();
   return VRT_OK;
 }

@@ -76,7 +76,8 @@ constexpr int kCntReplicas = 256;           // counter replicas (per-wave atomic
 constexpr uint32_t kOrdClasses = 8;         // tile-order lists: tile % 8 (the XCD of its slot)
 constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 256-byte line each)
 constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
-constexpr uint32_t kDeferHdr = 2 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 counter sets
+constexpr uint32_t kDeferHdr = 4 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 kinds x 2 sets
+constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave keeps its own exact-pass batch
 #if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_DEFER_GRID_DIV is an A/B knob of make variant builds"
 #endif

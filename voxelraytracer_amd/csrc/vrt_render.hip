@@ -2045,21 +2045,27 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
     const unsigned long long m = __ballot(deferred);
     if (m != 0ull) {
-      const uint32_t seg = blockIdx.x % kOrdClasses;
+      const uint32_t seg = blockIdx.x % kOrdClasses, first = uint32_t(__builtin_ctzll(m));
+      const uint32_t cnt = uint32_t(__builtin_popcountll(m));
+      // a wave with many deferred pixels (a glass region) keeps them as a chunk of its own, each
+      // at its lane (a coherent 8x8 tile of exact work); the others append compactly
+      const bool dense = cnt >= kDeferDense;
       uint32_t base = 0;
-      if (lane_id() == uint32_t(__builtin_ctzll(m)))
-        base = atomicAdd(a.defer + (a.defer_e * kOrdClasses + seg) * kOrdCtrStride,
-                         uint32_t(__builtin_popcountll(m)));
-      base = uint32_t(__builtin_amdgcn_readlane(int(base), int(__builtin_ctzll(m))));
-      if (deferred) {
+      if (lane_id() == first)
+        base = atomicAdd(a.defer + ((uint32_t(dense) * 2u + a.defer_e) * kOrdClasses + seg) * kOrdCtrStride,
+                         dense ? 1u : cnt);
+      base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
+      uint32_t* list = a.defer + kDeferHdr + seg * a.defer_seg;
+      const uint32_t l3 = lane_id();  // the pixel re-derived (not kept live across the walks)
+      const uint32_t id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
+      if (dense) {  // chunks fill the segment's region from its end
+        list[a.defer_seg - 64u * (base + 1u) + l3] = deferred ? id : ~0u;
+      } else if (deferred) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-        const uint32_t l3 = lane_id();  // the pixel re-derived (not kept live across the walks)
-        a.defer[kDeferHdr + seg * a.defer_seg + base + rank] =
-            (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
+        list[base + rank] = id;
       }
     }
   }
-
   if constexpr (ORD) {
     const bool heavy_wave = __ballot(heavy) != 0ull;
     if (lane_id() == 0) order_record(a, tile, heavy_wave);
@@ -2113,11 +2119,15 @@ __device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r)
   return pos;
 }
 
-// The deferred exact pass: the pixels a certified pass (render_kernel<..., DEFER>) appended to
-// its list, rendered with the exact path 64 to a wave — the certified pass's waves end with their
-// certified pixels, and the exact walks that would each have held a sparse wave of them run
-// densely here (the north_star's __ballot compaction of live rays). Batch b is list entries
-// [64 b, 64 b + 64) over the segments in order; batches b, b + gridDim.x, ... per workgroup.
+// The deferred exact pass: the pixels a certified pass (render_kernel<..., DEFER>) left to it,
+// rendered with the exact path 64 to a wave — the certified pass's waves end with their certified
+// pixels, and the exact walks that would each have held a sparse wave of them run densely here
+// (the north_star's __ballot compaction of live rays). Waves that deferred >= kDeferDense pixels
+// (glass regions) left them as a chunk in lane order: one batch each, the same coherent 8x8 tile
+// of exact work as in place (textured C3 0.0668 -> 0.0633 ms per frame against compact appends only,
+// C2-C4 within +-1.5 %, profiles/r03_s21). The rest
+// are batches of 64 list entries over the segments in order. Batches b, b + gridDim.x, ... per
+// workgroup.
 // Every deferred pixel is rendered exactly once, with the same exact path and epilogue as the
 // in-lane fallback, so images are identical. Workgroup 0 zeroes the other counter set for the
 // next launch on the stream (none of this launch's kernels reads it).
@@ -2125,30 +2135,39 @@ template <bool TEX, int CERT>
 __global__ void __launch_bounds__(64, VRT_EXACT_WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t lane = lane_id();
-  const uint32_t* ctr = a.defer + a.defer_e * kOrdClasses * kOrdCtrStride;
-  if (blockIdx.x == 0 && lane < kOrdClasses) a.defer[((a.defer_e ^ 1u) * kOrdClasses + lane) * kOrdCtrStride] = 0u;
-  uint32_t n[kOrdClasses], total = 0;
+  const uint32_t* ctr = a.defer;
+  if (blockIdx.x == 0 && lane < 2u * kOrdClasses)  // both kinds of the other set, for the next launch
+    a.defer[(((lane / kOrdClasses) * 2u + (a.defer_e ^ 1u)) * kOrdClasses + lane % kOrdClasses) * kOrdCtrStride] = 0u;
+  uint32_t ns[kOrdClasses], nd[kOrdClasses], total_s = 0, total_d = 0;
 #pragma unroll
   for (uint32_t q = 0; q < kOrdClasses; ++q) {
-    n[q] = ctr[q * kOrdCtrStride];
-    total += n[q];
+    ns[q] = ctr[(a.defer_e * kOrdClasses + q) * kOrdCtrStride];
+    nd[q] = ctr[((2u + a.defer_e) * kOrdClasses + q) * kOrdCtrStride];
+    total_s += ns[q];
+    total_d += nd[q];
   }
-  if (blockIdx.x * 64u >= total) return;
+  const uint32_t batches = total_d + (total_s + 63u) / 64u;
+  if (blockIdx.x >= batches) return;
   Ctx c;
   init_ctx(c, a, vox);
   __shared__ float4 ax_tab[64 * 3];
   c.ax = &ax_tab[lane * kAxLane];
-  for (uint32_t base = blockIdx.x * 64u; base < total; base += gridDim.x * 64u) {
-    uint32_t idx = base + lane;
-    if (idx >= total) continue;
+  for (uint32_t b = blockIdx.x; b < batches; b += gridDim.x) {
+    // batch b: dense chunk b (in segment order), else sparse entries [64 (b - total_d), + 64)
+    const bool dense = b < total_d;
+    uint32_t idx = dense ? b : (b - total_d) * 64u + lane;
+    if (!dense && idx >= total_s) continue;
     uint32_t seg = 0;
 #pragma unroll
     for (uint32_t q = 0; q + 1u < kOrdClasses; ++q) {
-      const bool past = seg == q && idx >= n[q];
-      idx -= past ? n[q] : 0u;
+      const uint32_t nq = dense ? nd[q] : ns[q];
+      const bool past = seg == q && idx >= nq;
+      idx -= past ? nq : 0u;
       seg += past ? 1u : 0u;
     }
-    const uint32_t e = a.defer[kDeferHdr + seg * a.defer_seg + idx];
+    const uint32_t* list = a.defer + kDeferHdr + seg * a.defer_seg;
+    const uint32_t e = dense ? list[a.defer_seg - 64u * (idx + 1u) + lane] : list[idx];
+    if (e == ~0u) continue;  // a lane of a dense chunk whose pixel the certified pass settled
     const int px = int(e & 0xFFFFu), li = int(e >> 16);
     const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
     Counters k;

@@ -542,8 +542,11 @@ def main():
                                 "rank's frame / GPU time per frame = per-launch rate x launches in "
                                 "flight; not a bandwidth"),
                 "achieved_per_launch": round(per_launch, 2),
-                "achieved_per_launch_is": ("bytes of one render_kernel launch / its mean duration "
-                                           "(launch_ms, as rocprofv3 reports it)"),
+                "achieved_per_launch_is": ("bytes of one launch / its mean duration (launch_ms); a "
+                                           "launch of a large band is the certified pass "
+                                           "(render_kernel) and its deferred exact pass "
+                                           "(exact_pass_kernel) on one stream, which rocprofv3 lists "
+                                           "as two kernels whose mean durations add up to it"),
                 "launches_in_flight": round(in_flight, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -557,9 +560,10 @@ def main():
                 "bytes_per_launch": int(bytes_per_launch),
                 "bytes_per_frame": own_bytes,
                 "launch_ms": round(launch_ms, 4),
-                "launch_ms_is": ("mean render_kernel duration from the kernels' device start / end "
-                                 "timestamps (hipExtLaunchKernelGGL events, vrt_set_launch_timing) "
-                                 "over a pass of the same frames after the timed region"),
+                "launch_ms_is": ("mean launch duration from the device timestamps of its first "
+                                 "kernel's start and last kernel's end (hipExtLaunchKernelGGL "
+                                 "events, vrt_set_launch_timing) over a pass of the same frames "
+                                 "after the timed region"),
                 "launches_per_frame": parts,
                 "lanes": lanes,
                 "kernel_ms": round(frame_gpu_ms, 4),

@@ -49,9 +49,12 @@ if passes:
         f.write(summ)
     s = json.loads(summ)
     if "fetch_bytes" in s and "write_bytes" in s:
-        out = {"config": a.config, "output": a.output, "kernel": "vrt::render_kernel<false, false, 2, true> (stats-free, colour-only, certified walks, heavy-first tile order)",
+        out = {"config": a.config, "output": a.output,
+               "kernel": "one frame's launch: vrt::render_kernel<false, false, 2, false, true> (certified "
+                         "pass) + vrt::exact_pass_kernel<false, 2> (deferred exact pass), summed",
                "source": f"profiles/{os.path.basename(dst)}/pmc (rocprofv3 --pmc FETCH_SIZE and --pmc "
-                         "WRITE_SIZE in separate passes over bench.py --steps 5 --warmup 1 --parts 1: one launch = one frame)",
+                         "WRITE_SIZE in separate passes over bench.py --steps 5 --warmup 1 "
+                         "--device-warmup-ms 0: one launch = one frame)",
                "fetch_size_bytes_raw": s["fetch_bytes"], "write_size_bytes": s["write_bytes"],
                "correction": "gfx950: FETCH_SIZE reports half the bytes of 128-B requests "
                              "(MI355X_MICROARCH.md HBM section) -> doubled; WRITE_SIZE as is",

@@ -49,8 +49,24 @@ __device__ __forceinline__ void set_comp(f3& a, int i, float f) {
   else if (i == 1) a.y = f;
   else a.z = f;
 }
+// RN(1 / RN(sqrt(s))) for s within 1024 ulps of 1 (bits b), in closed form: for s = 1 + k 2^-23
+// (k >= 0) the correctly rounded square root is 1 + floor(k/2) 2^-23 and its reciprocal
+// 1 - floor(k/2) 2^-23; for s = 1 - k 2^-24 they are 1 - ceil(k/2) 2^-24 and 1 + ceil(m/2) 2^-23,
+// m = ceil(k/2) (the square root and the reciprocal sit within m^2 2^-48 of those grid points or
+// midpoints, on the side that decides the rounding). Exact for |k| < 2898 (exhaustive against
+// IEEE sqrt and division: tests/test_normalize_fast.py); a normalised vector's squared length is
+// within a few ulps of 1, so RandomizeDirection's, the skybox's and GetRefractionRay's
+// normalize of an already normalised direction takes ~6 VALU instead of ~26.
+__device__ __forceinline__ float near_one_rsqrt(uint32_t b) {
+  const uint32_t one = 0x3F800000u;
+  const uint32_t r = b >= one ? (b - one < 2u ? one : one - ((b - one) & ~1u))
+                              : one + (((((one - b) + 1u) >> 1) + 1u) >> 1);
+  return __uint_as_float(r);
+}
 __device__ __forceinline__ f3 normalize3(f3 v) {
-  const float inv = 1.0f / __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+  const float s = v.x * v.x + v.y * v.y + v.z * v.z;
+  const uint32_t b = __float_as_uint(s);
+  const float inv = b - (0x3F800000u - 1024u) <= 2048u ? near_one_rsqrt(b) : 1.0f / __builtin_sqrtf(s);
   return v * inv;
 }
 __device__ __forceinline__ float gsign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
@@ -1008,7 +1024,9 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   //   gL(u) = 2^-23 sum len + 1e-4 + e0 (the length test)
   constexpr float k24 = 2.0f * 0x1p-24f;
   const float q2 = 0.5f * k24 * l1;
-  const float lin = 6.0f + l1 * (len0b + 1.0f), con = 18.0f / l1 + 3.0f * (len0b + 1.0f);
+  // 18 / |d|_1 only bounds a sum: the hardware reciprocal (<= 1 ulp) scaled up by 2^-19 stays above it
+  const float lin = 6.0f + l1 * (len0b + 1.0f),
+              con = (18.0f * 1.0000020f) * __builtin_amdgcn_rcpf(l1) + 3.0f * (len0b + 1.0f);
   const float nterm = 3.0f * c.fn + 11.0f;
   const f3 q1 = mk(k24 * (lin + 2.0f + ar.x * l1), k24 * (lin + 2.0f + ar.y * l1), k24 * (lin + 2.0f + ar.z * l1));
   const float c0 = k24 * (con + 2.0f * len0b) + 4e-5f + e0;

@@ -1032,6 +1032,11 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   const float c0 = k24 * (con + 2.0f * len0b) + 4e-5f + e0;
   const f3 q0 = mk(c0 + k24 * ar.x * nterm + ed.x, c0 + k24 * ar.y * nterm + ed.y, c0 + k24 * ar.z * nterm + ed.z);
   const float g2 = 2.0f * q2, g1 = 2.0f * k24 * lin, g0 = 2.0f * k24 * con + 1e-4f + e0;
+  // sign-folded start and direction: Ps_b + u |d_b| = s_b (P_b + u d_b) exactly (negation is exact),
+  // so a landing cell is floor(s x) ^ m, m = 0 or ~0 (ceil(x) - 1 = ~floor(-x)), without branches
+  const f3 Ps = mk(ux ? P.x : -P.x, uy ? P.y : -P.y, uz ? P.z : -P.z);
+  const f3 Da = mk(__builtin_fabsf(D.x), __builtin_fabsf(D.y), __builtin_fabsf(D.z));
+  const int mx = ux - 1, my = uy - 1, mz = uz - 1;
   f3 sig = mk((float(cx + ux) - P.x) * rcp.x, (float(cy + uy) - P.y) * rcp.y,
               (float(cz + uz) - P.z) * rcp.z);
   // start: the unguarded box from the diagonal neighbour (G(v + s) + 1 in the guarded formula)
@@ -1053,20 +1058,24 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     // (only for rays in air: empty cells are events in a glass medium)
     const uint32_t G = tex >> kDistShift;
     if (G >= 2u && (SHADOW || medium == 0u)) {
-      const float fg = float(G) - kCertMargin;
-      const float lx = (float(cx + 1 - ux) + float(sx) * fg - P.x) * rcp.x;
-      const float ly = (float(cy + 1 - uy) + float(sy) * fg - P.y) * rcp.y;
-      const float lz = (float(cz + 1 - uz) + float(sz) * fg - P.z) * rcp.z;
+      // the box's far face on axis b is G - 1 - margin cells beyond the plane of sig_b: its
+      // parameter sig_b + (G - 1 - margin) |1/d_b| up to a few ulps, far inside the margin's
+      // margin |1/d_b| (|sig_b| <= ~400 |1/d_b| in a 256^3 volume: 1e-4 |1/d_b| at 3 ulps)
+      const float fg1 = float(G) - (1.0f + kCertMargin);
+      const float lx = __builtin_fmaf(fg1, ar.x, sig.x);
+      const float ly = __builtin_fmaf(fg1, ar.y, sig.y);
+      const float lz = __builtin_fmaf(fg1, ar.z, sig.z);
       // per axis: the exact walk crosses the box face of axis b within gam_b of l_b, so its steps
       // up to min_b (l_b - gam_b) sample box cells (a common max(gam) would let one nearly
       // parallel axis, |1/d_b| huge, stop every jump: ~90 us cell-by-cell walks at C3)
       const float uj = __builtin_fminf(__builtin_fminf(lx - gam.x, ly - gam.y),
                                        __builtin_fminf(lz - gam.z, U + 2.0f));
       if (uj > s1) {
-        const float x = P.x + uj * D.x, y = P.y + uj * D.y, z = P.z + uj * D.z;
-        cx = sx > 0 ? int(__builtin_floorf(x)) : int(__builtin_ceilf(x)) - 1;
-        cy = sy > 0 ? int(__builtin_floorf(y)) : int(__builtin_ceilf(y)) - 1;
-        cz = sz > 0 ? int(__builtin_floorf(z)) : int(__builtin_ceilf(z)) - 1;
+        // the cell the exact walk is in there: floor(x) moving up, ceil(x) - 1 moving down
+        const float x = Ps.x + uj * Da.x, y = Ps.y + uj * Da.y, z = Ps.z + uj * Da.z;
+        cx = int(__builtin_floorf(x)) ^ mx;
+        cy = int(__builtin_floorf(y)) ^ my;
+        cz = int(__builtin_floorf(z)) ^ mz;
         sig = mk((float(cx + ux) - P.x) * rcp.x, (float(cy + uy) - P.y) * rcp.y,
                  (float(cz + uz) - P.z) * rcp.z);
         tex = path_texel(c, cx, cy, cz, obase);
@@ -1075,7 +1084,8 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     }
     // one crossing, s1 on axis a; prev = the crossing before it (the exact walk's len there)
     const f3 back = mk(sig.x - ar.x, sig.y - ar.y, sig.z - ar.z);
-    const float prev = gmax(gmax(back.x, 0.0f), gmax(back.y, back.z));
+    const float mback = gmax(back.x, gmax(back.y, back.z));
+    const float prev = gmax(mback, 0.0f);
     const float gL = __builtin_fmaf(__builtin_fmaf(g2, uu, g1), uu, g0);
     if (prev > U + gL) {
       r.res = CERT_MISS;
@@ -1091,16 +1101,24 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     // the ray has moved half an ulp of the coordinate off it (r02 s18: a shadow ray from
     // (33.000008, 127, 37.02) sampled the panel voxel (32, 127, 37) at its first x crossing, and
     // back.y rounded to just below 0 hid that alternative from the certified walk)
-    const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
-               ahz = a != 2 && sig.z - s1 < ga + gam.z;
-    const bool bhx = a != 0 && back.x > -gam.x && s1 - back.x < ga + gam.x;
-    const bool bhy = a != 1 && back.y > -gam.y && s1 - back.y < ga + gam.y;
-    const bool bhz = a != 2 && back.z > -gam.z && s1 - back.z < ga + gam.z;
-    const bool near = ahx | ahy | ahz | bhx | bhy | bhz;
+    // nf bits 0-2: ahead x, y, z; 3-5: behind x, y, z. They are rare: a superset test first (the
+    // second smallest sig bounds every sig_b, b != a, from below, the latest back every back_b from
+    // above, and ga + max gam every ga + gam_b; rounding is monotone), the flags only if it holds.
+    const float tg = ga + gmax(gam.x, gmax(gam.y, gam.z));
+    uint32_t nf = 0u;
+    if (__builtin_amdgcn_fmed3f(sig.x, sig.y, sig.z) - s1 < tg || s1 - mback < tg) {
+      const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
+                 ahz = a != 2 && sig.z - s1 < ga + gam.z;
+      const bool bhx = a != 0 && back.x > -gam.x && s1 - back.x < ga + gam.x;
+      const bool bhy = a != 1 && back.y > -gam.y && s1 - back.y < ga + gam.y;
+      const bool bhz = a != 2 && back.z > -gam.z && s1 - back.z < ga + gam.z;
+      nf = uint32_t(ahx) | uint32_t(ahy) << 1 | uint32_t(ahz) << 2 | uint32_t(bhx) << 3 |
+           uint32_t(bhy) << 4 | uint32_t(bhz) << 5;
+    }
     const uint32_t nb = ntex & kVoxMask;
     if (cert_event<SHADOW>(nb, medium)) {
       if (!(prev + gL < U)) return r;  // the length test might stop the walk first
-      if (!near) {
+      if (nf == 0u) {
         r.res = CERT_HIT;
         r.byte = nb;
         r.axis = a;
@@ -1111,12 +1129,12 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
         r.eu = ga;
         return r;
       }
-      if (SHADOW && int(ahx) + int(ahy) + int(ahz) + int(bhx) + int(bhy) + int(bhz) == 1) {
+      if (SHADOW && __builtin_popcount(nf) == 1) {
         // blocked whichever way the exact walk goes: near-behind b still samples nc (or nc - e_b
         // first); near-ahead b samples nc, or cell + e_b and then nc + e_b
         bool ok = true;
-        if (ahx | ahy | ahz) {
-          const int bx = ahx ? sx : 0, by = ahy ? sy : 0, bz = ahz ? sz : 0;
+        if (nf & 7u) {
+          const int bx = (nf & 1u) ? sx : 0, by = (nf & 2u) ? sy : 0, bz = (nf & 4u) ? sz : 0;
           ok = cert_event<true>(alt_byte(c, cx + bx, cy + by, cz + bz, obase), 0u) ||
                cert_event<true>(alt_byte(c, nx + bx, ny + by, nz + bz, obase), 0u);
         }
@@ -1127,9 +1145,11 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
       }
       return r;  // hit or unsure
     }
-    if (near) {  // cells the exact walk may sample instead of the path's: all must be non-events
-      const int nah = int(ahx) + int(ahy) + int(ahz), nbh = int(bhx) + int(bhy) + int(bhz);
-      if (nah + nbh >= 2) {  // near a corner: the 2x2x2 block ahead and the cells behind nc
+    if (nf) {  // cells the exact walk may sample instead of the path's: all must be non-events
+      const bool ahx = nf & 1u, ahy = nf & 2u, ahz = nf & 4u, bhx = nf & 8u, bhy = nf & 16u,
+                 bhz = nf & 32u;
+      const int nah = int(ahx) + int(ahy) + int(ahz);
+      if (__builtin_popcount(nf) >= 2) {  // near a corner: the 2x2x2 block ahead and the cells behind nc
         for (int q = 1; q < 8; ++q)
           if (cert_event<SHADOW>(alt_byte(c, cx + ((q & 1) ? sx : 0), cy + ((q & 2) ? sy : 0),
                                           cz + ((q & 4) ? sz : 0), obase), medium))

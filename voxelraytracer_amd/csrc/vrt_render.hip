@@ -1005,7 +1005,7 @@ __device__ __forceinline__ bool cert_event(uint32_t b, uint32_t medium) {
 template <bool SHADOW>
 __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 rcp, const float U,
                                 int cx, int cy, int cz, const float e0, const f3 ed,
-                                const float len0b, const uint32_t medium) {
+                                const float len0b, const uint32_t medium, const uint32_t tex0 = ~0u) {
   CertResult r;
   r.res = CERT_UNSURE;
   r.byte = 0u;
@@ -1040,7 +1040,8 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   f3 sig = mk((float(cx + ux) - P.x) * rcp.x, (float(cy + uy) - P.y) * rcp.y,
               (float(cz + uz) - P.z) * rcp.z);
   // start: the unguarded box from the diagonal neighbour (G(v + s) + 1 in the guarded formula)
-  uint32_t tex = path_texel(c, cx + sx, cy + sy, cz + sz, obase) + (1u << kDistShift);
+  // (tex0: that texel, loaded by the caller beside an earlier load; ~0u: load it here)
+  uint32_t tex = (tex0 != ~0u ? tex0 : path_texel(c, cx + sx, cy + sy, cz + sz, obase)) + (1u << kDistShift);
 #ifdef VRT_CERT_DIAG
   r.iters = 0;
 #endif
@@ -1250,6 +1251,12 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
     // shadow origin: the exact hit point; start cell: the air cell in front of the hit face
     int ax, ay, az;
     cell_before(h, ray.dir, ax, ay, az);
+    // the shadow walk's start texel (the diagonal neighbour in the sun's octant volume) is loaded
+    // first, so its latency overlaps the start checks and the air-cell load (same octant volume:
+    // every octant volume holds the same voxel bytes)
+    const uint32_t sob = ((S.x < 0.0f ? 1u : 0u) | (S.y < 0.0f ? 2u : 0u) | (S.z < 0.0f ? 4u : 0u)) * c.ostride;
+    const uint32_t t0 = path_texel(c, ax + (S.x > 0.0f ? 1 : -1), ay + (S.y > 0.0f ? 1 : -1),
+                                   az + (S.z > 0.0f ? 1 : -1), sob);
     f3 ed;
     if (!cert_start(hh.point, ray.dir, S, c.sun_rcp, h.axis, h.eu, ax, ay, az, ed)) {
       CERT_DIAG(6);
@@ -1257,9 +1264,9 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
     }
     const uint32_t n = uint32_t(c.n);
     if (uint32_t(ax) >= n || uint32_t(ay) >= n || uint32_t(az) >= n) { CERT_DIAG(7); return false; }
-    if (cert_event<true>(cell_texel(c, ax, ay, az, 0u) & kVoxMask, 0u)) { CERT_DIAG(7); return false; }
+    if (cert_event<true>(cell_texel(c, ax, ay, az, sob) & kVoxMask, 0u)) { CERT_DIAG(7); return false; }
     const CertResult s = cert_walk<true>(c, hh.point, S, c.sun_rcp, c.max_len - hh.len, ax, ay, az,
-                                         h.eu, ed, hh.len, 0u);
+                                         h.eu, ed, hh.len, 0u, t0);
     if (s.res == CERT_UNSURE) { CERT_DIAG(8); return false; }
     CERT_DIAG(9);
     brightness = s.res == CERT_HIT ? kAmbient : lit;

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 9
+#define VRT_ABI_VERSION 10
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -380,6 +380,14 @@ void vrt_params_default(vrt_params* out);
  * holds ceil((height - j) / k) rows, band row r = frame row j + r*k. Returns the largest band's
  * rows. Used by the whole-frame entry points; exported for tests. */
 int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out);
+
+/* ABI v10: the k strided copies that assemble a frame of `height` rows x `width` pixels of
+ * `elem_bytes` each from the k band buffers (band j's rows packed, band row r = frame row j + r*k):
+ * the pinned host staging of vrt_render / vrt_render_frame over k devices and the device-frame
+ * gather use exactly these. out[j*5 + 0..4] = {destination byte offset, destination pitch, source
+ * pitch, row bytes, rows} of one 2-D copy (hipMemcpy2D). Host arithmetic, no GPU; returns k.
+ * Exported for tests (unequal bands when height % k != 0). */
+int vrt_band_copy_plan(int32_t width, int32_t height, int32_t k, int32_t elem_bytes, int64_t* out);
 
 #ifdef __cplusplus
 }

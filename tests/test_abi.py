@@ -44,7 +44,7 @@ def test_struct_layouts():
 
 
 def test_abi_version(built):
-    assert vrt.lib().vrt_abi_version() == 9
+    assert vrt.lib().vrt_abi_version() == 10
 
 
 @pytest.mark.parametrize("scene", [0, 1, 2])
@@ -129,6 +129,41 @@ def test_band_plan_composes_the_oracle_frame(built):
         hb = len(range(j, h, k))
         frame[j::k] = bands[j, :hb]   # hipMemcpy2D: dst pitch k*W, src pitch W
     assert np.array_equal(frame.view(np.uint32), full.view(np.uint32))
+
+
+def _memcpy2d(dst, dst_off, dst_pitch, src, src_pitch, width, rows):
+    for r in range(rows):   # hipMemcpy2D semantics, byte for byte
+        d = dst_off + r * dst_pitch
+        assert 0 <= d and d + width <= dst.size, "copy out of the frame"
+        assert r * src_pitch + width <= src.size, "copy out of the band"
+        dst[d:d + width] = src[r * src_pitch:r * src_pitch + width]
+
+
+@pytest.mark.parametrize("width,height,k,elem", [(40, 27, 4, 4), (1920, 1081, 8, 4), (33, 7, 3, 16),
+                                                 (5, 5, 8, 16), (64, 1080, 7, 16), (3, 1, 1, 4)])
+def test_band_copy_plan_assembles_unequal_bands(built, width, height, k, elem):
+    """The copies the library issues to assemble a multi-device frame (pinned host staging of
+    vrt_render / vrt_render_frame, and the device-frame gather) place every band's packed rows at
+    their frame rows, each frame byte written once, when height % k != 0 leaves bands of unequal
+    height (and some empty when k > height): applied here with hipMemcpy2D's semantics."""
+    plan = vrt.band_copy_plan(width, height, k, elem)
+    row = width * elem
+    frame = np.zeros(height * row, np.uint8)
+    written = np.zeros(height * row, np.int32)
+    for j, (dst_off, dst_pitch, src_pitch, wbytes, rows) in enumerate(plan):
+        assert rows == len(range(j, height, k)) and wbytes == row and src_pitch == row
+        # band j: packed rows, each filled with a pattern naming its frame row and band
+        band = np.zeros(max(rows, 1) * row, np.uint8)
+        for r in range(rows):
+            band[r * row:(r + 1) * row] = (j + r * k) * 7 + j + 1 & 0xFF
+        _memcpy2d(frame, dst_off, dst_pitch, band, src_pitch, wbytes, rows)
+        ones = np.zeros_like(written)
+        _memcpy2d(ones, dst_off, dst_pitch, np.ones(max(rows, 1) * row, np.int32), src_pitch, wbytes, rows)
+        written += ones
+    assert np.all(written == 1)
+    for fr in range(height):
+        j = fr % k
+        assert np.all(frame[fr * row:(fr + 1) * row] == (fr * 7 + j + 1) & 0xFF)
 
 
 def test_headless_app_builds_and_parses(built):

@@ -170,6 +170,16 @@ def band_plan(height: int, k: int, parts: int = 2):
     return {(j, p): tuple(int(v) for v in o[j, p]) for j in range(k) for p in range(parts)}, cap
 
 
+def band_copy_plan(width: int, height: int, k: int, elem_bytes: int):
+    """The library's frame-assembly copies (vrt_band_copy_plan): per band j, (dst_offset,
+    dst_pitch, src_pitch, row_bytes, rows) of the 2-D copy of band j's packed rows into the frame."""
+    out = np.zeros(k * 5, np.int64)
+    r = lib().vrt_band_copy_plan(width, height, k, elem_bytes, out.ctypes.data)
+    if r < 0:
+        raise VrtError(r, "vrt_band_copy_plan")
+    return [tuple(int(v) for v in row) for row in out.reshape(k, 5)]
+
+
 class Renderer:
     """One vrt_ctx (replaces the GL context + FrameBuffer of the reference). `device` is a HIP
     device ordinal, or a sequence of ordinals: whole frames are then split into row bands across

@@ -100,6 +100,7 @@ SIGNATURES = {
     "vrt_device_count": (C.c_int, [C.c_void_p]),
     "vrt_device_ordinal": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_band_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "vrt_band_copy_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     "vrt_destroy": (None, [C.c_void_p]),
     "vrt_last_error": (C.c_char_p, [C.c_void_p]),
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),

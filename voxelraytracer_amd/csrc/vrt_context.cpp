@@ -203,6 +203,16 @@ struct DeviceGuard {
 int32_t band_rows(int32_t height, int32_t k, int32_t j) { return j < height ? (height - j + k - 1) / k : 0; }
 int32_t band_cap(int32_t height, int32_t k) { return (height + k - 1) / k; }
 
+// The strided copy that places band j (its rows packed at `row` bytes each) into its frame rows
+// j, j + k, ... of a frame of h rows: one hipMemcpy2D (staging to the host, gather on device).
+struct BandCopy {
+  size_t dst_off, dst_pitch, src_pitch, width, rows;
+};
+BandCopy band_copy(int32_t w, int32_t h, int32_t k, int32_t j, size_t elem) {
+  const size_t row = size_t(w) * elem;
+  return BandCopy{size_t(j) * row, size_t(k) * row, row, row, size_t(band_rows(h, k, j))};
+}
+
 // Part p of band j: frame rows (j + p k) + i (k P), band rows p + i P.
 struct PartRows {
   int32_t row0, rows, row_step, band_row0;
@@ -774,14 +784,13 @@ int stage_bands(vrt_ctx* ctx, int g, int32_t w, int32_t h, const void* const* ba
   const int32_t k = int32_t(ctx->sh.size());
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
-    const int32_t hb = band_rows(h, k, j);
-    if (hb == 0) continue;
+    const BandCopy bc = band_copy(w, h, k, j, elem);
+    if (bc.rows == 0) continue;
     VRT_HIP(ctx, hipSetDevice(s.device));
     int st = wait_lane(ctx, s, g, s.ls[g][0]);
     if (st != VRT_OK) return st;
-    const size_t row = size_t(w) * elem;
-    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(ctx->h_stage) + stage_off + size_t(j) * row, size_t(k) * row,
-                                  bands[j], row, row, size_t(hb), hipMemcpyDeviceToHost, s.ls[g][0]));
+    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(ctx->h_stage) + stage_off + bc.dst_off, bc.dst_pitch, bands[j],
+                                  bc.src_pitch, bc.width, bc.rows, hipMemcpyDeviceToHost, s.ls[g][0]));
   }
   return VRT_OK;
 }
@@ -843,10 +852,10 @@ int gather_frame(vrt_ctx* ctx, int32_t w, int32_t h, int slot, int g, hipEvent_t
   if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.gs, reuse, 0));
   uint32_t* out = ctx->d_frames[slot];
   for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
-    const int32_t hb = band_rows(h, k, j);
-    if (hb > 0)
-      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + size_t(j) * row, size_t(k) * row, src[j], row,
-                                    row, size_t(hb), hipMemcpyDeviceToDevice, root.gs));
+    const BandCopy bc = band_copy(w, h, k, j, 4);
+    if (bc.rows > 0)
+      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + bc.dst_off, bc.dst_pitch, src[j], bc.src_pitch,
+                                    bc.width, bc.rows, hipMemcpyDeviceToDevice, root.gs));
   }
   if (!ctx->distinct)
     for (int32_t j = 0; j < k; ++j) {  // same physical device: the bands were read here
@@ -967,6 +976,20 @@ int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out) {
       o[3] = pr.band_row0;
     }
   return band_cap(height, k);
+}
+
+int vrt_band_copy_plan(int32_t width, int32_t height, int32_t k, int32_t elem_bytes, int64_t* out) {
+  if (width < 1 || height < 1 || k < 1 || elem_bytes < 1 || !out) return VRT_ERR_INVALID;
+  for (int32_t j = 0; j < k; ++j) {
+    const BandCopy bc = band_copy(width, height, k, j, size_t(elem_bytes));
+    int64_t* o = out + size_t(j) * 5;
+    o[0] = int64_t(bc.dst_off);
+    o[1] = int64_t(bc.dst_pitch);
+    o[2] = int64_t(bc.src_pitch);
+    o[3] = int64_t(bc.width);
+    o[4] = int64_t(bc.rows);
+  }
+  return k;
 }
 
 int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {

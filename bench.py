@@ -110,6 +110,12 @@ def parse():
                     help="N > 1: gather every frame's bands to rank 0 over RCCL inside the timed "
                          "region (display delivery); default: bands stay on their ranks, one "
                          "gather after the timed region")
+    ap.add_argument("--pre-idle-ms", type=float, default=0.0,
+                    help="diagnostic: idle the synchronised device this long before the timed "
+                         "region (clock-ramp experiments)")
+    ap.add_argument("--frame-events", action="store_true",
+                    help="diagnostic: an event after every timed frame on its lane; prints each "
+                         "frame's completion time from the first lane start (JSON frame_events_ms)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the config's frame is split N ways (default); weak (opt-in): N "
                          "ranks render an N-fold taller frame (each a config-sized band)")
@@ -328,20 +334,41 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # Timed region: K frames; the GPU time per frame on this rank comes from one event pair on
-    # the main stream around them (the part streams are idle at ev0 and joined before ev1).
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # Timed region: K frames. The device is idle here (synchronised above), so the lane streams
+    # start without waiting on the main stream, and the closing device-wide synchronize waits for
+    # every lane (no cross-queue joins inside the timed region: each costs a few us of queue
+    # latency at both ends of a 20-frame run; scripts/diag/drv_shape.sh). GPU time per frame:
+    # from the earliest lane start event to the latest lane end event.
+    # (--gather-frames keeps the joins: the last frame's gather and assembly are timed frames' work)
+    if args.pre_idle_ms > 0:
+        time.sleep(args.pre_idle_ms * 1e-3)
+    if not tiler.gather:
+        tiler.mark_idle()
+    lane_st = (tiler.lane_streams() if not tiler.gather else []) or [stream]
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    for e, st in zip(ev0, lane_st):
+        e.record(st)
+    fev = []
+    for i_ in range(args.steps):
         tiler.frame()
-    tiler.finish()
-    ev1.record(stream)
+        if args.frame_events and not tiler.gather:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(lane_st[(i_ % tiler.lanes) * len(tiler.specs) % len(lane_st)])
+            fev.append(e)
+    if tiler.gather:
+        tiler.finish()
+    for e, st in zip(ev1, lane_st):
+        e.record(st)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    frame_gpu_ms = ev0.elapsed_time(ev1) / args.steps
+    if not tiler.gather:
+        tiler.finish()   # host bookkeeping: every lane is already complete
+    frame_gpu_ms = max(a.elapsed_time(b) for a in ev0 for b in ev1) / args.steps
+    frame_events_ms = [round(min(a.elapsed_time(e) for a in ev0), 4) for e in fev] or None
     # Launch-timing pass (after the timed region, the same FrameTiler path): the mean duration of
     # one render_kernel launch — what rocprofv3 reports per kernel — from the kernels' own device
     # start / end timestamps (vrt_set_launch_timing: hipExtLaunchKernelGGL events; launches of
@@ -567,15 +594,17 @@ def main():
                 "launches_per_frame": parts,
                 "lanes": lanes,
                 "kernel_ms": round(frame_gpu_ms, 4),
-                "kernel_ms_is": (f"GPU time per frame of this rank in the steady state ({lanes} "
-                                 f"frame(s) in flight, {parts} launch(es) per frame): HIP events "
-                                 "around the K timed frames on the main stream / K"),
+                "kernel_ms_is": (f"GPU time per frame of this rank ({lanes} frame(s) in flight, "
+                                 f"{parts} launch(es) per frame): from the earliest start event to "
+                                 "the latest end event of the lane streams around the K timed "
+                                 "frames / K (with fill and drain of the pipeline)"),
                 "kernel_ms_max_over_ranks": round(frame_ms_max, 4),
                 "valu_issue": valu,
                 "lib_sha256": lib_hash[:16],
                 "profile": prof_note,
             },
             "device_warmup": device_warmup,
+            "frame_events_ms": frame_events_ms,
             "verify": verify,
             "collect": collect,
             "oracle_check": oracle_check,

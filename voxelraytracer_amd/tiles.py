@@ -296,6 +296,15 @@ class FrameTiler:
         dist.gather(band, glist, dst=0, group=self.group)
         return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
 
+    def mark_idle(self) -> None:
+        """Declare the device idle (the caller has just synchronised it): the next frame's streams
+        need not wait for the current stream's work, so they start without cross-queue waits."""
+        self.fresh = False
+
+    def lane_streams(self):
+        """The HIP streams the frames are enqueued on (empty without part streams)."""
+        return [st for ln in (self.part_streams or ()) for st in ln]
+
     def finish(self) -> Optional[torch.Tensor]:
         cur = torch.cuda.current_stream() if self.cuda else None
         if not self.gather:

@@ -2002,9 +2002,11 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // The certified pass without the exact path fits 64 VGPRs (8 waves per SIMD) with 8 bytes of
 // scratch, but runs faster at 7 (72 VGPRs, no spills): C3 0.0464 -> 0.0447, C4 0.1751 -> 0.1605,
 // textured C3 -4 % (profiles/r03_s11, r03_s12); 6 is slower again.
-#if (defined(VRT_DEFER_WAVES) || defined(VRT_EXACT_WAVES)) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_DEFER_WAVES / VRT_EXACT_WAVES are A/B knobs of make variant builds"
+#if (defined(VRT_DEFER_WAVES) || defined(VRT_EXACT_WAVES) || defined(VRT_TPW)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEFER_WAVES / VRT_EXACT_WAVES / VRT_TPW are A/B knobs of make variant builds"
 #endif
+// VRT_TPW (diagnostic): the certified pass's workgroups render VRT_TPW consecutive tiles each, in
+// a loop (the multi-tile design of VERDICT r02 #2; record in DESIGN.md §10)
 #ifndef VRT_DEFER_WAVES
 #define VRT_DEFER_WAVES 7
 #endif
@@ -2024,7 +2026,14 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   const uint32_t wave_lin = blockIdx.x * kWgWaves + wave;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef VRT_TPW
+#pragma nounroll
+  for (uint32_t it = 0; it < (DEFER ? uint32_t(VRT_TPW) : 1u); ++it) {
+  uint32_t tile = DEFER ? blockIdx.x * uint32_t(VRT_TPW) + it : blockIdx.x;
+  if (tile >= a.tiles) break;
+#else
   uint32_t tile = blockIdx.x;
+#endif
   if constexpr (ORD) {  // heavy-first tile order (a.order): its own instance
     tile = ordered_tile(a, blockIdx.x);
     if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
@@ -2136,6 +2145,9 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
       if (lane_id() == 0 && v) atomicAdd(slot + q, v);
     }
   }
+#ifdef VRT_TPW
+  }
+#endif
 }
 
 // The r-th (from 0) set bit of m (r < popcount(m)): binary search on popcounts
@@ -2431,7 +2443,11 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   if (a.defer && !stats && a.cert == 2) {
     // certified pass, then the exact pass over the pixels it deferred (no tile order: the
     // certified pass has no long waves)
+#ifdef VRT_TPW
+    const dim3 g1((a.tiles + VRT_TPW - 1) / VRT_TPW), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+#else
     const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+#endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1> : exact_pass_kernel<false, 2>;
     if (ev_begin)

@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--shading", default="color", choices=["color", "textured"],
                     help="color: _COLOR_ONLY materials (SURVEY §8d configs); textured: the "
                          "reference's default build, atlas shading (synthetic 256/128 atlas)")
+    ap.add_argument("--atlas", default="ref", choices=["ref", "synthetic"],
+                    help="textured atlas: the reference's own textures (tests/golden/atlas fixture) "
+                         "or the synthetic one (fractional glass alpha)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="frames in flight per rank, each on its own stream(s) and output buffer "
                          "(tiles.py); 0: 4 at alpha 1 (frames independent), else 1")
@@ -229,8 +232,13 @@ def main():
     cam = vrt.make_camera(w, h)   # the config's projection (aspect W/H) at any sample density
     cam.height = frame_h
     params = vrt.default_params(R, T)
+    atlas = None
     if args.shading == "textured":
-        params = vrt.textured_params(params, vrt.make_atlas())
+        # the reference's own textures (res/textures/*128.png, decoded into a committed fixture by
+        # tests/golden/make_atlas_ref.py), or the synthetic atlas with fractional glass alpha
+        atlas = (np.load(os.path.join(ROOT, "tests", "golden", "atlas", "atlas_ref128.npz"),
+                         allow_pickle=False)["atlas"] if args.atlas == "ref" else vrt.make_atlas())
+        params = vrt.textured_params(params, atlas)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     rgba8 = args.output == "rgba8"
@@ -244,6 +252,11 @@ def main():
     ren.set_exact_pass(args.exact_pass)
     ren.set_certified(args.certified)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
+    kparams = params   # the kernel's params: textured frames use the atlas uploaded once
+    if atlas is not None:
+        ren.upload_atlas(atlas)
+        kparams = type(params).from_buffer_copy(params)
+        kparams.atlas_rgba = None   # the context's atlas: no per-call compare of its bytes
 
     def launch(row0, rows, step, out, prev, cnt_ptr=0):
         sp = torch.cuda.current_stream(dev).cuda_stream   # the part's stream (FrameTiler)
@@ -251,11 +264,11 @@ def main():
         pitch = row_pitch(out) if out.dim() == 3 else 0
         if rgba8:
             assert prev.dim() != 3 or row_pitch(prev) == pitch, "one pitch for history and output"
-            ren.render_temporal_rows_async(cam, params, args.alpha, row0, rows, step,
+            ren.render_temporal_rows_async(cam, kparams, args.alpha, row0, rows, step,
                                            prev.data_ptr(), out.data_ptr(), 0, 0, cnt_ptr, sp,
                                            pitch=pitch)
         else:
-            ren.render_rows_async(cam, params, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sp,
+            ren.render_rows_async(cam, kparams, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sp,
                                   pitch=pitch)
 
     def render_band(row0, rows, step, out, prev):
@@ -264,10 +277,10 @@ def main():
     def launch_ptrs(row0, rows, step, out_ptr, prev_ptr, pitch, sp):
         # the lean form (FrameTiler's precomputed launches): one ctypes call per part launch
         if rgba8:
-            ren.render_temporal_rows_async(cam, params, args.alpha, row0, rows, step, prev_ptr,
+            ren.render_temporal_rows_async(cam, kparams, args.alpha, row0, rows, step, prev_ptr,
                                            out_ptr, 0, 0, 0, sp, pitch=pitch)
         else:
-            ren.render_rows_async(cam, params, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch)
+            ren.render_rows_async(cam, kparams, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch)
 
     lanes = args.lanes or (4 if args.alpha == 1.0 and not args.gather_frames else 1)
     if args.gather_frames and lanes > 1:
@@ -543,7 +556,7 @@ def main():
                                              if frame_h != h else ""),
                 "max_reflections": R,
                 "max_transparencies": T,
-                "shading": ("textured (synthetic 256x256 atlas, 128 px tiles)"
+                "shading": (f"textured ({'the reference textures, atlas_ref128.npz' if args.atlas == 'ref' else 'synthetic'} 256x256 atlas, 128 px tiles)"
                             if args.shading == "textured" else "colour-only"),
                 "output": ("RGB8 ray-trace store + temporal filter (alpha %g) fused, RGBA8 words"
                            % args.alpha) if rgba8 else "float RGBA",

@@ -275,8 +275,9 @@ int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt
  * the atlas: it is uploaded by vrt_upload_atlas, or by any render call whose
  * vrt_params.atlas_rgba is non-NULL and whose bytes (or size) differ from the last upload
  * (compared on the host each call; a synchronous copy when they differ; ABI v8: by content, not
- * by pointer identity). atlas_rgba = NULL renders with the context's atlas. Replaces the Atlas
- * texture of main.cpp:187-193. */
+ * by pointer identity). atlas_rgba = NULL renders with the context's atlas: a frame loop uploads
+ * once and passes NULL (a non-NULL atlas costs a host compare of its bytes on every call, ~10 us
+ * for 256 x 256). Replaces the Atlas texture of main.cpp:187-193. */
 int vrt_upload_atlas(vrt_ctx* ctx, const uint8_t* rgba, int32_t atlas_size);
 
 /* ---- temporal filter + RGB8 framebuffer ------------------------------ */

@@ -352,7 +352,8 @@ __device__ __forceinline__ float4 lds_load(uint32_t addr) {
   return make_float4(r.x, r.y, r.z, r.w);
 }
 
-// keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop)
+// keep a per-ray constant in a register (stops the compiler re-deriving it inside the loop: the
+// IEEE 1/d per DDA step instead of a register read; v2 of DESIGN.md §6's performance log)
 __device__ __forceinline__ float opaque(float x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -444,7 +445,9 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
       q = q - s;
       t = mk(ax ? q : tp.x, ay ? q : tp.y, az ? q : tp.z);
       pidx_sel = inb ? pidx : ~0u;
-      asm volatile("" : "+v"(pidx_sel));  // materialise: no SALU live-out mask for inb
+      // materialise: no SALU live-out mask for inb (v9, DESIGN.md §6 log: 0.316 -> 0.310 ms with
+      // the other live-out masks removed)
+      asm volatile("" : "+v"(pidx_sel));
       const bool hit = SHADOW ? (v_raw != 0u && v_raw != 2u) : (v_raw != medium);
       if (!inb | hit | !(len < c.max_len) | (k >= k_max)) break;
     }
@@ -521,7 +524,9 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
   c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
   uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
-  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));  // three VGPRs, not re-derived
+  // three VGPRs, not re-derived per step (v34: C4 -2.9 %, C2 -2.7 %,
+  // profiles/r01_v34_ab_lds_address_select.log)
+  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));
   const bool skip_ok = SHADOW || medium == 0u;
   // this ray's octant volume (its skip distances look along the ray's direction); uniform for
   // shadow rays. Every octant volume holds the same voxel bytes.
@@ -586,7 +591,8 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const float num = (ca + sa) - pa;
       const float q = div_rn(num, da, ra) - s;
       t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
-      asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));  // issue it before the sample's load
+      // issue the t update before the sample's load wait (v2: its ALU then overlaps the load)
+      asm volatile("" :: "v"(t.x), "v"(t.y), "v"(t.z));
       if (!(s < s_lim)) {  // a sampled step (GetVoxel, voxel.glsl:149-154)
         const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
         const bool ex = tp.x == 0.0f;
@@ -622,6 +628,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
           x_axis = axis_index(mey, mez);
           x_vidx = inb ? int32_t(canonical_index(c, vi, vj, vk)) : -1;
           // integers in VGPRs: a bool carried out of a divergent loop costs SALU mask merges
+          // (v28 register-lean walk: 0.2146 -> 0.2038 ms with 8 waves, DESIGN.md §6 log)
           asm volatile("" : "+v"(k_exit), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
           break;
         }
@@ -629,7 +636,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     }
     it = it0 + k_exit;
     const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
-    asm volatile("" : "+v"(x_out));
+    asm volatile("" : "+v"(x_out));  // (v28, as above: kept in a VGPR across the exit)
     check = x_out != 0u;
     if (event) {  // events only come from sampled steps
       axis_out = int(x_axis);

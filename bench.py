@@ -576,21 +576,22 @@ def main():
             },
             "roofline": {
                 "bound": "valu-issue/latency",
-                "achieved": round(achieved, 2),
+                "achieved": round(per_launch, 2),
                 "achieved_is": ("reference-normalised algorithmic bytes (1 B per DDA step of the "
-                                "reference walk + 2 B per refraction probe + pixel bytes) of this "
-                                "rank's frame / GPU time per frame = per-launch rate x launches in "
-                                "flight; not a bandwidth"),
-                "achieved_per_launch": round(per_launch, 2),
-                "achieved_per_launch_is": ("bytes of one launch / its mean duration (launch_ms); a "
-                                           "launch of a large band is the certified pass "
-                                           "(render_kernel) and its deferred exact pass "
-                                           "(exact_pass_kernel) on one stream, which rocprofv3 lists "
-                                           "as two kernels whose mean durations add up to it"),
+                                "reference walk + 2 B per refraction probe + pixel bytes) of one "
+                                "launch / its mean duration (launch_ms; not a bandwidth: the certified "
+                                "walks read a few texels per pixel). A launch of a large band is the "
+                                "certified pass (render_kernel) and its deferred exact pass "
+                                "(exact_pass_kernel) on one stream, which rocprofv3 lists as two "
+                                "kernels"),
+                "achieved_frame_rate": round(achieved, 2),
+                "achieved_frame_rate_is": ("the same bytes per frame / GPU time per frame (kernel_ms) "
+                                           "= achieved x launches_in_flight: launches of frames in "
+                                           "flight overlap"),
                 "launches_in_flight": round(in_flight, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac": round(per_launch / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_is": ("measured HBM bytes per launch: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a "
                                "one-launch frame (profile stamped with this library's hash) / parts"),

@@ -12,7 +12,7 @@ import voxelraytracer_amd as vrt
 
 pytestmark = pytest.mark.gpu
 CAP = 64  # kDistCap (VRT_DIST_CAP) of csrc/vrt_render.hip
-FWD_CAP = 64  # kFwdCap (VRT_FWD_CAP)
+FWD_CAP = 128  # kFwdCap (VRT_FWD_CAP)
 
 
 def forward_reference(vox, n, octant):

@@ -502,7 +502,13 @@ __device__ __forceinline__ int dda_walk(const Ctx& c, const f3 pos, const f3 dir
 // still executed, in the reference's order, so the walk is bit-identical.
 constexpr uint32_t kDistCap = 64;  // (profiles/r01_v32_ab_distance_cap.log: 128/255 add nothing)
 static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
-constexpr uint32_t kFwdCap = 64;  // cap of F; G = F - 1 is stored in 8 bits (r01_v36_ab_fwd_cap.log)
+#if defined(VRT_FWD_CAP) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_FWD_CAP is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_FWD_CAP
+#define VRT_FWD_CAP 128
+#endif
+constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F (G = F - 1 in 8 bits): 128 vs 64 C4 -1.4 %, C1-C3 +-0.3 % (r03_s42)
 static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
 
@@ -2009,7 +2015,7 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 // The certified pass without the exact path fits 64 VGPRs (8 waves per SIMD) with 8 bytes of
 // scratch, but runs faster at 7 (72 VGPRs, no spills): C3 0.0464 -> 0.0447, C4 0.1751 -> 0.1605,
 // textured C3 -4 % (profiles/r03_s11, r03_s12); 6 is slower again.
-#if (defined(VRT_DEFER_WAVES) || defined(VRT_EXACT_WAVES) || defined(VRT_TPW)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#if (defined(VRT_DEFER_WAVES) || defined(VRT_EXACT_WAVES) || defined(VRT_TPW) || defined(VRT_DIAG_SKIP_EXACT)) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_DEFER_WAVES / VRT_EXACT_WAVES / VRT_TPW are A/B knobs of make variant builds"
 #endif
 // VRT_TPW (diagnostic): the certified pass's workgroups render VRT_TPW consecutive tiles each, in
@@ -2202,6 +2208,9 @@ __global__ void __launch_bounds__(64, VRT_EXACT_WAVES) exact_pass_kernel(KArgs a
   const uint32_t* ctr = a.defer;
   if (blockIdx.x == 0 && lane < 2u * kOrdClasses)  // both kinds of the other set, for the next launch
     a.defer[(((lane / kOrdClasses) * 2u + (a.defer_e ^ 1u)) * kOrdClasses + lane % kOrdClasses) * kOrdCtrStride] = 0u;
+#ifdef VRT_DIAG_SKIP_EXACT  // diagnostic bound (wrong images): the frame without its deferred pixels
+  return;
+#endif
   uint32_t ns[kOrdClasses], nd[kOrdClasses], total_s = 0, total_d = 0;
 #pragma unroll
   for (uint32_t q = 0; q < kOrdClasses; ++q) {

@@ -38,11 +38,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (default 4): the lanes'
-# streams (4 frames in flight), the main stream and, at N > 1, the RCCL streams need more than 4,
-# or two streams share a queue and serialise; 16 (before HIP initialises). Neutral for one stream
-# pair (C3 0.0667 ms/frame at 4 queues, 0.0669 at 16, profiles/r02_s08).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# HIP spreads streams round-robin over GPU_MAX_HW_QUEUES hardware queues (HIP's default 4, and what
+# the GPU box exports): the four lanes (frames in flight) then have a queue each. More queues or
+# lanes are slower (C3 ms/frame at 4 / 8 / 16 queues: 4 lanes 0.0386 / 0.0388 / 0.0387, 6 lanes
+# 0.0469 / 0.0435 / 0.0628, 8 lanes 0.0387 / 0.0420 / 0.0497; profiles/r03_s48). Set before HIP
+# initialises, only when the environment has no value.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "4")
 
 CONFIGS = {
     # name: (scene, N, W, H, R, T, description)
@@ -90,7 +91,13 @@ def parse():
                          "or the synthetic one (fractional glass alpha)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="frames in flight per rank, each on its own stream(s) and output buffer "
-                         "(tiles.py); 0: 4 at alpha 1 (frames independent), else 1")
+                         "(tiles.py); 0 at alpha 1 (frames independent): 8 for a band below one "
+                         "dispatch round of waves (with 8 hardware queues, see --queues), else 4; "
+                         "1 at alpha != 1")
+    ap.add_argument("--queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts); 0: 8 with "
+                         "8 lanes for bands below one dispatch round of waves, else the "
+                         "environment's value (4 on the GPU box, HIP's default)")
     ap.add_argument("--parts", type=int, default=0,
                     help="interleaved row parts per frame, each on its own HIP stream (tiles.py); "
                          "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
@@ -107,6 +114,13 @@ def parse():
                     help="one GPU, one process: time only rank 0's band of a K-way strong split "
                          "(what each GPU of a K-GPU run renders per frame; rays counted over the "
                          "whole frame); a diagnostic of the scaling path, labelled as such")
+    ap.add_argument("--rehearse-rank", type=int, default=0,
+                    help="with --rehearse-ranks K: time rank R's band instead of rank 0's (block-"
+                         "cyclic bands differ by up to one block; the K-GPU frame is the slowest)")
+    ap.add_argument("--row-block", type=int, default=0,
+                    help="rows per block of a rank's band (vrt_render_*_blocks_pitched_async, ABI "
+                         "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 8 for a "
+                         "split frame of one part per lane, else 1 (cyclic rows)")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
     ap.add_argument("--gather-frames", action="store_true",
@@ -199,8 +213,37 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+# resident waves of the certified pass on one MI355X: 256 CUs x 4 SIMDs x 7 waves
+# (vrt_context.cpp's wave_slots; a band below one such round is latency-bound)
+WAVE_SLOTS = 256 * 4 * 7
+
+
+def pipeline_shape(args, world: int):
+    """(lanes, hardware queues) of this rank's frame pipeline, decided before HIP starts. A band
+    below one dispatch round of waves (C3 / C2 at 8 ranks: 4 080 waves) is the latency of its
+    slowest waves, and 8 frames in flight on 8 hardware queues hide them (C3 k = 8, slowest rank:
+    0.0139 -> 0.0085 ms per frame; C2 k = 8 0.0130 -> 0.0111); larger bands and whole frames are
+    faster with 4 on 4 (whole C3 0.0387 vs 0.0420; C3 k = 4 0.0149 vs 0.0154; C4 k = 8 0.0236 vs
+    0.0275; profiles/r03_s48-r03_s50)."""
+    _, _, w, h, _, _, _ = CONFIGS[args.config]
+    frame_h = h * world if args.scaling == "weak" else h
+    split = max(world, args.rehearse_ranks if world == 1 else 1)
+    rows = -(-frame_h // split)
+    waves = -(-w // 8) * -(-rows // 8)
+    small = split > 1 and waves < WAVE_SLOTS
+    independent = args.alpha == 1.0 and not args.gather_frames
+    lanes = args.lanes or ((8 if small else 4) if independent else 1)
+    queues = args.queues or (8 if small and lanes == 8 else 4)
+    return lanes, queues
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    lanes, queues = pipeline_shape(args, world)
+    if args.queues or queues != 4:   # before HIP initialises (the GPU box exports 4)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -208,7 +251,6 @@ def main():
     import voxelraytracer_amd as vrt
     from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume, row_pitch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
@@ -258,7 +300,7 @@ def main():
         kparams = type(params).from_buffer_copy(params)
         kparams.atlas_rgba = None   # the context's atlas: no per-call compare of its bytes
 
-    def launch(row0, rows, step, out, prev, cnt_ptr=0):
+    def launch(row0, rows, step, out, prev, cnt_ptr=0, row_block=1):
         sp = torch.cuda.current_stream(dev).cuda_stream   # the part's stream (FrameTiler)
         # a part may be a row-strided view into the frame (FrameTiler's single-rank mode)
         pitch = row_pitch(out) if out.dim() == 3 else 0
@@ -266,23 +308,23 @@ def main():
             assert prev.dim() != 3 or row_pitch(prev) == pitch, "one pitch for history and output"
             ren.render_temporal_rows_async(cam, kparams, args.alpha, row0, rows, step,
                                            prev.data_ptr(), out.data_ptr(), 0, 0, cnt_ptr, sp,
-                                           pitch=pitch)
+                                           pitch=pitch, row_block=row_block)
         else:
             ren.render_rows_async(cam, kparams, row0, rows, step, out.data_ptr(), 0, cnt_ptr, sp,
-                                  pitch=pitch)
+                                  pitch=pitch, row_block=row_block)
 
-    def render_band(row0, rows, step, out, prev):
-        launch(row0, rows, step, out, prev)
+    def render_band(row0, rows, step, out, prev, row_block=1):
+        launch(row0, rows, step, out, prev, row_block=row_block)
 
-    def launch_ptrs(row0, rows, step, out_ptr, prev_ptr, pitch, sp):
+    def launch_ptrs(row0, rows, step, out_ptr, prev_ptr, pitch, sp, row_block=1):
         # the lean form (FrameTiler's precomputed launches): one ctypes call per part launch
         if rgba8:
             ren.render_temporal_rows_async(cam, kparams, args.alpha, row0, rows, step, prev_ptr,
-                                           out_ptr, 0, 0, 0, sp, pitch=pitch)
+                                           out_ptr, 0, 0, 0, sp, pitch=pitch, row_block=row_block)
         else:
-            ren.render_rows_async(cam, kparams, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch)
+            ren.render_rows_async(cam, kparams, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch,
+                                  row_block=row_block)
 
-    lanes = args.lanes or (4 if args.alpha == 1.0 and not args.gather_frames else 1)
     if args.gather_frames and lanes > 1:
         raise SystemExit("--gather-frames renders one frame at a time (--lanes 1)")
     parts = args.parts or (1 if lanes > 1 else 2)
@@ -291,10 +333,18 @@ def main():
     rehearse = args.rehearse_ranks if world == 1 and args.rehearse_ranks > 1 else 0
     if rehearse and (args.gather_frames or args.scaling != "strong"):
         raise SystemExit("--rehearse-ranks rehearses the strong split without per-frame gathers")
-    tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None, rank=0 if rehearse else None,
+    if not 0 <= args.rehearse_rank < max(rehearse, 1):
+        raise SystemExit("--rehearse-rank must be one of the rehearsed split's ranks")
+    split = max(world, rehearse) > 1
+    # block-cyclic bands (8-row blocks) for a split frame rendered as one part per lane: every
+    # 8x8 wave covers 8 adjacent frame rows, as in the whole frame
+    row_block = args.row_block or (8 if split and parts == 1 and not args.gather_frames else 1)
+    tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None,
+                       rank=args.rehearse_rank if rehearse else None,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
                        gather=args.gather_frames, lanes=lanes,
-                       independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs)
+                       independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs,
+                       row_block=row_block)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -302,19 +352,22 @@ def main():
     part_bytes = []
     own = None
     count_specs = tiler.specs
-    if rehearse:   # the whole frame's rays: every rank's parts of the rehearsed split
-        from voxelraytracer_amd.tiles import part_spec
-        count_specs = [part_spec(r_, rehearse, s_, parts, frame_h) for r_ in range(rehearse)
-                       for s_ in range(parts)]
+    if rehearse:   # the whole frame's rays: every rank's parts of the rehearsed split, own first
+        from voxelraytracer_amd.tiles import block_band_spec, part_spec
+        order = [args.rehearse_rank] + [r_ for r_ in range(rehearse) if r_ != args.rehearse_rank]
+        count_specs = ([block_band_spec(r_, rehearse, frame_h, row_block) for r_ in order]
+                       if row_block > 1 else
+                       [part_spec(r_, rehearse, s_, parts, frame_h) for r_ in order
+                        for s_ in range(parts)])
     own_cnt = torch.zeros_like(cnt)
     for i_, (row0, rows, step) in enumerate(count_specs):
         pc = torch.zeros_like(cnt)
         scratch = torch.zeros((rows, w, 4), dtype=torch.uint8 if rgba8 else torch.float32, device=dev)
-        launch(row0, rows, step, scratch, scratch, pc.data_ptr())
+        launch(row0, rows, step, scratch, scratch, pc.data_ptr(), row_block)
         torch.cuda.synchronize(dev)
         pcd = vrt.counters_dict(pc.cpu().tolist())
         cnt += pc
-        if i_ < parts:   # this rank's own parts (rank 0's when rehearsing)
+        if i_ < parts:   # this rank's own parts (the rehearsed rank's when rehearsing)
             part_bytes.append(vrt.algorithmic_bytes(pcd, 8 if rgba8 else 16))
             own_cnt += pc
     own = vrt.counters_dict(own_cnt.cpu().tolist())
@@ -429,7 +482,7 @@ def main():
                 got = last_parts()[s_].contiguous()
                 ref = torch.zeros_like(got)
                 prev_c = prev_parts[s_].contiguous()
-                launch(row0, rows, step, ref, prev_c, vc.data_ptr())   # counters on: STATS instance
+                launch(row0, rows, step, ref, prev_c, vc.data_ptr(), row_block)   # STATS instance
                 torch.cuda.synchronize(dev)
                 bad += int((got != ref).sum().item())
                 total += got.numel()
@@ -459,6 +512,8 @@ def main():
                        "what": "one gather of every rank's band of the last frame to rank 0 and its "
                                "re-interleave, after the timed region"}
 
+    band_kind = (f"block-cyclic bands of {row_block}-row blocks" if row_block > 1 else
+                 "cyclic row bands")
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
@@ -562,17 +617,19 @@ def main():
                            % args.alpha) if rgba8 else "float RGBA",
                 "parallelism": ((f"cyclic row bands x{world} + RCCL gather to rank 0 every frame"
                                  if args.gather_frames else
-                                 f"cyclic row bands x{world} ({args.scaling} scaling), no collective "
+                                 f"{band_kind} x{world} ({args.scaling} scaling), no collective "
                                  "in the timed region (one RCCL gather of the last frame after it)")
                                 if world > 1 else
-                                (f"REHEARSAL on one GPU: only rank 0's band of a {rehearse}-way strong "
-                                 "split is rendered and timed; rays counted over the whole frame"
+                                (f"REHEARSAL on one GPU: only rank {args.rehearse_rank}'s band "
+                                 f"({band_kind}) of a {rehearse}-way strong split is rendered and "
+                                 "timed; rays counted over the whole frame"
                                  if rehearse else "single GPU, whole frame"))
                                + (f", {lanes} frames in flight (lanes)" if lanes > 1 else "")
                                + f", {parts} interleaved row part{'s' if parts > 1 else ''} per "
                                f"frame on {lanes * parts} HIP stream{'s' if lanes * parts > 1 else ''}",
                 "rays_per_frame": rays_per_frame,
                 "algorithmic_bytes_per_frame": bytes_per_frame,
+                "hw_queues": queues,
             },
             "roofline": {
                 "bound": "valu-issue/latency",

@@ -25,7 +25,7 @@ def free_port():
 
 
 def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1, gather=True,
-           lanes=1):
+           lanes=1, row_block=1):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -33,7 +33,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle
     import voxelraytracer_amd as vrt
-    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume
+    from voxelraytracer_amd.tiles import FrameTiler, band_frame_rows, broadcast_volume
 
     vox = torch.from_numpy(vrt.build_scene("glass_cube", n)) if rank == 0 else \
         torch.zeros(n ** 3, dtype=torch.uint8)
@@ -43,9 +43,13 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
     params = [vrt.default_params(1, 2, time=float(t + 1), ray_noise=0.05) for t in range(frames)]
     state = {"i": 0}
 
-    def render_band(row0, rows, step, out, prev):
-        rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"] // parts], row0=row0, rows=rows,
-                                   row_step=step, threads=1)
+    def render_band(row0, rows, step, out, prev, row_block=1):
+        if row_block > 1:   # block-cyclic band: the band's frame rows of a whole oracle frame
+            full, _, _ = oracle.render(cam, vox_np, n, params[state["i"] // parts], threads=1)
+            rgba = full[band_frame_rows(row0, rows, step, row_block).numpy()]
+        else:
+            rgba, _, _ = oracle.render(cam, vox_np, n, params[state["i"] // parts], row0=row0,
+                                       rows=rows, row_step=step, threads=1)
         if mode == "rgba8":   # the fused temporal filter + RGB8 store, band-local history
             _, cur = oracle.temporal(rgba, prev.numpy().copy(), alpha)
             out.copy_(torch.from_numpy(cur))
@@ -55,7 +59,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
 
     tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
                        dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts,
-                       gather=gather, lanes=lanes)
+                       gather=gather, lanes=lanes, row_block=row_block)
     got = []
     for _ in range(frames):
         f = tiler.frame()
@@ -279,6 +283,54 @@ def test_distributed_lanes(built, world, lanes):
     port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
                                               1, False, lanes)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, _ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    hist = np.zeros((h, w, 4), np.uint8)
+    assert len(got) == frames
+    for t in range(frames):
+        rgba, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                   ray_noise=0.05))
+        _, hist = oracle.temporal(rgba, hist, alpha)
+        assert np.array_equal(got[t], hist), t
+
+
+def test_block_band_spec_covers_the_frame():
+    """Block-cyclic bands (ABI v11 row_block): every frame row exactly once, bands within one
+    block of each other, block 1 = the cyclic band, ragged heights and more ranks than blocks."""
+    from voxelraytracer_amd.tiles import band_frame_rows, band_spec, block_band_spec
+
+    assert block_band_spec(1, 4, 1080, 1) == band_spec(1, 4, 1080)
+    assert block_band_spec(0, 8, 1080, 8) == (0, 136, 64)   # 135 blocks: ranks 0-6 get 17
+    assert block_band_spec(7, 8, 1080, 8) == (56, 128, 64)
+    for h, world, b in [(1080, 8, 8), (2160, 8, 8), (21, 3, 4), (12, 2, 8), (5, 4, 8), (7, 3, 2)]:
+        specs = [block_band_spec(r, world, h, b) for r in range(world)]
+        rows = torch.cat([band_frame_rows(*sp, b) for sp in specs])
+        assert sorted(rows.tolist()) == list(range(h)), (h, world, b)
+        assert max(sp[1] for sp in specs) - min(sp[1] for sp in specs) <= b
+    with pytest.raises(ValueError):
+        block_band_spec(0, 2, 16, 3)
+
+
+@pytest.mark.parametrize("world,h,row_block,lanes", [(2, 16, 8, 2), (3, 21, 4, 2)])
+def test_block_bands_without_per_frame_gather(built, world, h, row_block, lanes):
+    """Block-cyclic bands kept on their ranks with frames in flight (bench.py's multi-GPU default:
+    8-row blocks), incl. a ragged split (21 rows in blocks of 4 over 3 ranks: bands of 8, 8, 5
+    rows): collect() assembles the single-process RGBA8 temporal sequence bit for bit."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, frames, alpha = 16, 20, 3, 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
+                                              1, False, lanes, row_block)) for r in range(world)]
     for p in procs:
         p.start()
     got, _ = q.get(timeout=120)

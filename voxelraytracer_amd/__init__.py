@@ -288,9 +288,19 @@ class Renderer:
 
     def render_rows_async(self, cam: Camera, params: Params, row0: int, rows: int, row_step: int,
                           d_out: int, d_hit: int = 0, d_counters: int = 0, stream: int = 0,
-                          pitch: int = 0):
+                          pitch: int = 0, row_block: int = 1):
         """Band render into device pointers (e.g. torch tensors' data_ptr()) on a HIP stream.
-        pitch: pixels from one band row to the next (0 = width: a compact band buffer)."""
+        pitch: pixels from one band row to the next (0 = width: a compact band buffer).
+        row_block > 1: block-cyclic band (ABI v11): band row i is frame row
+        row0 + (i // row_block) * row_step + i % row_block."""
+        if row_block != 1:
+            self._check(
+                self._lib.vrt_render_blocks_pitched_async(
+                    self._h, C.byref(cam), C.byref(params), row0, rows, row_step, row_block,
+                    pitch or cam.width, d_out, d_hit or None, d_counters or None, stream or None),
+                "vrt_render_blocks_pitched_async",
+            )
+            return
         if pitch:
             self._check(
                 self._lib.vrt_render_rows_pitched_async(
@@ -309,10 +319,20 @@ class Renderer:
     def render_temporal_rows_async(self, cam: Camera, params: Params, alpha: float, row0: int,
                                    rows: int, row_step: int, d_prev: int, d_cur: int,
                                    d_raw: int = 0, d_hit: int = 0, d_counters: int = 0,
-                                   stream: int = 0, pitch: int = 0):
+                                   stream: int = 0, pitch: int = 0, row_block: int = 1):
         """Band render with the fused temporal filter + RGB8 store (vrt_render_temporal_rows_async)
         into device RGBA8 buffers (e.g. torch uint8 [rows, W, 4] tensors' data_ptr()). pitch:
-        pixels from one band row to the next in every buffer (0 = width)."""
+        pixels from one band row to the next in every buffer (0 = width). row_block > 1:
+        block-cyclic band (vrt_render_temporal_blocks_pitched_async, ABI v11)."""
+        if row_block != 1:
+            self._check(
+                self._lib.vrt_render_temporal_blocks_pitched_async(
+                    self._h, C.byref(cam), C.byref(params), alpha, row0, rows, row_step,
+                    row_block, pitch or cam.width, d_prev, d_cur, d_raw or None, d_hit or None,
+                    d_counters or None, stream or None),
+                "vrt_render_temporal_blocks_pitched_async",
+            )
+            return
         if pitch:
             self._check(
                 self._lib.vrt_render_temporal_rows_pitched_async(

@@ -70,7 +70,7 @@ constexpr int kRing = 8;
 static_assert(kRing % kLanes == 0, "a ring slot is always written from the same lane");
 
 struct OrderSlot {
-  int32_t width = 0, rows = 0, row0 = 0, row_step = 0;
+  int32_t width = 0, rows = 0, row0 = 0, row_step = 0, row_blk_sh = 0;
   hipStream_t stream = nullptr;
   uint32_t* d = nullptr;       // kOrderSlotWords words inside the shard's pool
   bool used = false;
@@ -357,6 +357,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.row0 = row0;
   a.rows = rows;
   a.row_step = row_step;
+  a.row_blk_sh = 0;
   a.pitch = cam->width;
   a.ostride = s.octants == 8 ? uint32_t(uint64_t(s.n + 1) * (s.n + 1) * (s.n + 1) * sizeof(uint16_t)) : 0u;
   a.max_refl = p->max_reflections;
@@ -394,7 +395,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
   OrderSlot* slot = nullptr;
   for (auto& o : s.order)
     if (o.used && o.width == a.width && o.rows == a.rows && o.row0 == a.row0 && o.row_step == a.row_step &&
-        o.stream == st)
+        o.row_blk_sh == a.row_blk_sh && o.stream == st)
       slot = &o;
   if (!slot) {
     slot = &s.order[0];
@@ -408,6 +409,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
     slot->rows = a.rows;
     slot->row0 = a.row0;
     slot->row_step = a.row_step;
+    slot->row_blk_sh = a.row_blk_sh;
     slot->stream = st;
     slot->epoch = 0;
     slot->last_defer = false;
@@ -1178,11 +1180,18 @@ int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_
   return VRT_OK;
 }
 
-// Band arguments shared by the async entry points: rows inside the image, pitch >= width.
+// Band arguments shared by the async entry points: rows inside the image, pitch >= width; blocks
+// of row_block rows (a power of two <= 64) that do not overlap (row_step >= row_block unless the
+// band is one block). *sh receives log2(row_block).
 static int check_band(vrt_ctx* ctx, const vrt_camera* cam, int32_t row0, int32_t rows, int32_t row_step,
-                      int64_t pitch) {
-  if (rows < 0 || row_step < 1 || row0 < 0 ||
-      (rows > 0 && int64_t(row0) + int64_t(rows - 1) * row_step >= cam->height))
+                      int64_t pitch, int32_t row_block = 1, int32_t* sh = nullptr) {
+  int32_t b = 0;
+  while (b < 7 && (1 << b) != row_block) ++b;
+  if (b == 7) return fail(ctx, VRT_ERR_INVALID, "row_block must be a power of two in [1, 64]");
+  if (sh) *sh = b;
+  const int64_t last = rows > 0 ? int64_t(row0) + int64_t((rows - 1) >> b) * row_step + ((rows - 1) & (row_block - 1)) : 0;
+  if (rows < 0 || row_step < 1 || row0 < 0 || (rows > row_block && row_step < row_block) ||
+      (rows > 0 && last >= cam->height))
     return fail(ctx, VRT_ERR_INVALID, "row band outside the image");
   if (pitch < cam->width || pitch > INT32_MAX) return fail(ctx, VRT_ERR_INVALID, "row pitch must be >= the image width");
   return VRT_OK;
@@ -1196,17 +1205,19 @@ void launch_timing_events(vrt_ctx* ctx, hipEvent_t& begin, hipEvent_t& end) {
   end = ctx->lt_ev[ctx->lt_used++];
 }
 
-int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
-                                  int32_t rows, int32_t row_step, int64_t pitch, float* d_out_rgba,
-                                  vrt_hit* d_out_hit, uint64_t* d_counters, void* hip_stream) {
+int vrt_render_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                                    int32_t rows, int32_t row_step, int32_t row_block, int64_t pitch,
+                                    float* d_out_rgba, vrt_hit* d_out_hit, uint64_t* d_counters, void* hip_stream) {
   if (!ctx) return VRT_ERR_INVALID;
   int st = check_render_args(ctx, cam, p);
   if (st != VRT_OK) return st;
   if (!d_out_rgba) return fail(ctx, VRT_ERR_INVALID, "null output");
-  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
+  int32_t sh = 0;
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch, row_block, &sh)) != VRT_OK) return st;
   if (rows == 0) return VRT_OK;
   Shard& s = ctx->sh[0];
   vrt::KArgs a = make_args(ctx, s, cam, p, row0, rows, row_step);
+  a.row_blk_sh = sh;
   a.pitch = int32_t(pitch);
   hipEvent_t eb, ee;
   launch_timing_events(ctx, eb, ee);
@@ -1214,6 +1225,13 @@ int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt
          reinterpret_cast<unsigned long long*>(d_counters), static_cast<hipStream_t>(hip_stream), eb, ee);
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
+}
+
+int vrt_render_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0,
+                                  int32_t rows, int32_t row_step, int64_t pitch, float* d_out_rgba,
+                                  vrt_hit* d_out_hit, uint64_t* d_counters, void* hip_stream) {
+  return vrt_render_blocks_pitched_async(ctx, cam, p, row0, rows, row_step, 1, pitch, d_out_rgba, d_out_hit,
+                                         d_counters, hip_stream);
 }
 
 int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, int32_t row0, int32_t rows,
@@ -1225,19 +1243,21 @@ int vrt_render_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params*
                                        d_counters, hip_stream);
 }
 
-int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
-                                           float alpha, int32_t row0, int32_t rows, int32_t row_step,
-                                           int64_t pitch, const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
-                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
-                                           void* hip_stream) {
+int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
+                                             float alpha, int32_t row0, int32_t rows, int32_t row_step,
+                                             int32_t row_block, int64_t pitch, const uint32_t* d_prev_rgba8,
+                                             uint32_t* d_cur_rgba8, uint32_t* d_raw_rgba8, vrt_hit* d_out_hit,
+                                             uint64_t* d_counters, void* hip_stream) {
   if (!ctx) return VRT_ERR_INVALID;
   int st = check_render_args(ctx, cam, p);
   if (st != VRT_OK) return st;
   if (!d_prev_rgba8 || !d_cur_rgba8) return fail(ctx, VRT_ERR_INVALID, "null history or output");
-  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch)) != VRT_OK) return st;
+  int32_t sh = 0;
+  if ((st = check_band(ctx, cam, row0, rows, row_step, pitch, row_block, &sh)) != VRT_OK) return st;
   if (rows == 0) return VRT_OK;
   Shard& s = ctx->sh[0];
   vrt::KArgs a = make_args(ctx, s, cam, p, row0, rows, row_step);
+  a.row_blk_sh = sh;
   a.pitch = int32_t(pitch);
   a.alpha = alpha;
   a.prev = d_prev_rgba8;
@@ -1249,6 +1269,16 @@ int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, 
          static_cast<hipStream_t>(hip_stream), eb, ee);
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
+}
+
+int vrt_render_temporal_rows_pitched_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p,
+                                           float alpha, int32_t row0, int32_t rows, int32_t row_step,
+                                           int64_t pitch, const uint32_t* d_prev_rgba8, uint32_t* d_cur_rgba8,
+                                           uint32_t* d_raw_rgba8, vrt_hit* d_out_hit, uint64_t* d_counters,
+                                           void* hip_stream) {
+  return vrt_render_temporal_blocks_pitched_async(ctx, cam, p, alpha, row0, rows, row_step, 1, pitch,
+                                                  d_prev_rgba8, d_cur_rgba8, d_raw_rgba8, d_out_hit,
+                                                  d_counters, hip_stream);
 }
 
 int vrt_render_temporal_rows_async(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float alpha,

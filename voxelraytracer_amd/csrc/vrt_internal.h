@@ -23,7 +23,9 @@ struct KArgs {
   float fn;
   int32_t n, width, height;
   int32_t row0, rows, row_step;
-  int32_t pitch;  // pixels from one band row to the next in every output/history buffer (>= width)
+  int32_t row_blk_sh;  // log2 of the band's row block (ABI v11): band row i -> frame row
+                       // row0 + (i >> row_blk_sh) * row_step + (i & (2^row_blk_sh - 1))
+  int32_t pitch; // pixels from one band row to the next in every output/history buffer (>= width)
   uint32_t ostride;  // bytes from one direction octant's packed volume to the next (0: one volume)
   int32_t max_refl, max_transp;
   // textured mode (!_COLOR_ONLY): atlas of atlas_size^2 RGBA8 words, row 0 = bottom

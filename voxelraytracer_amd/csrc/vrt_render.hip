@@ -1777,6 +1777,11 @@ __device__ __forceinline__ int pixel_x(uint32_t tx, int wave, uint32_t lane) {
 __device__ __forceinline__ int pixel_row(uint32_t ty, int wave, uint32_t lane) {
   return int(ty) * kTileH + (wave >> 1) * 8 + int(lane >> 3);
 }
+// frame row of band row li: blocks of 2^row_blk_sh adjacent rows, row_step rows apart (ABI v11);
+// row_blk_sh = 0 is the cyclic-row band row0 + li * row_step
+__device__ __forceinline__ int frame_row(const KArgs& a, int li) {
+  return a.row0 + (li >> a.row_blk_sh) * a.row_step + (li & ((1 << a.row_blk_sh) - 1));
+}
 
 #ifdef VRT_STAMPS
 // Diagnostic build only (scripts/stamps.py): per wave {start, end} s_memrealtime (100 MHz) and
@@ -2068,7 +2073,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     init_ctx(c, a, vox);
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * kAxLane];
-    const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
+    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
     uint32_t steps = 0, flags = 0;
@@ -2242,7 +2247,7 @@ __global__ void __launch_bounds__(64, VRT_EXACT_WAVES) exact_pass_kernel(KArgs a
     const uint32_t e = dense ? list[a.defer_seg - 64u * (idx + 1u) + lane] : list[idx];
     if (e == ~0u) continue;  // a lane of a dense chunk whose pixel the certified pass settled
     const int px = int(e & 0xFFFFu), li = int(e >> 16);
-    const Ray ray = primary_ray(a, c, px, a.row0 + li * a.row_step);
+    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
     Counters k;
 #pragma unroll
     for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;

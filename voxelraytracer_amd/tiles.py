@@ -45,6 +45,29 @@ def band_spec(rank: int, world: int, height: int):
     return rank, height // world, world
 
 
+def block_band_spec(rank: int, world: int, height: int, block: int):
+    """(row0, rows, row_step) of rank's block-cyclic band (ABI v11's row_block form): blocks of
+    `block` adjacent frame rows, rank r owns blocks r, r + world, ...; band row i is frame row
+    row0 + (i // block) * row_step + i % block. The last block is short when height % block != 0,
+    and bands differ by at most one block (no divisibility needed). block = 1 is band_spec's
+    cyclic band. An 8x8 pixel wave of a block-8 band covers 8 adjacent frame rows, as in the whole
+    frame, instead of 8 rows `world` apart (coherent walks: DESIGN.md §8)."""
+    if block & (block - 1) or not 1 <= block <= 64:
+        raise ValueError("block must be a power of two in [1, 64]")
+    nb = -(-height // block)
+    own = max(0, (nb - rank + world - 1) // world)
+    rows = own * block
+    if own and (nb - 1) % world == rank:
+        rows -= nb * block - height
+    return rank * block, rows, world * block
+
+
+def band_frame_rows(row0: int, rows: int, row_step: int, block: int = 1) -> torch.Tensor:
+    """Frame row of every band row of a (block-)cyclic band, as an int64 index tensor."""
+    i = torch.arange(rows, dtype=torch.int64)
+    return row0 + (i // block) * row_step + i % block
+
+
 def part_spec(rank: int, world: int, part: int, parts: int, height: int):
     """(row0, rows, row_step) of part `part` of rank's band: global part q = part*world + rank
     owns frame rows q, q + world*parts, ...; height must divide by world*parts."""
@@ -118,7 +141,7 @@ class FrameTiler:
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
                  channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
                  lanes: int = 1, independent: bool = False, launch: Optional[Callable] = None,
-                 world: Optional[int] = None, rank: Optional[int] = None):
+                 world: Optional[int] = None, rank: Optional[int] = None, row_block: int = 1):
         # world / rank: override the process group's (one process rehearsing rank `rank` of a
         # `world`-way split on one GPU; no exchange may then be requested)
         self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -127,8 +150,18 @@ class FrameTiler:
             raise ValueError("a rehearsed split keeps its band (gather=False)")
         self.group = group
         self.width, self.height, self.parts = width, height, parts
-        self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
-        self.specs = [part_spec(self.rank, self.world, s, parts, height) for s in range(parts)]
+        self.row_block = row_block
+        if row_block > 1:   # block-cyclic band, one part, kept on its rank (bands may be unequal)
+            if parts != 1 or gather:
+                raise ValueError("block-cyclic bands are one part per lane and stay on their rank "
+                                 "(parts=1, gather=False)")
+            self.row0, self.rows, self.step = block_band_spec(self.rank, self.world, height, row_block)
+            self.specs = [(self.row0, self.rows, self.step)]
+        else:
+            self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
+            self.specs = [part_spec(self.rank, self.world, s, parts, height) for s in range(parts)]
+        # render_band / launch receive row_block= only for block-cyclic bands
+        self.block_kw = {"row_block": row_block} if row_block > 1 else {}
         self.rows_p = self.specs[0][1]
         self.render_band = render_band
         self.cuda = torch.device(device).type == "cuda"
@@ -201,7 +234,7 @@ class FrameTiler:
             if wait_work is not None:
                 wait_work.wait()
             for s, (row0, rows, step) in enumerate(self.specs):
-                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
+                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev), **self.block_kw)
             return None
         cur = torch.cuda.current_stream()
         if self.fresh:
@@ -219,7 +252,7 @@ class FrameTiler:
                     wait_work.wait()
                 if dep and self.part_done[prev_lane][s] is not None:
                     st.wait_event(self.part_done[prev_lane][s])   # the history rows of part s
-                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev))
+                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev), **self.block_kw)
                 ev = st.record_event() if (dep or self.gather) else None
                 self.part_done[lane][s] = ev
                 events.append(ev)
@@ -237,7 +270,7 @@ class FrameTiler:
                         st.wait_stream(cur)
                 self.fresh = False
             for args in self.plan[lane]:
-                self.launch(*args)
+                self.launch(*args, **self.block_kw)
             return self.bufs[lane]
         if not self.gather:   # one rank, or ranks that keep their bands: no exchange
             lane = self.k % self.lanes
@@ -292,9 +325,23 @@ class FrameTiler:
         band = self.last().contiguous()
         if self.world == 1:
             return band
-        glist = ([torch.empty_like(band) for _ in range(self.world)] if self.rank == 0 else None)
-        dist.gather(band, glist, dst=0, group=self.group)
-        return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
+        if self.row_block == 1:
+            glist = ([torch.empty_like(band) for _ in range(self.world)] if self.rank == 0 else None)
+            dist.gather(band, glist, dst=0, group=self.group)
+            return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
+        # block-cyclic bands may differ by one block: gather them padded to the largest
+        specs = [block_band_spec(r, self.world, self.height, self.row_block) for r in range(self.world)]
+        rmax = max(sp[1] for sp in specs)
+        pad = band.new_zeros((rmax,) + tuple(band.shape[1:]))
+        pad[:band.shape[0]] = band
+        glist = ([torch.empty_like(pad) for _ in range(self.world)] if self.rank == 0 else None)
+        dist.gather(pad, glist, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
+        out = band.new_empty((self.height,) + tuple(band.shape[1:]))
+        for r, (row0, rows, step) in enumerate(specs):
+            out[band_frame_rows(row0, rows, step, self.row_block).to(out.device)] = glist[r][:rows]
+        return out
 
     def mark_idle(self) -> None:
         """Declare the device idle (the caller has just synchronised it): the next frame's streams

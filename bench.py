@@ -119,7 +119,7 @@ def parse():
                          "cyclic bands differ by up to one block; the K-GPU frame is the slowest)")
     ap.add_argument("--row-block", type=int, default=0,
                     help="rows per block of a rank's band (vrt_render_*_blocks_pitched_async, ABI "
-                         "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 8 for a "
+                         "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 16 for a "
                          "split frame of one part per lane, else 1 (cyclic rows)")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
@@ -336,9 +336,11 @@ def main():
     if not 0 <= args.rehearse_rank < max(rehearse, 1):
         raise SystemExit("--rehearse-rank must be one of the rehearsed split's ranks")
     split = max(world, rehearse) > 1
-    # block-cyclic bands (8-row blocks) for a split frame rendered as one part per lane: every
-    # 8x8 wave covers 8 adjacent frame rows, as in the whole frame
-    row_block = args.row_block or (8 if split and parts == 1 and not args.gather_frames else 1)
+    # block-cyclic bands (16-row blocks) for a split frame rendered as one part per lane: every
+    # 8x8 wave covers 8 adjacent frame rows, as in the whole frame, and a 16x8 workgroup's two
+    # neighbours in the band are adjacent too (16 vs 8 rows: C4 k = 8 -3 %, C3 k = 4 -5 %, others
+    # equal; profiles/r03_s54)
+    row_block = args.row_block or (16 if split and parts == 1 and not args.gather_frames else 1)
     tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None,
                        rank=args.rehearse_rank if rehearse else None,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,

@@ -3,7 +3,7 @@
 The per-pixel program has no halo and no inter-ray exchange, so a frame splits into row bands,
 one per rank (one process per GPU). Bands are cyclic — rank r owns rows r, r+N, r+2N, ... — so
 every rank gets the same mix of cheap sky rows and expensive geometry rows. With row_block = B
-(ABI v11; bench.py's split frames use 8) rank r owns blocks r, r+N, ... of B adjacent rows instead,
+(ABI v11; bench.py's split frames use 16) rank r owns blocks r, r+N, ... of B adjacent rows instead,
 so an 8x8 pixel wave covers 8 adjacent frame rows and its rays' walks stay as coherent as in the
 whole frame (the slowest of 8 bands: C3 0.0150 -> 0.0139, C4 0.0274 -> 0.0237 ms per frame,
 profiles/r03_s45, r03_s46); bands then differ by at most one block. Each rank renders its

@@ -377,6 +377,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.ord_r = a.ord_w = a.ctr_r = a.ctr_w = a.ctr_z = a.ord_q = 0;
   a.defer = nullptr;
   a.defer_e = a.defer_seg = 0;
+  a.exact_fat = 0;
   return a;
 }
 
@@ -448,6 +449,8 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
     a.defer = d;
     a.defer_e = uint32_t(slot->defer_epoch & 1u);
     a.defer_seg = uint32_t((a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * uint32_t(vrt::kWgThreads);
+    // bands of under 4 rounds: the exact pass's latency follows a short certified pass
+    a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
     slot->defer_epoch++;
     slot->last_defer = true;
     return;

@@ -56,6 +56,7 @@ struct KArgs {
   // words per segment (a segment holds at most ceil(tiles / 8) tiles' pixels)
   uint32_t* defer;
   uint32_t defer_e, defer_seg;
+  int32_t exact_fat;  // the exact pass's 4-wave instance (colour-only bands of < 4 rounds of waves)
 };
 
 // Waves per workgroup, each rendering an 8x8 pixel tile. Two (a 16x8 tile): a finished

@@ -2206,8 +2206,14 @@ __device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r)
 // Every deferred pixel is rendered exactly once, with the same exact path and epilogue as the
 // in-lane fallback, so images are identical. Workgroup 0 zeroes the other counter set for the
 // next launch on the stream (none of this launch's kernels reads it).
-template <bool TEX, int CERT>
-__global__ void __launch_bounds__(64, VRT_EXACT_WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
+// WAVES: resident waves per SIMD the instance is built for. 7 (72 VGPRs, ~1 KB of spills per lane)
+// for whole frames, where its waves share the CUs with the next frames' certified passes (fewer
+// cost 10-30 %, profiles/r03_s25); 4 (no spills: shorter exact walks) for colour-only bands of
+// under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
+// (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
+// slower, profiles/r03_s67)
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES>
+__global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t lane = lane_id();
   const uint32_t* ctr = a.defer;
@@ -2470,7 +2476,8 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
-    auto k2 = a.textured ? exact_pass_kernel<true, 1> : exact_pass_kernel<false, 2>;
+    auto k2 = a.textured ? exact_pass_kernel<true, 1>
+                         : (a.exact_fat ? exact_pass_kernel<false, 2, 4> : exact_pass_kernel<false, 2>);
     if (ev_begin)
       hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);
     else

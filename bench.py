@@ -105,9 +105,6 @@ def parse():
                     help="pixels the certified walks cannot settle rendered by a second, compacted "
                          "exact pass (vrt_set_exact_pass): 1 automatic (launches of >= 2 rounds of "
                          "resident waves), 2 always, 0 never (in their own lanes)")
-    ap.add_argument("--stagger", action="store_true",
-                    help="diagnostic: in the timed region, each lane's first frame waits for the "
-                         "previous lane's first frame (lanes out of phase)")
     ap.add_argument("--tile-order", type=int, default=1, choices=[0, 1],
                     help="heavy-first tile order of in-lane launches with glass (vrt_set_tile_order)")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
@@ -417,7 +414,6 @@ def main():
     if args.pre_idle_ms > 0:
         time.sleep(args.pre_idle_ms * 1e-3)
     if not tiler.gather:
-        tiler.stagger = args.stagger
         tiler.mark_idle()
     lane_st = (tiler.lane_streams() if not tiler.gather else []) or [stream]
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]

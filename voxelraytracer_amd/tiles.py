@@ -211,11 +211,6 @@ class FrameTiler:
                     row.append((row0, rows, step, o.data_ptr(), pv.data_ptr(), row_pitch(o),
                                 self.part_streams[g][q].cuda_stream))
                 self.plan.append(row)
-        # stagger (diagnostic): after the device was idle, lane g's first frame waits for lane g-1's
-        # first frame, so the lanes do not run in phase
-        self.stagger = False
-        self.stagger_ev = None
-        self.stagger_left = 0
         self.pending = [None, None]     # gather that still reads bands[b]
         self.assembled = [None, None]   # rank 0: assembly that still reads gathered[b]
         self.prev = None                # rank 0: buffer index of the frame awaiting assembly
@@ -278,13 +273,8 @@ class FrameTiler:
                     for st in ln:
                         st.wait_stream(cur)
                 self.fresh = False
-            if self.stagger_left > 0 and self.stagger_ev is not None:
-                self.part_streams[lane][0].wait_event(self.stagger_ev)
             for args in self.plan[lane]:
                 self.launch(*args, **self.block_kw)
-            if self.stagger_left > 0:
-                self.stagger_left -= 1
-                self.stagger_ev = self.part_streams[lane][0].record_event()
             return self.bufs[lane]
         if not self.gather:   # one rank, or ranks that keep their bands: no exchange
             lane = self.k % self.lanes
@@ -361,8 +351,6 @@ class FrameTiler:
         """Declare the device idle (the caller has just synchronised it): the next frame's streams
         need not wait for the current stream's work, so they start without cross-queue waits."""
         self.fresh = False
-        if self.stagger:
-            self.stagger_left, self.stagger_ev = self.lanes, None
 
     def lane_streams(self):
         """The HIP streams the frames are enqueued on (empty without part streams)."""

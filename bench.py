@@ -18,12 +18,15 @@ scripts/diag/strong_pipe.py). At u_Alpha != 1 frames depend on their history: on
 interleaved row parts on two streams, filtered in place (the round-2 scheme).
 
 Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
-cyclic row bands (rank r owns rows r, r+N, ...); every rank renders and filters its band in HBM.
-The per-pixel program has no exchange step, so the timed frames run with no collective; after the
-timed region rank 0 gathers the last frame's bands over RCCL once (collect()). --gather-frames
-gathers every frame to rank 0 inside the timed region instead (display delivery, one lane,
-pipelined so the gather of frame k overlaps the render of frame k+1). Default --scaling strong:
-the config's frame (C3: 1920x1080) is split N ways, the reference's one frame per draw
+block-cyclic bands of 16 rows (rank r owns row blocks r, r+N, ...); every rank renders and filters
+its band in HBM, and every timed frame is gathered to rank 0 over RCCL (xGMI) and assembled there
+(north_star's "RCCL gather of per-tile RGBA"; the reference displays every frame from one device,
+main.cpp:379-385): per frame, on the frame's lane stream, the render, the library's ncclGather
+(one communicator per lane, vrt_gather_band_async) and rank 0's assembly kernel
+(vrt_assemble_blocks_async), so the gathers of frames in flight overlap the renders of the others.
+The JSON's "render_only" object times the same frames without the gather (labelled; --no-gather
+makes that the timed path and gathers the last frame once instead). Default --scaling strong: the
+config's frame (C3: 1920x1080) is split N ways, the reference's one frame per draw
 (main.cpp:325-361) tiled across the GPUs; --scaling weak renders an N-fold taller frame of the same
 view instead (each rank a config-sized band; opt-in, no BASELINE config names that frame).
 
@@ -31,8 +34,10 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4
                        [--output rgba8|f32] [--alpha A] [--scaling strong|weak] [--lanes L]
 """
 import argparse
+import faulthandler
 import json
 import os
+import signal
 import sys
 import time
 
@@ -125,10 +130,14 @@ def parse():
                          "split frame of one part per lane, else 1 (cyclic rows)")
     ap.add_argument("--same-device", action="store_true",
                     help="test only: every rank on cuda:0 (rehearse N > 1 on a one-GPU box)")
-    ap.add_argument("--gather-frames", action="store_true",
-                    help="N > 1: gather every frame's bands to rank 0 over RCCL inside the timed "
-                         "region (display delivery); default: bands stay on their ranks, one "
-                         "gather after the timed region")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: keep the bands on their ranks in the timed frames (no per-frame "
+                         "gather; one gather of the last frame after the timed region); default: "
+                         "every frame gathered to rank 0 and assembled there inside the timed region")
+    ap.add_argument("--watchdog-s", type=float, default=0.0,
+                    help="dump every thread's Python stack to stderr after this many seconds if the "
+                         "run is still going (0: off; the two-rank GPU test sets it). SIGUSR1 dumps "
+                         "them at any time")
     ap.add_argument("--pre-idle-ms", type=float, default=0.0,
                     help="diagnostic: idle the synchronised device this long before the timed "
                          "region (clock-ramp experiments)")
@@ -233,14 +242,35 @@ def pipeline_shape(args, world: int):
     rows = -(-frame_h // split)
     waves = -(-w // 8) * -(-rows // 8)
     small = split > 1 and waves < WAVE_SLOTS
-    independent = args.alpha == 1.0 and not args.gather_frames
+    independent = args.alpha == 1.0
     lanes = args.lanes or ((8 if small else 4) if independent else 1)
     queues = args.queues or (8 if small and lanes == 8 else 4)
     return lanes, queues
 
 
+def share_ids(ids, count, dev):
+    """RCCL unique ids created on rank 0, broadcast to every rank over the job's process group."""
+    import torch
+    import torch.distributed as dist
+
+    from voxelraytracer_amd.abi import VRT_COMM_ID_BYTES
+
+    buf = torch.zeros(count * VRT_COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    if ids is not None:
+        buf.copy_(torch.frombuffer(bytearray(b"".join(ids)), dtype=torch.uint8))
+    dist.broadcast(buf, 0)
+    raw = bytes(buf.cpu().numpy())
+    return [raw[i * VRT_COMM_ID_BYTES:(i + 1) * VRT_COMM_ID_BYTES] for i in range(count)]
+
+
 def main():
     args = parse()
+    # a hung run (e.g. a collective that never completes) shows every thread's stack: on SIGUSR1
+    # (the two-rank test sends it before killing the job) and after --watchdog-s
+    faulthandler.enable()
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
+    if args.watchdog_s > 0:
+        faulthandler.dump_traceback_later(args.watchdog_s, exit=False)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     lanes, queues = pipeline_shape(args, world)
     if args.queues or queues != 4:   # before HIP initialises (the GPU box exports 4)
@@ -251,7 +281,7 @@ def main():
     import torch.distributed as dist
 
     import voxelraytracer_amd as vrt
-    from voxelraytracer_amd.tiles import FrameTiler, broadcast_volume, row_pitch
+    from voxelraytracer_amd.tiles import FrameTiler, GatherLib, broadcast_volume, row_pitch
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -328,14 +358,15 @@ def main():
             ren.render_rows_async(cam, kparams, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch,
                                   row_block=row_block)
 
-    if args.gather_frames and lanes > 1:
-        raise SystemExit("--gather-frames renders one frame at a time (--lanes 1)")
-    parts = args.parts or (1 if lanes > 1 else 2)
+    gather = world > 1 and not args.no_gather
+    parts = args.parts or (1 if lanes > 1 or gather else 2)
     parts = parts if frame_h % (max(world, args.rehearse_ranks) * parts) == 0 else 1
+    if gather and parts != 1:
+        raise SystemExit("gathered bands are one launch per frame (--parts 1)")
     # independent frames: at alpha 1 the kernel does not read the history (tiles.py)
     rehearse = args.rehearse_ranks if world == 1 and args.rehearse_ranks > 1 else 0
-    if rehearse and (args.gather_frames or args.scaling != "strong"):
-        raise SystemExit("--rehearse-ranks rehearses the strong split without per-frame gathers")
+    if rehearse and args.scaling != "strong":
+        raise SystemExit("--rehearse-ranks rehearses the strong split")
     if not 0 <= args.rehearse_rank < max(rehearse, 1):
         raise SystemExit("--rehearse-rank must be one of the rehearsed split's ranks")
     split = max(world, rehearse) > 1
@@ -343,13 +374,19 @@ def main():
     # 8x8 wave covers 8 adjacent frame rows, as in the whole frame, and a 16x8 workgroup's two
     # neighbours in the band are adjacent too (16 vs 8 rows: C4 k = 8 -3 %, C3 k = 4 -5 %, others
     # equal; profiles/r03_s54)
-    row_block = args.row_block or (16 if split and parts == 1 and not args.gather_frames else 1)
+    row_block = args.row_block or (16 if split and parts == 1 else 1)
+    exchange = None
+    if gather:   # the per-frame exchange: the library's RCCL path, or torch (gloo rehearsal)
+        from voxelraytracer_amd.tiles import GatherLib, GatherTorch
+
+        exchange = (GatherLib(ren, lanes, world, rank, lambda ids, n_: share_ids(ids, n_, dev))
+                    if args.backend == "nccl" else GatherTorch())
     tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None,
                        rank=args.rehearse_rank if rehearse else None,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
-                       gather=args.gather_frames, lanes=lanes,
+                       gather=gather, lanes=lanes,
                        independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs,
-                       row_block=row_block)
+                       row_block=row_block, exchange=exchange)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -408,38 +445,59 @@ def main():
     # Timed region: K frames. The device is idle here (synchronised above), so the lane streams
     # start without waiting on the main stream, and the closing device-wide synchronize waits for
     # every lane (no cross-queue joins inside the timed region: each costs a few us of queue
-    # latency at both ends of a 20-frame run; scripts/diag/drv_shape.sh). GPU time per frame:
-    # from the earliest lane start event to the latest lane end event.
-    # (--gather-frames keeps the joins: the last frame's gather and assembly are timed frames' work)
-    if args.pre_idle_ms > 0:
-        time.sleep(args.pre_idle_ms * 1e-3)
-    if not tiler.gather:
+    # latency at both ends of a 20-frame run; profiles/r03_s33). GPU time per frame: from the
+    # earliest lane start event to the latest lane end event. With the per-frame gather, each
+    # frame's gather and (rank 0) assembly are on its lane stream: inside both clocks.
+    lane_st = tiler.lane_streams() or [stream]
+
+    def timed_frames(steps, events=False):
+        """(wall seconds, GPU ms per frame, per-frame completion ms) of `steps` frames between a
+        synchronised barrier and a synchronize + barrier (max over ranks is taken by the caller)."""
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        if args.pre_idle_ms > 0:
+            time.sleep(args.pre_idle_ms * 1e-3)
         tiler.mark_idle()
-    lane_st = (tiler.lane_streams() if not tiler.gather else []) or [stream]
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
-    t0 = time.perf_counter()
-    for e, st in zip(ev0, lane_st):
-        e.record(st)
-    fev = []
-    for i_ in range(args.steps):
-        tiler.frame()
-        if args.frame_events and not tiler.gather:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(lane_st[(i_ % tiler.lanes) * len(tiler.specs) % len(lane_st)])
-            fev.append(e)
-    if tiler.gather:
-        tiler.finish()
-    for e, st in zip(ev1, lane_st):
-        e.record(st)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if not tiler.gather:
+        ev0 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
+        ev1 = [torch.cuda.Event(enable_timing=True) for _ in lane_st]
+        t0_ = time.perf_counter()
+        for e, st in zip(ev0, lane_st):
+            e.record(st)
+        fev_ = []
+        for i_ in range(steps):
+            tiler.frame()
+            if events:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(lane_st[(i_ % tiler.lanes) * len(tiler.specs) % len(lane_st)])
+                fev_.append(e)
+        for e, st in zip(ev1, lane_st):
+            e.record(st)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0_
         tiler.finish()   # host bookkeeping: every lane is already complete
-    frame_gpu_ms = max(a.elapsed_time(b) for a in ev0 for b in ev1) / args.steps
-    frame_events_ms = [round(min(a.elapsed_time(e) for a in ev0), 4) for e in fev] or None
+        gpu_ms = max(a.elapsed_time(b) for a in ev0 for b in ev1) / steps
+        return el, gpu_ms, [round(min(a.elapsed_time(e) for a in ev0), 4) for e in fev_] or None
+
+    elapsed, frame_gpu_ms, frame_events_ms = timed_frames(args.steps, args.frame_events)
+    # The same frames without the per-frame gather (labelled "render_only"): what the split alone
+    # sustains, beside the timed gathered frames above
+    render_only = None
+    if tiler.gather:
+        tiler.exchange_on = False
+        ro_el, ro_gpu, _ = timed_frames(args.steps)
+        tiler.exchange_on = True
+        t_ro = torch.tensor([ro_el, ro_gpu], dtype=torch.float64, device=dev)
+        dist.all_reduce(t_ro, op=dist.ReduceOp.MAX)
+        ro_el, ro_gpu = t_ro.tolist()
+        render_only = {"value": round(rays_per_frame * args.steps / ro_el / 1e6, 3),
+                       "ms_per_step": round(ro_el / args.steps * 1e3, 4),
+                       "kernel_ms_max_over_ranks": round(ro_gpu, 4),
+                       "what": "the same timed frames with the per-frame gather and assembly off "
+                               "(bands kept on their ranks); not the headline value"}
     # Launch-timing pass (after the timed region, the same FrameTiler path): the mean duration of
     # one render_kernel launch — what rocprofv3 reports per kernel — from the kernels' own device
     # start / end timestamps (vrt_set_launch_timing: hipExtLaunchKernelGGL events; launches of
@@ -458,29 +516,66 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, frame_ms_max = t.tolist()
 
+    # Single-frame latency (after the timed region): one frame alone on the device — its lane's
+    # launches (certified pass + deferred exact pass; with the per-frame gather also the gather
+    # and rank 0's assembly) between device events on that lane, ranks aligned by a barrier —
+    # what the reference's blocking GL_TIME_ELAPSED query around its one draw measures
+    # (main.cpp:350-356); median of 15. And the drop-in's synchronous call (vrt_render_frame:
+    # in-lane exact path, two parts) on one GPU: its kernel_ms (device timestamps).
+    lat = []
+    for _ in range(15):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        st_ = tiler.next_stream()
+        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ea.record(st_)
+        tiler.frame()
+        eb.record(st_)
+        torch.cuda.synchronize(dev)
+        lat.append(ea.elapsed_time(eb))
+    tiler.finish()
+    lat_t = torch.tensor([float(np.median(lat))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
+    latency = {"frame_latency_ms": round(float(np.median(lat)), 4),
+               "frame_latency_ms_max_over_ranks": round(lat_t.item(), 4),
+               "what": "one frame alone through the timed path (its lane's launches"
+                       + (", gather and rank 0's assembly" if tiler.gather else "")
+                       + ", device events), median of 15"}
+    if world == 1 and not rehearse and rgba8:
+        sync_ms = []
+        for _ in range(9):
+            _, st_d = ren.render_frame(cam, kparams, args.alpha)
+            sync_ms.append(st_d["kernel_ms"])
+        latency["sync_frame_kernel_ms"] = round(float(np.median(sync_ms)), 4)
+        latency["sync_frame_is"] = ("vrt_render_frame (the drop-in's synchronous call: two "
+                                    "interleaved parts, exact path in lane), device timestamps of "
+                                    "its launches, median of 9 (the host copy excluded)")
+
     # Check of the timed path (after all timing): the next `verify_frames` frames through the same
     # FrameTiler (lanes and parts on their streams, tile order seeded by the frames before
     # them, certified walks), each against the exact STATS instance (exact walks, counters on)
     # rendering the same rows from a copy of the same history: the stored bytes (or float frame)
     # must be equal. Single rank: the frames and their histories are kept for the oracle check.
+    # With the per-frame gather, rank 0's assembled frame is also compared with an independent
+    # assembly of the ranks' bands (torch.distributed gather + index placement, tiles.collect).
     verify = None
     pairs = []   # (history before, frame after) of each verified frame, host copies
 
     def last_parts():   # this rank's part buffers of the last frame enqueued
-        if tiler.gather:
-            band = tiler.bands[(tiler.k - 1) % 2]
-            return [band[s_] for s_ in range(parts)]
         return [tiler.part_rows(tiler.last(), s_) for s_ in range(parts)]
 
     if not args.no_verify:
         bad = 0
         total = 0
         vc = torch.zeros_like(cnt)
+        gather_bad = None
         for _ in range(max(1, args.verify_frames)):
             tiler.finish()
             prev_parts = [t_.clone() for t_ in last_parts()]   # the next frame's history
-            prev_full = tiler.last().clone() if world == 1 and not tiler.gather else None
-            tiler.frame()
+            prev_full = tiler.last().clone() if world == 1 else None
+            got_frame = tiler.frame()
             tiler.finish()
             torch.cuda.synchronize(dev)
             for s_, (row0, rows, step) in enumerate(tiler.specs):
@@ -491,21 +586,28 @@ def main():
                 torch.cuda.synchronize(dev)
                 bad += int((got != ref).sum().item())
                 total += got.numel()
+            if tiler.gather:
+                full = tiler.collect()
+                torch.cuda.synchronize(dev)
+                if rank == 0:
+                    gather_bad = (gather_bad or 0) + int((full != got_frame).sum().item())
             if prev_full is not None:
                 pairs.append((prev_full.cpu().numpy(), tiler.last().cpu().numpy()))
         verify = {"verified": bad == 0, "frames": max(1, args.verify_frames),
                   "mismatched_elements": bad, "elements": total,
                   "against": "exact walks (STATS instance, counters on) on a copy of the same "
                              "history, every part of this rank"}
-        ok = torch.tensor([1 if bad == 0 else 0], device=dev)
+        if gather_bad is not None:
+            verify["gathered_frame_mismatched_elements"] = gather_bad
+        ok = torch.tensor([1 if bad == 0 and not gather_bad else 0], device=dev)
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         verify["verified_all_ranks"] = bool(ok.item())
 
-    # Bands that stayed on their ranks: one RCCL gather of the last frame to rank 0 (after all
-    # timing), the delivery a display of the whole frame would do
+    # Bands that stayed on their ranks (--no-gather): one RCCL gather of the last frame to rank 0
+    # (after all timing), the delivery a display of the whole frame would do
     collect = None
-    if world > 1 and not args.gather_frames:
+    if world > 1 and not tiler.gather:
         tiler.finish()
         torch.cuda.synchronize(dev)
         t_c = time.perf_counter()
@@ -519,9 +621,21 @@ def main():
 
     band_kind = (f"block-cyclic bands of {row_block}-row blocks" if row_block > 1 else
                  "cyclic row bands")
+    gather_how = ("RCCL ncclGather over xGMI, one communicator per lane, library assembly kernel"
+                  if isinstance(tiler.exchange, GatherLib) else "torch.distributed gather, "
+                  f"{args.backend} backend") if tiler.gather else None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
+        rehearsal = None
+        if rehearse:   # one band of a K-way split: value counts that band's own rays only
+            own_rays = vrt.total_rays(own)
+            rehearsal = {"ranks": rehearse, "rank": args.rehearse_rank, "band_rays_per_frame": own_rays,
+                         "whole_frame_equivalent_value": round(value, 3),
+                         "whole_frame_equivalent_is": ("the whole frame's rays per rehearsed band time: "
+                                                       "what a K-GPU run reports if every rank is as "
+                                                       "fast as this one")}
+            value = own_rays * args.steps / elapsed / 1e6
         # Roofline of the dominant kernel (render_kernel). Algorithmic bytes are the reference's:
         # 1 B per DDA step of its walk + 2 B per refraction probe + the pixel bytes;
         # the certified walks read only a few texels per pixel, so this is a reference-normalised
@@ -620,10 +734,13 @@ def main():
                             if args.shading == "textured" else "colour-only"),
                 "output": ("RGB8 ray-trace store + temporal filter (alpha %g) fused, RGBA8 words"
                            % args.alpha) if rgba8 else "float RGBA",
-                "parallelism": ((f"cyclic row bands x{world} + RCCL gather to rank 0 every frame"
-                                 if args.gather_frames else
+                "parallelism": ((f"{band_kind} x{world} ({args.scaling} scaling) + every frame "
+                                 f"gathered to rank 0 ({gather_how}) and assembled there, inside "
+                                 "the timed region"
+                                 if tiler.gather else
                                  f"{band_kind} x{world} ({args.scaling} scaling), no collective "
-                                 "in the timed region (one RCCL gather of the last frame after it)")
+                                 "in the timed region (--no-gather: one gather of the last frame "
+                                 "after it)")
                                 if world > 1 else
                                 (f"REHEARSAL on one GPU: only rank {args.rehearse_rank}'s band "
                                  f"({band_kind}) of a {rehearse}-way strong split is rendered and "
@@ -679,6 +796,14 @@ def main():
                 "lib_sha256": lib_hash[:16],
                 "profile": prof_note,
             },
+            "rehearsal": rehearsal,
+            "gather": (None if world == 1 else
+                       {"per_frame": tiler.gather, "how": gather_how,
+                        "band_rows_padded": getattr(tiler, "rmax", None),
+                        "bytes_to_rank0_per_frame": (tiler.rmax * w * (4 if rgba8 else 16) * (world - 1)
+                                                     if tiler.gather else None),
+                        "render_only": render_only}),
+            "latency": latency,
             "device_warmup": device_warmup,
             "frame_events_ms": frame_events_ms,
             "verify": verify,

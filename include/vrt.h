@@ -15,12 +15,13 @@
  *   - Volumes are N^3 bytes, x fastest: idx = x + y*N + z*N*N   (main.cpp:227).
  *   - Images are W*H RGBA float, row 0 = bottom row (GL window convention).
  *   - A context spans one or more GPUs (vrt_create's device mask). Whole-frame entry points
- *     (vrt_render, vrt_render_frame, vrt_render_frame_device) split the frame into cyclic row
- *     bands, one per device, rendered on context-owned streams: frame f on lane f % 4. A frame
- *     that runs alone (synchronous calls) or reads its history is two interleaved row parts on
- *     two streams; a device-output frame at u_Alpha = 1 is one launch per band, and up to four
- *     of them are in flight (ABI v9). The *_async band entry points run on the context's first
- *     (root) device.
+ *     (vrt_render, vrt_render_frame, vrt_render_frame_device) split the frame over k > 1 devices
+ *     into block-cyclic bands of 16 adjacent rows (ABI v12; device j renders row blocks j, j+k,
+ *     ..., one launch per band; vrt_frame_row_block), rendered on context-owned streams: frame f
+ *     on lane f % 4. On one device a frame that runs alone (synchronous calls) or reads its
+ *     history is two interleaved row parts on two streams; a device-output frame at u_Alpha = 1
+ *     is one launch, and up to four frames are in flight (ABI v9). The *_async band entry points
+ *     run on the context's first (root) device.
  */
 #ifndef VRT_H
 #define VRT_H
@@ -31,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 11
+#define VRT_ABI_VERSION 12
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -120,9 +121,10 @@ typedef struct {
 /* ---- context / device ---------------------------------------------------------------------- */
 
 /* Create a context on the HIP devices of `device_mask` (bit i = device ordinal i):
- * one device renders whole frames; k devices split every whole frame into k cyclic row bands
- * (device j of the mask renders rows j, j+k, ...; the volume is replicated on every device:
- * RCCL broadcast from the first device, RCCL communicators over the mask's devices). */
+ * one device renders whole frames; k devices split every whole frame into k block-cyclic bands
+ * (ABI v12: device j of the mask renders the 16-row blocks j, j+k, ...; until v11 cyclic rows j,
+ * j+k, ...; the volume is replicated on every device: RCCL broadcast from the first device, RCCL
+ * communicators over the mask's devices). */
 int vrt_create(uint32_t device_mask, vrt_ctx** out);
 /* Same over an explicit device list; a device may repeat (rehearses a k-device split on fewer
  * GPUs: the bands and the gather then use device-to-device copies instead of RCCL). */
@@ -411,6 +413,49 @@ int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out);
  * pitch, row bytes, rows} of one 2-D copy (hipMemcpy2D). Host arithmetic, no GPU; returns k.
  * Exported for tests (unequal bands when height % k != 0). */
 int vrt_band_copy_plan(int32_t width, int32_t height, int32_t k, int32_t elem_bytes, int64_t* out);
+
+/* ABI v12: rows per block of the bands the whole-frame entry points split a frame into over k
+ * devices: 1 for k = 1 (the whole frame), 16 for k > 1 (block-cyclic bands). */
+int vrt_frame_row_block(int32_t k);
+
+/* ABI v12: the block-cyclic band of every device j < k for blocks of row_block rows (a power of
+ * two <= 64): out[j*3 + 0..2] = {row0, rows, row_step}, band row i = frame row
+ * row0 + (i / row_block) * row_step + i % row_block (the *_blocks_pitched_async arguments; k = 1:
+ * the whole frame). Returns the largest band's rows. Host arithmetic, no GPU. */
+int vrt_block_band_plan(int32_t height, int32_t k, int32_t row_block, int32_t* out);
+
+/* ABI v12: the 2-D copies that assemble a frame from k packed block-cyclic band buffers (what
+ * vrt_render / vrt_render_frame stage with over k > 1 devices when row_block is
+ * vrt_frame_row_block(k)): per band two entries, out[(j*2 + c)*7 + 0..6] = {band j, destination
+ * byte offset, destination pitch, source byte offset, source pitch, width bytes, rows} (the band's
+ * full blocks, then a short last block; rows = 0 when absent). Returns the number of copies. */
+int vrt_block_copy_plan(int32_t width, int32_t height, int32_t k, int32_t row_block, int32_t elem_bytes,
+                        int64_t* out);
+
+/* ---- one process per GPU (ABI v12) ------------------------------------------------------------
+ * A job of nranks processes, one GPU each (torchrun), each rendering its block-cyclic band of
+ * every frame into its own buffers, gathers the bands to rank 0 over RCCL (xGMI) and assembles the
+ * frame there — the drop-in's ncclGather path with the ranks in separate processes. */
+#define VRT_COMM_ID_BYTES 128
+/* A new RCCL unique id (ncclGetUniqueId) into out (>= VRT_COMM_ID_BYTES bytes; rank 0 creates the
+ * ids and the job distributes them). Returns VRT_COMM_ID_BYTES. */
+int vrt_comm_unique_id(uint8_t* out, int32_t bytes);
+/* Join `count` communicators (ids: count x VRT_COMM_ID_BYTES) as `rank` of `nranks` on the
+ * context's device (one-device contexts). Blocks until every rank has joined each one, in order.
+ * One communicator per lane of frames in flight: a communicator's operations run in issue order,
+ * separate ones do not order each other. */
+int vrt_comm_join(vrt_ctx* ctx, const uint8_t* ids, int32_t count, int32_t nranks, int32_t rank);
+/* ncclGather of `bytes` from d_band on every rank to rank 0's d_gathered (nranks x bytes, rank
+ * order; ignored elsewhere) over communicator `comm`, enqueued on hip_stream. */
+int vrt_gather_band_async(vrt_ctx* ctx, int32_t comm, const void* d_band, uint64_t bytes, void* d_gathered,
+                          void* hip_stream);
+/* The frame (height rows of width RGBA8 words, rows frame_pitch words apart) from k gathered
+ * block-cyclic bands of row_block rows (band j at d_bands + j * band_rows_cap * width words, band
+ * row i = frame row ((i / row_block) * k + j) * row_block + i % row_block): one HIP kernel, one
+ * workgroup per frame row, on hip_stream. */
+int vrt_assemble_blocks_async(vrt_ctx* ctx, const uint32_t* d_bands, int32_t k, int32_t band_rows_cap,
+                              int32_t width, int32_t height, int32_t row_block, uint32_t* d_frame,
+                              int64_t frame_pitch, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,7 @@
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
 # steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
-#        sq[:CFG] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
+#        sq[:CFG] | waits[:CFG] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -43,6 +43,7 @@ for st in "$@"; do
       done; unset VRT_LIB ;;
     write) pmc write ${arg:-C3} WRITE_SIZE ;;
     fetch) pmc fetch ${arg:-C3} FETCH_SIZE ;;
+    waits) pmc waits ${arg:-C3} SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM ;;
     sq) pmc sq ${arg:-C3} SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD ;;
     trace) run trace_${arg:-C3} 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${arg:-C3}" -o run --output-format csv -- \
              python3 "$ROOT/bench.py" --config ${arg:-C3} --steps 20 --warmup 3 --cpu-seconds 0 ;;

@@ -44,7 +44,7 @@ def test_struct_layouts():
 
 
 def test_abi_version(built):
-    assert vrt.lib().vrt_abi_version() == 11
+    assert vrt.lib().vrt_abi_version() == 12
 
 
 @pytest.mark.parametrize("scene", [0, 1, 2])
@@ -164,6 +164,82 @@ def test_band_copy_plan_assembles_unequal_bands(built, width, height, k, elem):
     for fr in range(height):
         j = fr % k
         assert np.all(frame[fr * row:(fr + 1) * row] == (fr * 7 + j + 1) & 0xFF)
+
+
+@pytest.mark.parametrize("height,k,block", [(1080, 2, 16), (1080, 8, 16), (2160, 8, 16), (1081, 3, 16),
+                                            (7, 3, 4), (5, 8, 16), (100, 1, 16), (4000, 7, 64)])
+def test_block_band_plan_covers_every_row_once(built, height, k, block):
+    """vrt_block_band_plan (ABI v12: the whole-frame split over k > 1 devices): every frame row is
+    rendered by exactly one band, band row i = frame row row0 + (i // B) * step + i % B, the
+    largest band is band 0's, and the plan equals tiles.block_band_spec (bench.py's split)."""
+    from voxelraytracer_amd.tiles import block_band_spec
+
+    plan, cap = vrt.block_band_plan(height, k, block)
+    seen = np.zeros(height, np.int32)
+    for j, (row0, rows, step) in enumerate(plan):
+        assert (row0, rows, step) == block_band_spec(j, k, height, block)
+        assert rows <= cap
+        for i in range(rows):
+            seen[row0 + (i // block) * step + i % block] += 1
+    assert np.all(seen == 1)
+    assert cap == max(r for _, r, _ in plan)
+
+
+def test_frame_row_block(built):
+    assert vrt.frame_row_block(1) == 1 and vrt.frame_row_block(2) == 16 and vrt.frame_row_block(8) == 16
+
+
+@pytest.mark.parametrize("width,height,k,block,elem", [(40, 27, 4, 4, 4), (1920, 1081, 8, 16, 4),
+                                                       (33, 7, 3, 2, 16), (5, 5, 8, 16, 16),
+                                                       (64, 1080, 7, 16, 16), (3, 1, 1, 16, 4),
+                                                       (3840, 2160, 8, 16, 4)])
+def test_block_copy_plan_assembles_unequal_bands(built, width, height, k, block, elem):
+    """The copies the library issues to assemble a multi-device frame from block-cyclic bands
+    (ABI v12: staging of vrt_render / vrt_render_frame, the repeated-device gather): every frame
+    byte written once, from the band row that renders it, with hipMemcpy2D's semantics."""
+    plan, cap = vrt.block_band_plan(height, k, block)
+    copies = vrt.block_copy_plan(width, height, k, block, elem)
+    row = width * elem
+    frame = np.zeros(height * row, np.uint8)
+    written = np.zeros(height * row, np.int32)
+    bands = []
+    for j, (row0, rows, step) in enumerate(plan):
+        band = np.zeros(max(cap, 1) * row, np.uint8)
+        for i in range(rows):   # band row i holds a pattern naming its frame row
+            fr = row0 + (i // block) * step + i % block
+            band[i * row:(i + 1) * row] = (fr * 7 + 3) & 0xFF
+        bands.append(band)
+    for j, dst_off, dst_pitch, src_off, src_pitch, wbytes, rows in copies:
+        _memcpy2d(frame, dst_off, dst_pitch, bands[j][src_off:], src_pitch, wbytes, rows)
+        ones = np.zeros_like(written)
+        _memcpy2d(ones, dst_off, dst_pitch, np.ones(bands[j].size - src_off, np.int32), src_pitch, wbytes, rows)
+        written += ones
+    assert np.all(written == 1)
+    for fr in range(height):
+        assert np.all(frame[fr * row:(fr + 1) * row] == (fr * 7 + 3) & 0xFF)
+
+
+def test_block_bands_compose_the_oracle_frame(built):
+    """The library's k-device split (block-cyclic bands, one launch per band) with the oracle as the
+    band renderer and the library's copy plan as the assembly reproduces the whole frame."""
+    n, w, h, k = 16, 40, 53, 3
+    block = vrt.frame_row_block(k)
+    vox = vrt.build_scene("refraction", n)
+    cam = vrt.make_camera(w, h)
+    p = vrt.default_params(4, 4)
+    full, _, _ = oracle.render(cam, vox, n, p)
+    plan, cap = vrt.block_band_plan(h, k, block)
+    bands = []
+    for row0, rows, step in plan:
+        b = np.full((cap, w, 4), np.nan, np.float32)
+        for i in range(rows):
+            fr = row0 + (i // block) * step + i % block
+            b[i] = oracle.render(cam, vox, n, p, row0=fr, rows=1)[0][0]
+        bands.append(b.reshape(-1).view(np.uint8))
+    frame = np.zeros(h * w * 16, np.uint8)
+    for j, dst_off, dst_pitch, src_off, src_pitch, wbytes, rows in vrt.block_copy_plan(w, h, k, block, 16):
+        _memcpy2d(frame, dst_off, dst_pitch, bands[j][src_off:], src_pitch, wbytes, rows)
+    assert np.array_equal(frame.view(np.uint32), full.reshape(-1).view(np.uint8).view(np.uint32))
 
 
 def test_headless_app_builds_and_parses(built):

@@ -1,14 +1,17 @@
 """Rehearsal of bench.py's multi-rank path on a one-GPU box: torch.distributed.run with two ranks
 sharing cuda:0 over gloo (RCCL needs one GPU per rank; the driver's 8-GPU run uses it). Checks the
-JSON contract of rank 0's line for N = 2, weak scaling (the frame is 2 x 1080 rows), the bands
-kept on their ranks with one gather after the timed region (the default) or the per-frame gather of
-RGBA8 parts (--gather-frames), and the max-over-ranks timing — the code path the scaling runs take."""
+JSON contract of rank 0's line for N = 2, strong and weak scaling (weak: the frame is 2 x 1080
+rows), the per-frame gather of RGBA8 block-cyclic bands to rank 0 with frames in flight (the
+default; over gloo here, the library's RCCL path in the driver's runs) or the bands kept on their
+ranks with one gather after the timed region (--no-gather), and the max-over-ranks timing — the
+code path the scaling runs take. A hang fails the test with every rank's Python stacks."""
 import json
 import os
 import signal
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -25,37 +28,37 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("scaling,gather", [("weak", False), ("strong", False), ("weak", True)])
+@pytest.mark.parametrize("scaling,gather", [("weak", False), ("strong", False), ("weak", True),
+                                            ("strong", True)])
 def test_bench_two_ranks_json(built, scaling, gather):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
-           "--backend", "gloo", "--same-device", "--scaling", scaling, "--cpu-seconds", "0"]
-    cmd += ["--gather-frames"] if gather else []
+           "--backend", "gloo", "--same-device", "--scaling", scaling, "--cpu-seconds", "0",
+           "--watchdog-s", "100"]
+    cmd += [] if gather else ["--no-gather"]
     env = dict(os.environ, OMP_NUM_THREADS="4")
-    # own process group: a hung run is killed with its torchrun workers
+    # own process group: a hung run is killed with its torchrun workers, after SIGUSR1 has made
+    # every rank dump all its threads' Python stacks (bench.py registers faulthandler for it; the
+    # ranks' --watchdog-s dump comes first) into the failure message
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT,
                          env=env, start_new_session=True)
     try:
         out_s, err_s = p.communicate(timeout=150)
-        r = subprocess.CompletedProcess(cmd, p.returncode, out_s, err_s)
     except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGUSR1)
+        time.sleep(3)
         os.killpg(p.pid, signal.SIGKILL)
-        p.communicate()
-        if gather:
-            # Two late round-3 runs (profiles/r03_s74) hung in this variant (per-frame gloo gathers
-            # of CUDA tensors between two processes on one GPU) where three earlier runs of the same
-            # code passed; the driver's N > 1 runs use RCCL and no per-frame gather. Reported, not
-            # hidden: the case is marked xfail instead of blocking the rest of the GPU suite.
-            pytest.xfail("two-rank gloo per-frame gather on one GPU did not finish in 150 s")
-        raise
+        out_s, err_s = p.communicate()
+        pytest.fail("two-rank bench did not finish in 150 s; rank stacks:\n" + err_s[-20000:])
+    r = subprocess.CompletedProcess(cmd, p.returncode, out_s, err_s)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout          # rank 0 prints exactly one JSON line
     out = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
-              "cpu_baseline"):
+              "cpu_baseline", "latency", "gather"):
         assert k in out, k
     assert out["n_gpus"] == 2 and out["steps"] == 6 and out["scaling"] == scaling
     assert out["value"] > 0 and out["ms_per_step"] > 0
@@ -63,8 +66,12 @@ def test_bench_two_ranks_json(built, scaling, gather):
     assert out["roofline"]["kernel_ms_max_over_ranks"] >= out["roofline"]["kernel_ms"]
     assert out["cpu_baseline"] is None        # rank 0 at N=1 only
     assert out["verified"] is True
-    if gather:
+    assert out["latency"]["frame_latency_ms"] > 0
+    rows = 2160 if scaling == "weak" else 1080
+    if gather:   # every timed frame gathered and assembled on rank 0, checked against collect()
         assert out["collect"] is None and "every frame" in out["config"]["parallelism"]
+        assert out["gather"]["per_frame"] is True and out["gather"]["render_only"]["value"] > 0
+        assert out["verify"]["gathered_frame_mismatched_elements"] == 0
+        assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * 4
     else:   # one gather of the last frame after the timed region
-        rows = 2160 if scaling == "weak" else 1080
         assert out["collect"]["rows"] == rows and out["collect"]["bytes"] == rows * 1920 * 4

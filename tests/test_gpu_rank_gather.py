@@ -1,0 +1,68 @@
+"""The library's one-process-per-GPU exchange (ABI v12) on the one-GPU box: RCCL communicators
+joined from unique ids (vrt_comm_unique_id / vrt_comm_join, a one-rank job here), ncclGather of a
+band through vrt_gather_band_async, and the assembly kernel (vrt_assemble_blocks_async) that
+re-interleaves k gathered block-cyclic bands into the frame — checked byte for byte against the
+band placement of tiles.band_frame_rows. Also tiles.GatherLib, the exchange bench.py's nccl runs
+use, through a one-rank job. Between distinct GPUs the gather runs only in the driver's runs."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def reference_frame(bands: torch.Tensor, k: int, height: int, block: int) -> torch.Tensor:
+    from voxelraytracer_amd.tiles import band_frame_rows, block_band_spec
+
+    frame = torch.zeros((height,) + tuple(bands.shape[2:]), dtype=bands.dtype)
+    for j in range(k):
+        row0, rows, step = block_band_spec(j, k, height, block)
+        frame[band_frame_rows(row0, rows, step, block)] = bands[j, :rows].cpu()
+    return frame
+
+
+@pytest.mark.parametrize("k,width,height,block", [(3, 40, 53, 16), (8, 1920, 1080, 16), (8, 3840, 2160, 16),
+                                                  (2, 37, 9, 1), (5, 64, 100, 4)])
+def test_assemble_blocks_matches_band_placement(built, k, width, height, block):
+    import voxelraytracer_amd as vrt
+
+    plan, cap = vrt.block_band_plan(height, k, block)
+    g = torch.Generator().manual_seed(k * 1000 + width)
+    bands = torch.randint(0, 256, (k, cap, width, 4), dtype=torch.uint8, generator=g).cuda()
+    frame = torch.full((height, width, 4), 7, dtype=torch.uint8, device="cuda")
+    with vrt.Renderer(0) as ren:
+        st = torch.cuda.current_stream().cuda_stream
+        ren.assemble_blocks_async(bands.data_ptr(), k, cap, width, height, block, frame.data_ptr(), width, st)
+        torch.cuda.synchronize()
+        with pytest.raises(vrt.VrtError):   # a band slice too small for the largest band
+            ren.assemble_blocks_async(bands.data_ptr(), k, cap - 1, width, height, block, frame.data_ptr(),
+                                      width, st)
+    assert torch.equal(frame.cpu(), reference_frame(bands, k, height, block))
+
+
+def test_rank_comm_gather_one_rank(built):
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import GatherLib
+
+    w, h, block, lanes = 96, 40, 16, 2
+    with vrt.Renderer(0) as ren:
+        ex = GatherLib(ren, lanes, 1, 0, lambda ids, n: ids)   # a one-rank job: the ids stay here
+        st = [torch.cuda.Stream() for _ in range(lanes)]
+        bufs = [torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)]
+        tiler = types.SimpleNamespace(
+            width=w, height=h, channels=4, dtype=torch.uint8, world=1, rank=0, rmax=h, row_block=block,
+            lanes=lanes, bufs=bufs, part_streams=[[s] for s in st],
+            gathered=[torch.zeros((1, h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)],
+            frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)])
+        for lane in range(lanes):
+            ex.run(tiler, lane)
+        torch.cuda.synchronize()
+        for lane in range(lanes):
+            assert torch.equal(tiler.gathered[lane][0], bufs[lane])      # ncclGather of one rank
+            assert torch.equal(tiler.frames[lane][:h], bufs[lane])       # assembly of one band
+        with pytest.raises(vrt.VrtError):
+            ren.gather_band_async(lanes, bufs[0].data_ptr(), bufs[0].numel(), 0, 0)  # no such comm
+        with pytest.raises(vrt.VrtError):   # joined once per context
+            ren.comm_join([vrt.comm_unique_id()], 1, 0)

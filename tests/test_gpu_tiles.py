@@ -1,8 +1,9 @@
 """FrameTiler on the GPU with the real HIP kernel: two ranks (processes) sharing cuda:0 over the
 gloo backend with CUDA tensors (RCCL needs one GPU per rank; the driver's 8-GPU run uses it).
-Exercises the CUDA-only parts of the multi-GPU path — uint8 RGBA8 bands, the temporal history
-carried in the previous band buffer, rank 0's side-stream re-interleave — and checks the
-assembled frames against a single-process render of the same frames, bit for bit."""
+Exercises the CUDA-only parts of the multi-GPU path — uint8 RGBA8 block-cyclic bands, the
+temporal history carried in the previous lane's band buffer, the per-frame gather and rank 0's
+re-interleave on the frame's lane stream — and checks the assembled frames against a
+single-process render of the same frames, bit for bit."""
 import os
 import socket
 
@@ -30,7 +31,7 @@ def frame_params(vrt, t):
     return vrt.default_params(4, 2, time=float(t + 1), ray_noise=0.03)
 
 
-def worker(rank, world, port, q, parts):
+def worker(rank, world, port, q, lanes, row_block):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -48,14 +49,14 @@ def worker(rank, world, port, q, parts):
     cam = vrt.make_camera(W, H)
     state = {"t": 0}
 
-    def render_band(row0, rows, step, out, prev):
-        ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"] // parts), ALPHA, row0,
+    def render_band(row0, rows, step, out, prev, row_block=1):
+        ren.render_temporal_rows_async(cam, frame_params(vrt, state["t"]), ALPHA, row0,
                                        rows, step, prev.data_ptr(), out.data_ptr(),
                                        stream=torch.cuda.current_stream().cuda_stream,
-                                       pitch=row_pitch(out))
+                                       pitch=row_pitch(out), row_block=row_block)
         state["t"] += 1
 
-    tiler = FrameTiler(W, H, render_band, dev, dtype=torch.uint8, parts=parts)
+    tiler = FrameTiler(W, H, render_band, dev, dtype=torch.uint8, lanes=lanes, row_block=row_block)
     got = []
     for _ in range(FRAMES):
         f = tiler.frame()
@@ -65,7 +66,7 @@ def worker(rank, world, port, q, parts):
     f = tiler.finish()
     torch.cuda.synchronize()
     if f is not None:
-        got.append(f.cpu().numpy())
+        assert np.array_equal(f.cpu().numpy(), got[-1])
     if rank == 0:
         q.put(got)
     dist.barrier()
@@ -73,14 +74,14 @@ def worker(rank, world, port, q, parts):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("parts", [1, 2])
-def test_two_ranks_on_one_gpu_match_single_process(built, parts):
+@pytest.mark.parametrize("lanes,row_block", [(1, 1), (3, 16), (2, 8)])
+def test_two_ranks_on_one_gpu_match_single_process(built, lanes, row_block):
     import voxelraytracer_amd as vrt
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, q, parts)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, 2, port, q, lanes, row_block)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)

@@ -63,7 +63,8 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
     got = []
     for _ in range(frames):
         f = tiler.frame()
-        if gather:
+        if gather:   # rank 0: the frame just rendered, gathered and assembled
+            assert (f is not None) == (rank == 0)
             if f is not None:
                 got.append(f.clone().numpy())
         else:   # bands stay on their ranks; gather each frame here only to check it
@@ -72,16 +73,19 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
             if rank == 0:
                 got.append(full.clone().numpy())
     f = tiler.finish()
-    if gather and f is not None:
-        got.append(f.clone().numpy())
+    if gather and rank == 0:
+        assert np.array_equal(f.numpy(), got[-1])
     if rank == 0:
         q.put((got, bytes(vox_np)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,parts", [(2, 1), (3, 1), (2, 3)])
-def test_tiled_frames_match_single_process(built, world, parts):
+@pytest.mark.parametrize("world,lanes,row_block", [(2, 1, 1), (3, 1, 1), (2, 3, 1), (3, 2, 4), (2, 4, 8)])
+def test_tiled_frames_match_single_process(built, world, lanes, row_block):
+    """The per-frame gather (bench.py's multi-rank default): cyclic or block-cyclic bands (ragged:
+    18 rows over 3 ranks in blocks of 4), frames in flight on several lanes; rank 0's assembled
+    frames equal single-process oracle frames bit for bit."""
     import oracle
     import voxelraytracer_amd as vrt
 
@@ -90,7 +94,7 @@ def test_tiled_frames_match_single_process(built, world, parts):
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "f32", 0.5,
-                                              parts)) for r in range(world)]
+                                              1, True, lanes, row_block)) for r in range(world)]
     for p in procs:
         p.start()
     got, vox_bytes = q.get(timeout=120)
@@ -118,10 +122,11 @@ def test_band_spec_and_assembly():
     assert torch.equal(assemble_cyclic(bands), frame)
 
 
-@pytest.mark.parametrize("parts", [1, 2])
-def test_tiled_temporal_rgba8_frames(built, parts):
-    """RGBA8 bands with the temporal filter: each rank's history is its own band of the previous
-    frame, so the assembled sequence equals the single-process filtered sequence bit for bit."""
+@pytest.mark.parametrize("lanes,row_block", [(1, 1), (2, 4), (3, 2)])
+def test_tiled_temporal_rgba8_frames(built, lanes, row_block):
+    """RGBA8 bands with the temporal filter, gathered every frame (dependent lanes at alpha 0.5):
+    each rank's history is its own band of the previous frame, so the assembled sequence equals
+    the single-process filtered sequence bit for bit."""
     import oracle
     import voxelraytracer_amd as vrt
 
@@ -130,7 +135,7 @@ def test_tiled_temporal_rgba8_frames(built, parts):
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, "rgba8", alpha,
-                                              parts)) for r in range(world)]
+                                              1, True, lanes, row_block)) for r in range(world)]
     for p in procs:
         p.start()
     got, _ = q.get(timeout=120)

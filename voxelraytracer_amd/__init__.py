@@ -180,6 +180,42 @@ def band_copy_plan(width: int, height: int, k: int, elem_bytes: int):
     return [tuple(int(v) for v in row) for row in out.reshape(k, 5)]
 
 
+def frame_row_block(k: int) -> int:
+    """Rows per block of the bands the whole-frame entry points split a frame into over k devices
+    (vrt_frame_row_block: 1 for one device, 16 for k > 1)."""
+    return int(lib().vrt_frame_row_block(k))
+
+
+def block_band_plan(height: int, k: int, row_block: int):
+    """vrt_block_band_plan: ([(row0, rows, row_step)] per device, rows of the largest band) of the
+    block-cyclic split of `height` rows over k devices in blocks of row_block rows."""
+    out = np.zeros(k * 3, np.int32)
+    cap = lib().vrt_block_band_plan(height, k, row_block, out.ctypes.data)
+    if cap < 0:
+        raise VrtError(cap, "vrt_block_band_plan")
+    return [tuple(int(v) for v in row) for row in out.reshape(k, 3)], cap
+
+
+def block_copy_plan(width: int, height: int, k: int, row_block: int, elem_bytes: int):
+    """vrt_block_copy_plan: the 2-D copies (band, dst_offset, dst_pitch, src_offset, src_pitch,
+    width_bytes, rows) that assemble a frame from k packed block-cyclic band buffers."""
+    out = np.zeros(k * 2 * 7, np.int64)
+    n = lib().vrt_block_copy_plan(width, height, k, row_block, elem_bytes, out.ctypes.data)
+    if n < 0:
+        raise VrtError(n, "vrt_block_copy_plan")
+    return [tuple(int(v) for v in row) for row in out.reshape(k * 2, 7) if row[6] > 0]
+
+
+def comm_unique_id() -> bytes:
+    """vrt_comm_unique_id: a new RCCL unique id (rank 0 of a one-process-per-GPU job creates one
+    per communicator and the job distributes them)."""
+    buf = (C.c_uint8 * abi.VRT_COMM_ID_BYTES)()
+    r = lib().vrt_comm_unique_id(buf, abi.VRT_COMM_ID_BYTES)
+    if r != abi.VRT_COMM_ID_BYTES:
+        raise VrtError(r, "vrt_comm_unique_id")
+    return bytes(buf)
+
+
 class Renderer:
     """One vrt_ctx (replaces the GL context + FrameBuffer of the reference). `device` is a HIP
     device ordinal, or a sequence of ordinals: whole frames are then split into row bands across
@@ -428,6 +464,26 @@ class Renderer:
                     "vrt_debug_randomize")
         return out
 
+
+    def comm_join(self, ids, nranks: int, rank: int):
+        """vrt_comm_join: one RCCL communicator per id (a list of VRT_COMM_ID_BYTES-byte ids), this
+        context's device as `rank` of `nranks` (blocks until every rank joined each one)."""
+        blob = b"".join(ids)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        self._check(self._lib.vrt_comm_join(self._h, buf, len(ids), nranks, rank), "vrt_comm_join")
+
+    def gather_band_async(self, comm: int, d_band: int, nbytes: int, d_gathered: int, stream: int):
+        """vrt_gather_band_async: ncclGather of nbytes from every rank's d_band to rank 0's
+        d_gathered (nranks x nbytes) on communicator `comm`, enqueued on `stream`."""
+        self._check(self._lib.vrt_gather_band_async(self._h, comm, d_band, nbytes, d_gathered or None,
+                                                    stream or None), "vrt_gather_band_async")
+
+    def assemble_blocks_async(self, d_bands: int, k: int, band_rows_cap: int, width: int, height: int,
+                              row_block: int, d_frame: int, frame_pitch: int, stream: int):
+        """vrt_assemble_blocks_async: the frame's rows from k gathered block-cyclic bands."""
+        self._check(self._lib.vrt_assemble_blocks_async(self._h, d_bands, k, band_rows_cap, width, height,
+                                                        row_block, d_frame, frame_pitch, stream or None),
+                    "vrt_assemble_blocks_async")
 
     def build_scene_device(self, scene: str, n: int, seed: int = 0, stream: int = 0):
         """Build a scene's volume on the device (vrt_build_scene_device) and make it current."""

@@ -22,6 +22,7 @@ VRT_HIT_FLAG_TIE3 = 1
 VRT_HIT_FLAG_STEP_CAP = 2
 VRT_HIT_FLAG_STACK_FULL = 4
 VRT_MAX_STEPS = 4096
+VRT_COMM_ID_BYTES = 128
 
 SCENE_TERRAIN = 0
 SCENE_GLASS_CUBE = 1
@@ -101,6 +102,15 @@ SIGNATURES = {
     "vrt_device_ordinal": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_band_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     "vrt_band_copy_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    # ABI v12: block-cyclic whole-frame split, one process per GPU (RCCL gather + assembly)
+    "vrt_frame_row_block": (C.c_int, [C.c_int32]),
+    "vrt_block_band_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "vrt_block_copy_plan": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "vrt_comm_unique_id": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_comm_join": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "vrt_gather_band_async": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "vrt_assemble_blocks_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                            C.c_int32, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p]),
     "vrt_destroy": (None, [C.c_void_p]),
     "vrt_last_error": (C.c_char_p, [C.c_void_p]),
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),

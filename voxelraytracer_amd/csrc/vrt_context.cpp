@@ -160,6 +160,11 @@ struct vrt_ctx {
   bool slot_valid[kRing] = {};
   void* h_stage = nullptr;              // pinned host staging of synchronous frames (k bands in)
   size_t h_stage_bytes = 0;
+  // ABI v12: this process's rank of a one-process-per-GPU job (vrt_comm_join): one RCCL
+  // communicator per lane, so that frames in flight on different lane streams gather without
+  // ordering each other (a communicator's operations run in issue order)
+  std::vector<ncclComm_t> rank_comms;
+  int32_t rank_nranks = 0, rank_id = -1;
   std::string err;
 };
 
@@ -200,17 +205,61 @@ struct DeviceGuard {
   }
 };
 
-int32_t band_rows(int32_t height, int32_t k, int32_t j) { return j < height ? (height - j + k - 1) / k : 0; }
-int32_t band_cap(int32_t height, int32_t k) { return (height + k - 1) / k; }
+// Cyclic-row bands (ABI v8/v10 plans): band j holds frame rows j, j + k, ...
+int32_t cyc_band_rows(int32_t height, int32_t k, int32_t j) { return j < height ? (height - j + k - 1) / k : 0; }
 
-// The strided copy that places band j (its rows packed at `row` bytes each) into its frame rows
-// j, j + k, ... of a frame of h rows: one hipMemcpy2D (staging to the host, gather on device).
-struct BandCopy {
-  size_t dst_off, dst_pitch, src_pitch, width, rows;
+// Whole frames over k > 1 devices (ABI v12): block-cyclic bands of kFrameRowBlock adjacent rows,
+// band j = blocks j, j + k, ... (band row i = frame row ((i / B) k + j) B + i % B), one launch per
+// band and frame, as bench.py's one-process-per-GPU split (tiles.block_band_spec): an 8x8 wave of
+// a band covers 8 adjacent frame rows as in the whole frame, so its walks stay coherent (slowest
+// of 8 bands: C3 0.0150 -> 0.0139, C4 0.0274 -> 0.0229 ms per frame against cyclic rows,
+// profiles/r03_s45, r03_s54). One device renders the whole frame (B = 1, kParts parts).
+constexpr int32_t kFrameRowBlock = 16;
+constexpr int32_t kFrameRowBlockSh = 4;
+static_assert((1 << kFrameRowBlockSh) == kFrameRowBlock, "row block is 2^sh");
+struct BandGeom {
+  int32_t row0, rows, row_step, sh;
 };
-BandCopy band_copy(int32_t w, int32_t h, int32_t k, int32_t j, size_t elem) {
+BandGeom block_band(int32_t height, int32_t k, int32_t block, int32_t j) {
+  if (k == 1) return BandGeom{0, height, 1, 0};
+  int32_t sh = 0;
+  while ((1 << sh) < block) ++sh;
+  const int32_t nb = (height + block - 1) / block;
+  const int32_t own = j < nb ? (nb - j + k - 1) / k : 0;
+  int32_t rows = own * block;
+  if (own > 0 && (nb - 1) % k == j) rows -= nb * block - height;
+  return BandGeom{j * block, rows, k * block, sh};
+}
+int32_t frame_block(int32_t k) { return k > 1 ? kFrameRowBlock : 1; }
+int32_t band_rows(int32_t height, int32_t k, int32_t j) { return block_band(height, k, frame_block(k), j).rows; }
+// rows of the largest band (band 0's): every band buffer and the gather's per-device slice
+int32_t band_cap(int32_t height, int32_t k) {
+  if (k == 1) return height;
+  const int32_t nb = (height + kFrameRowBlock - 1) / kFrameRowBlock;
+  return (nb + k - 1) / k * kFrameRowBlock;
+}
+
+// The 2-D copies that place band j (its rows packed at `row` bytes each) into its frame rows:
+// cyclic rows (block 1) are one copy of `rows` rows k rows apart; block-cyclic bands one copy of
+// the band's full blocks (block x row bytes each, k blocks apart) and one of a short last block.
+// Staging to the host and the device-to-device assembly use exactly these (vrt_block_copy_plan).
+struct BandCopy {
+  size_t dst_off, dst_pitch, src_off, src_pitch, width, rows;
+};
+int band_copies(int32_t w, int32_t h, int32_t k, int32_t block, int32_t j, size_t elem, BandCopy out[2]) {
   const size_t row = size_t(w) * elem;
-  return BandCopy{size_t(j) * row, size_t(k) * row, row, row, size_t(band_rows(h, k, j))};
+  if (block == 1) {
+    out[0] = BandCopy{size_t(j) * row, size_t(k) * row, 0, row, row, size_t(cyc_band_rows(h, k, j))};
+    return out[0].rows ? 1 : 0;
+  }
+  const BandGeom g = block_band(h, k, block, j);
+  const size_t full = size_t(g.rows) / size_t(block), rest = size_t(g.rows) % size_t(block);
+  int n = 0;
+  if (full) out[n++] = BandCopy{size_t(j) * block * row, size_t(k) * block * row, 0, size_t(block) * row,
+                                size_t(block) * row, full};
+  if (rest) out[n++] = BandCopy{(full * size_t(k) + size_t(j)) * size_t(block) * row, rest * row,
+                                full * size_t(block) * row, rest * row, rest * row, 1};
+  return n;
 }
 
 // Part p of band j: frame rows (j + p k) + i (k P), band rows p + i P.
@@ -218,7 +267,7 @@ struct PartRows {
   int32_t row0, rows, row_step, band_row0;
 };
 PartRows part_rows(int32_t height, int32_t k, int32_t parts, int32_t j, int32_t p) {
-  const int32_t hb = band_rows(height, k, j);
+  const int32_t hb = cyc_band_rows(height, k, j);
   return PartRows{j + p * k, hb > p ? (hb - p + parts - 1) / parts : 0, k * parts, p};
 }
 
@@ -659,7 +708,8 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
   const bool hist = rgba8 && alpha != 1.0f;
   const bool single = counting || hits;  // one counter replica set: one counted launch
   // one_part: device-output frames consumed on their own stream (vrt_frame_stream)
-  const int nparts = single || one_part || (overlap && !hist) ? 1 : kParts;
+  // k > 1: one launch per block-cyclic band (a band's blocks are not split into parts)
+  const int nparts = single || one_part || (overlap && !hist) || k > 1 ? 1 : kParts;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
     VRT_HIP(ctx, hipSetDevice(s.device));
@@ -690,12 +740,14 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
       VRT_HIP(ctx, hipMemsetAsync(s.d_cnt, 0, sizeof(unsigned long long) * VRT_CNT_COUNT, s.ls[g][0]));
     const uint32_t* hsrc = ctx->reset_pending && !ctx->raw_is_cur[pslot] ? s.d_rawbuf[pslot] : s.d_ring[pslot];
     for (int q = 0; q < nparts; ++q) {
-      const PartRows pr = nparts == 1 ? PartRows{j, hb, k, 0} : part_rows(h, k, kParts, j, q);
+      const BandGeom bg = block_band(h, k, frame_block(k), j);
+      const PartRows pr = nparts == 1 ? PartRows{bg.row0, bg.rows, bg.row_step, 0} : part_rows(h, k, kParts, j, q);
       if (pr.rows == 0) {
         VRT_HIP(ctx, hipEventRecord(s.ev_done[g][q], s.ls[g][q]));
         continue;
       }
       vrt::KArgs a = make_args(ctx, s, cam, p, pr.row0, pr.rows, pr.row_step);
+      a.row_blk_sh = nparts == 1 ? bg.sh : 0;
       a.pitch = int32_t(int64_t(w) * nparts);
       const size_t off = size_t(pr.band_row0) * size_t(w);
       s.timed[q] = timing;
@@ -789,13 +841,16 @@ int stage_bands(vrt_ctx* ctx, int g, int32_t w, int32_t h, const void* const* ba
   const int32_t k = int32_t(ctx->sh.size());
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
-    const BandCopy bc = band_copy(w, h, k, j, elem);
-    if (bc.rows == 0) continue;
+    BandCopy bc[2];
+    const int nc = band_copies(w, h, k, frame_block(k), j, elem, bc);
+    if (nc == 0) continue;
     VRT_HIP(ctx, hipSetDevice(s.device));
     int st = wait_lane(ctx, s, g, s.ls[g][0]);
     if (st != VRT_OK) return st;
-    VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(ctx->h_stage) + stage_off + bc.dst_off, bc.dst_pitch, bands[j],
-                                  bc.src_pitch, bc.width, bc.rows, hipMemcpyDeviceToHost, s.ls[g][0]));
+    for (int c = 0; c < nc; ++c)
+      VRT_HIP(ctx, hipMemcpy2DAsync(static_cast<char*>(ctx->h_stage) + stage_off + bc[c].dst_off, bc[c].dst_pitch,
+                                    static_cast<const char*>(bands[j]) + bc[c].src_off, bc[c].src_pitch, bc[c].width,
+                                    bc[c].rows, hipMemcpyDeviceToHost, s.ls[g][0]));
   }
   return VRT_OK;
 }
@@ -856,11 +911,19 @@ int gather_frame(vrt_ctx* ctx, int32_t w, int32_t h, int slot, int g, hipEvent_t
   VRT_HIP(ctx, hipSetDevice(root.device));
   if (reuse) VRT_HIP(ctx, hipStreamWaitEvent(root.gs, reuse, 0));
   uint32_t* out = ctx->d_frames[slot];
-  for (int32_t j = 0; j < k; ++j) {  // band row r -> frame row j + r k
-    const BandCopy bc = band_copy(w, h, k, j, 4);
-    if (bc.rows > 0)
-      VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + bc.dst_off, bc.dst_pitch, src[j], bc.src_pitch,
-                                    bc.width, bc.rows, hipMemcpyDeviceToDevice, root.gs));
+  if (ctx->distinct) {  // the gathered bands, cap rows apart, into their frame rows: one kernel
+    vrt::launch_assemble_blocks(ctx->d_gather, uint64_t(cap) * uint64_t(w), k, k > 1 ? kFrameRowBlockSh : 0, w, h,
+                                out, uint64_t(w), root.gs);
+    VRT_HIP(ctx, hipGetLastError());
+  } else {
+    for (int32_t j = 0; j < k; ++j) {  // each band's blocks into their frame rows
+      BandCopy bc[2];
+      const int nc = band_copies(w, h, k, frame_block(k), j, 4, bc);
+      for (int c = 0; c < nc; ++c)
+        VRT_HIP(ctx, hipMemcpy2DAsync(reinterpret_cast<char*>(out) + bc[c].dst_off, bc[c].dst_pitch,
+                                      reinterpret_cast<const char*>(src[j]) + bc[c].src_off, bc[c].src_pitch,
+                                      bc[c].width, bc[c].rows, hipMemcpyDeviceToDevice, root.gs));
+    }
   }
   if (!ctx->distinct)
     for (int32_t j = 0; j < k; ++j) {  // same physical device: the bands were read here
@@ -942,6 +1005,11 @@ void vrt_destroy(vrt_ctx* c) {
   if (!c) return;
   DeviceGuard guard;
   for (ncclComm_t cm : c->comms) (void)ncclCommDestroy(cm);
+  if (!c->rank_comms.empty()) {
+    (void)hipSetDevice(c->sh[0].device);
+    (void)hipDeviceSynchronize();  // no gather still runs on them
+    for (ncclComm_t cm : c->rank_comms) (void)ncclCommDestroy(cm);
+  }
   if (!c->sh.empty()) {
     (void)hipSetDevice(c->sh[0].device);
     if (c->d_gather) (void)hipFree(c->d_gather);
@@ -980,21 +1048,65 @@ int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out) {
       o[2] = pr.row_step;
       o[3] = pr.band_row0;
     }
-  return band_cap(height, k);
+  return (height + k - 1) / k;  // the largest cyclic band
 }
 
 int vrt_band_copy_plan(int32_t width, int32_t height, int32_t k, int32_t elem_bytes, int64_t* out) {
   if (width < 1 || height < 1 || k < 1 || elem_bytes < 1 || !out) return VRT_ERR_INVALID;
   for (int32_t j = 0; j < k; ++j) {
-    const BandCopy bc = band_copy(width, height, k, j, size_t(elem_bytes));
+    BandCopy bc[2];
+    const int nc = band_copies(width, height, k, 1, j, size_t(elem_bytes), bc);
     int64_t* o = out + size_t(j) * 5;
-    o[0] = int64_t(bc.dst_off);
-    o[1] = int64_t(bc.dst_pitch);
-    o[2] = int64_t(bc.src_pitch);
-    o[3] = int64_t(bc.width);
-    o[4] = int64_t(bc.rows);
+    o[0] = int64_t(bc[0].dst_off);
+    o[1] = int64_t(bc[0].dst_pitch);
+    o[2] = int64_t(bc[0].src_pitch);
+    o[3] = int64_t(bc[0].width);
+    o[4] = nc ? int64_t(bc[0].rows) : 0;
   }
   return k;
+}
+
+int vrt_frame_row_block(int32_t k) { return k < 1 ? VRT_ERR_INVALID : frame_block(k); }
+
+int vrt_block_band_plan(int32_t height, int32_t k, int32_t row_block, int32_t* out) {
+  if (height < 1 || k < 1 || !out || row_block < 1 || row_block > 64 || (row_block & (row_block - 1)))
+    return VRT_ERR_INVALID;
+  int32_t cap = 0;
+  for (int32_t j = 0; j < k; ++j) {
+    // k = 1: the whole frame as one band of blocks row_block apart (the same row formula)
+    const BandGeom g = k == 1 ? BandGeom{0, height, row_block, 0} : block_band(height, k, row_block, j);
+    out[size_t(j) * 3 + 0] = g.row0;
+    out[size_t(j) * 3 + 1] = g.rows;
+    out[size_t(j) * 3 + 2] = g.row_step;
+    cap = std::max(cap, g.rows);
+  }
+  return cap;
+}
+
+int vrt_block_copy_plan(int32_t width, int32_t height, int32_t k, int32_t row_block, int32_t elem_bytes,
+                        int64_t* out) {
+  if (width < 1 || height < 1 || k < 1 || elem_bytes < 1 || !out || row_block < 1 || row_block > 64 ||
+      (row_block & (row_block - 1)))
+    return VRT_ERR_INVALID;
+  int n = 0;
+  for (int32_t j = 0; j < k; ++j) {
+    BandCopy bc[2];
+    const int nc = k == 1 ? band_copies(width, height, 1, 1, 0, size_t(elem_bytes), bc)
+                          : band_copies(width, height, k, row_block, j, size_t(elem_bytes), bc);
+    for (int c = 0; c < 2; ++c) {
+      int64_t* o = out + (size_t(j) * 2 + c) * 7;
+      const BandCopy b = c < nc ? bc[c] : BandCopy{0, 0, 0, 0, 0, 0};
+      o[0] = j;
+      o[1] = int64_t(b.dst_off);
+      o[2] = int64_t(b.dst_pitch);
+      o[3] = int64_t(b.src_off);
+      o[4] = int64_t(b.src_pitch);
+      o[5] = int64_t(b.width);
+      o[6] = int64_t(b.rows);
+      n += c < nc ? 1 : 0;
+    }
+  }
+  return n;
 }
 
 int vrt_upload_volume(vrt_ctx* ctx, const vrt_volume* vol) {
@@ -1400,6 +1512,76 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
 }
 
 void* vrt_frame_stream(const vrt_ctx* ctx) { return ctx ? static_cast<void*>(ctx->frame_stream) : nullptr; }
+
+int vrt_comm_unique_id(uint8_t* out, int32_t bytes) {
+  static_assert(sizeof(ncclUniqueId) == VRT_COMM_ID_BYTES, "RCCL unique id size");
+  if (!out || bytes < VRT_COMM_ID_BYTES) return VRT_ERR_INVALID;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return VRT_ERR_DEVICE;
+  std::memcpy(out, &id, sizeof(id));
+  return VRT_COMM_ID_BYTES;
+}
+
+int vrt_comm_join(vrt_ctx* ctx, const uint8_t* ids, int32_t count, int32_t nranks, int32_t rank) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (ctx->sh.size() != 1) return fail(ctx, VRT_ERR_INVALID, "vrt_comm_join: a one-device context per rank");
+  if (!ids || count < 1 || count > 16 || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(ctx, VRT_ERR_INVALID, "vrt_comm_join: 1..16 ids, 0 <= rank < nranks");
+  if (!ctx->rank_comms.empty()) return fail(ctx, VRT_ERR_INVALID, "vrt_comm_join: already joined");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  for (int32_t i = 0; i < count; ++i) {  // every rank in the same order: each init waits for all ranks
+    ncclUniqueId id;
+    std::memcpy(&id, ids + size_t(i) * VRT_COMM_ID_BYTES, sizeof(id));
+    ncclComm_t cm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&cm, nranks, id, rank);
+    if (r != ncclSuccess) {
+      for (ncclComm_t c2 : ctx->rank_comms) (void)ncclCommDestroy(c2);
+      ctx->rank_comms.clear();
+      return nccl_fail(ctx, r, "ncclCommInitRank");
+    }
+    ctx->rank_comms.push_back(cm);
+  }
+  ctx->rank_nranks = nranks;
+  ctx->rank_id = rank;
+  ctx->err.clear();
+  return VRT_OK;
+}
+
+int vrt_gather_band_async(vrt_ctx* ctx, int32_t comm, const void* d_band, uint64_t bytes, void* d_gathered,
+                          void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (comm < 0 || size_t(comm) >= ctx->rank_comms.size())
+    return fail(ctx, VRT_ERR_INVALID, "vrt_gather_band_async: no such communicator (vrt_comm_join)");
+  if (!d_band || (ctx->rank_id == 0 && !d_gathered))
+    return fail(ctx, VRT_ERR_INVALID, "vrt_gather_band_async: null band or (root) gather buffer");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  VRT_NCCL(ctx, ncclGather(d_band, ctx->rank_id == 0 ? d_gathered : nullptr, size_t(bytes), ncclUint8, 0,
+                           ctx->rank_comms[size_t(comm)], static_cast<hipStream_t>(hip_stream)));
+  return VRT_OK;
+}
+
+int vrt_assemble_blocks_async(vrt_ctx* ctx, const uint32_t* d_bands, int32_t k, int32_t band_rows_cap,
+                              int32_t width, int32_t height, int32_t row_block, uint32_t* d_frame,
+                              int64_t frame_pitch, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int32_t sh = 0;
+  while (sh < 7 && (1 << sh) != row_block) ++sh;
+  if (sh == 7) return fail(ctx, VRT_ERR_INVALID, "row_block must be a power of two in [1, 64]");
+  if (!d_bands || !d_frame || k < 1 || width < 1 || height < 1 || frame_pitch < width)
+    return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_async: bad buffers or sizes");
+  // every band must fit its slice: band 0 holds the most rows
+  const int32_t nb = (height + row_block - 1) / row_block;
+  if (int64_t((nb + k - 1) / k) * row_block > band_rows_cap)
+    return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_async: band_rows_cap below the largest band");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  vrt::launch_assemble_blocks(d_bands, uint64_t(band_rows_cap) * uint64_t(width), k, sh, width, height, d_frame,
+                              uint64_t(frame_pitch), static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
 
 int vrt_debug_collectives(vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;

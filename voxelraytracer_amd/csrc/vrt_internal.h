@@ -112,6 +112,10 @@ void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* 
 void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise, hipStream_t s);
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,
                       float* out, hipStream_t s);
+// frame rows [0, height) from k block-cyclic bands of 2^sh-row blocks, band_words words apart
+// (band j's row i = frame row ((i >> sh) k + j) 2^sh + i % 2^sh), rows frame_pitch words apart
+void launch_assemble_blocks(const uint32_t* bands, uint64_t band_words, int32_t k, int32_t sh, int32_t width,
+                            int32_t height, uint32_t* frame, uint64_t frame_pitch, hipStream_t s);
 
 }  // namespace vrt
 

@@ -662,13 +662,215 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   return result;
 }
 
-// RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant)
-template <bool STATS, bool LEN0Z = false>
+// ------------------------------------------------------------ block-pipelined skip walk --
+//
+// skip_walk waits for each sampled step's texel before the next step: the texel's skip distance
+// decides whether the next step samples. A wave whose 64 lanes walk unrelated rays (the deferred
+// exact pass's compacted pixels) then waits for a texel round trip at nearly every step — some
+// lane samples at almost every step — where a coherent 8x8 wave waits only at its ~10 % sampled
+// steps. pipe_walk runs the same exact steps in blocks of KB: within a block no lane waits (a step
+// beyond the lane's skip window issues its texel load and goes on), and at the block's end the
+// wave waits once for all of the block's loads and then decides, per lane, in step order:
+//  - the first sampled step that stops the reference's walk (an event byte, an outside sample,
+//    the length test) ends the walk there: the lane restores the block's start state and replays
+//    the exact steps up to that one (the steps after it were speculative; state and exit record are
+//    then the ones skip_walk leaves at that step);
+//  - otherwise the block's last sampled step opens the next skip window, as in skip_walk.
+// A step inside a window is still a step of an empty in-volume voxel, so skipping it is exact; the
+// pipelined walk only samples more steps (those after the block's first sample) and never fewer
+// reference decisions. The state update of every step is the reference's, op for op (exact_step).
+
+// One exact DDA step (voxel.glsl:275-281 / :323-327, then the crossed axis' t, :296 / :381) with the
+// crossed axis' operands from the lane's LDS table: skip_walk's step, factored for pipe_walk's
+// main and replay loops (identical ops). Returns s = len - len0; tp, mey, mez as in skip_walk.
+__device__ __forceinline__ float exact_step(f3& t, float& len, const float len0, const uint32_t ax_a0,
+                                            const uint32_t ax_a1, const uint32_t ax_a2, f3& tp,
+                                            unsigned long long& mey, unsigned long long& mez) {
+  const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
+  tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
+  len += tmin;
+  const float s = len - len0;
+  mey = __builtin_amdgcn_ballot_w64(tp.y == 0.0f);
+  mez = __builtin_amdgcn_ballot_w64(tp.z == 0.0f);
+  const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+  const float ca = ae.x + s * ae.y;
+  const float num = (ca + ae.w) - ae.x;
+  const float q = div_rn(num, ae.y, ae.z) - s;
+  t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
+  return s;
+}
+
+#if defined(VRT_PIPE_K) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_PIPE_K is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_PIPE_K
+#define VRT_PIPE_K 8
+#endif
+
+template <bool SHADOW, int KB>
+__device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
+                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
+                                         int32_t& vidx_out, uint32_t& v_out) {
+  static_assert(KB >= 2 && KB <= 8, "flag bytes hold at most 8 steps");
+  const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
+                     __builtin_copysignf(1.0f, dir.z));
+  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
+  const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
+  const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
+  c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
+  c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
+  c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
+  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
+  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));
+  const bool skip_ok = SHADOW || medium == 0u;
+  const uint32_t obase =
+      ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
+  const float s_len = c.max_len - len0;
+  f3 t = w.t;
+  float len = w.len;
+  uint32_t it = w.it;
+  bool check = w.check_cube;
+  int result;
+  constexpr uint32_t kOutside = 0x100u;
+  for (;;) {
+    // loop-top tests of the reference (as skip_walk)
+    if (!(len < c.max_len)) {
+      result = WALK_MISS;
+      break;
+    }
+    if (check) {
+      const float sc = len - len0;
+      if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
+        result = WALK_MISS;
+        break;
+      }
+    }
+    if (it >= VRT_MAX_STEPS) {
+      result = WALK_CAP;
+      break;
+    }
+    const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
+    const uint32_t it0 = it;
+    uint32_t k = 0;  // wave-uniform (SGPR): steps of this inner walk
+    uint32_t k_exit = k_max;
+    uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;
+    int32_t x_vidx = -1;
+    float s_lim = -1.0f;
+    for (;;) {
+      if (k >= k_max) break;  // wave-uniform step bound
+      // block start: the state a stopping lane replays from
+      const f3 t_cp = t;
+      const float len_cp = len;
+      const uint32_t k_cp = k;
+      uint32_t pk[KB];
+      // bit j: step j sampled; 8 + j: its sample was outside; 16 + j: len >= max_len after it
+      uint32_t fl = 0u;
+      float wvi = 0.0f, wvj = 0.0f, wvk = 0.0f;  // the last sampled step's cell (window)
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        pk[j] = 0u;
+        if (k >= k_max) break;
+        ++k;
+        f3 tp;
+        unsigned long long mey, mez;
+        const float s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
+        if (!(s < s_lim)) {  // sampled: issue the texel load, consume it at the block's end
+          const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+          const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
+                            cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
+          const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+          const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+          const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+          const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
+          const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
+          pk[j] = load_u16_at(c.vox, mad24(mad24(vk, c.p, vj), c.p, vi), obase);
+          fl |= (1u << j) | (inb ? 0u : 1u << (8 + j)) | (len < c.max_len ? 0u : 1u << (16 + j));
+          wvi = float(vi);
+          wvj = float(vj);
+          wvk = float(vk);
+        }
+      }
+      // block end: one wait for the block's loads; the first stopping step, the last sample
+      uint32_t jst = uint32_t(KB), pst = 0u, plast = 0u;
+#pragma unroll
+      for (int j = KB - 1; j >= 0; --j) {
+        const uint32_t v_ev = (fl >> (8 + j)) & 1u ? kOutside : (pk[j] & kVoxMask);
+        const bool stop = ((fl >> j) & 1u) &&
+                          ((SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium)) || ((fl >> (16 + j)) & 1u));
+        jst = stop ? uint32_t(j) : jst;
+        pst = stop ? pk[j] : pst;
+      }
+      const uint32_t sm = fl & 0xFFu;
+      const uint32_t jl = sm ? 31u - uint32_t(__builtin_clz(sm)) : 0u;
+#pragma unroll
+      for (int j = 0; j < KB; ++j) plast = jl == uint32_t(j) ? pk[j] : plast;
+      if (jst < uint32_t(KB)) {
+        // the walk stops at step jst of this block: replay the exact steps from the block start
+        t = t_cp;
+        len = len_cp;
+        f3 tp = mk(0.0f, 0.0f, 0.0f);
+        float s = 0.0f;
+        for (uint32_t r = 0; r <= jst; ++r) {
+          unsigned long long mey, mez;
+          s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
+        }
+        const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+        const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
+                          cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
+        const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+        const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+        const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+        const bool out = (fl >> (8 + jst)) & 1u;
+        k_exit = k_cp + jst + 1u;
+        x_v = out ? 0u : (pst & kVoxMask);  // outside samples read 0 (GetVoxel :151-152)
+        x_out = out ? 1u : 0u;
+        x_axis = tp.z == 0.0f ? 2u : (tp.y == 0.0f ? 1u : 0u);  // axis_index of the step's masks
+        x_vidx = out ? -1 : int32_t(canonical_index(c, cvt_flr(qx), cvt_flr(qy), cvt_flr(qz)));
+        asm volatile("" : "+v"(k_exit), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
+        break;
+      }
+      if (sm) {  // the next skip window from the block's last sample (as skip_walk's)
+        const uint32_t dist = plast >> kDistShift;
+        const float fd = float(dist) - kSkipMargin;
+        const float lx = __builtin_fmaf(wvi, rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
+        const float ly = __builtin_fmaf(wvj, rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
+        const float lz = __builtin_fmaf(wvk, rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
+        const bool open = skip_ok & (((fl >> (8 + jl)) & 1u) == 0u) & ((plast & kVoxMask) == 0u) & (dist >= 2u);
+        s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
+      }
+    }
+    it = it0 + k_exit;
+    const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
+    asm volatile("" : "+v"(x_out));
+    check = x_out != 0u;
+    if (event) {
+      axis_out = int(x_axis);
+      vidx_out = x_vidx;
+      v_out = x_v;
+      result = WALK_EVENT;
+      break;
+    }
+  }
+  const float s_end = len - len0;
+  w.t = t;
+  w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
+  w.len = len;
+  w.it = it;
+  w.ties = 0;
+  w.check_cube = check;
+  return result;
+}
+
+// RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant).
+// PIPE: block size of pipe_walk (stats-free instances of the deferred exact pass), 0: skip_walk.
+template <bool STATS, bool LEN0Z = false, int PIPE = 0>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v) {
+  static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
+    if constexpr (PIPE > 0) return pipe_walk<false, PIPE>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
     // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
     return skip_walk<false, STATS, false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
@@ -676,13 +878,16 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
 }
 
 // RayMarchShadow walk: the direction is normalize(u_SunDir) for every ray (uniform constants)
-template <bool STATS>
+template <bool STATS, int PIPE = 0>
 __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len0, WalkState& w) {
+  static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   int axis;
   int32_t vidx;
   uint32_t v;
-  if (__builtin_expect(fast_path_ok(c.sun_n), 1))
+  if (__builtin_expect(fast_path_ok(c.sun_n), 1)) {
+    if constexpr (PIPE > 0) return pipe_walk<true, PIPE>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
     return skip_walk<true, STATS>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+  }
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
 
@@ -767,19 +972,19 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 }
 
 // RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
-template <bool STATS>
+template <bool STATS, int PIPE = 0>
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
   WalkState w;
   walk_init(w, ray);
-  const int r = walk_shadow<STATS>(c, ray.pos, ray.len, w);
+  const int r = walk_shadow<STATS, PIPE>(c, ray.pos, ray.len, w);
   walk_account(w, r, VRT_CNT_SHADOW_STEPS, k, steps, flags);
   return r == WALK_EVENT;
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
 // PRIMARY: the primary ray (len 0, medium air: every event is a hit, no in-volume refraction)
-template <bool STATS, bool TEX, bool PRIMARY = false>
+template <bool STATS, bool TEX, bool PRIMARY = false, int PIPE = 0>
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -798,7 +1003,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk_ray<STATS, PRIMARY>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
+    r = walk_ray<STATS, PRIMARY, PIPE>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -882,7 +1087,7 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h);
 // (stats-free colour-only): the shadow bit by a certified walk from the exact hit point when it
 // settles it (cert_shadow_exact), and no shadow walk when it cannot change the brightness
 // (lit == ambient).
-template <bool STATS, bool TEX, bool CSH>
+template <bool STATS, bool TEX, bool CSH, int PIPE = 0>
 __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h, f3& color, Counters& k,
                                       uint32_t& steps, uint32_t& flags) {
   static_assert(!CSH || !STATS, "certified shadows in stats-free instances only");
@@ -901,12 +1106,12 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
       int blocked = 0;
       if (lit != kAmbient) {
         blocked = cert_shadow_exact(c, h);
-        if (blocked < 0) blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
+        if (blocked < 0) blocked = march_shadow<STATS, PIPE>(c, sr, k, steps, flags) ? 1 : 0;
       }
       brightness = blocked ? kAmbient : lit;
     } else {
       k.c[VRT_CNT_SHADOW_RAYS]++;
-      const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
+      const bool in_shadow = march_shadow<STATS, PIPE>(c, sr, k, steps, flags);
       brightness = in_shadow ? kAmbient : lit_brightness<TEX>(h, sr.dir, ray.dir);
     }
     apply_hit_color<TEX>(c, h, ray.energy, brightness, color);
@@ -916,11 +1121,11 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
 }
 
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
-template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
+template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false, int PIPE = 0>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
-  shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
+  const Hit h = march<STATS, TEX, PRIMARY, PIPE>(c, ray, k, steps, flags);
+  shade<STATS, TEX, CSH, PIPE>(c, ray, h, color, k, steps, flags);
   return h;
 }
 
@@ -1519,6 +1724,7 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
 // air — settled by certified walks where they can be (settled: colour updated, no secondary
 // rays); the exact march (as march()) otherwise.
 // (Out of line it costs C2-C4 +45 %, profiles/r01_v69_ab_noinline_w6.log.)
+template <int PIPE = 0>
 __device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k,
                           uint32_t& steps, uint32_t& flags) {
   Hit h;
@@ -1539,7 +1745,7 @@ __device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Coun
     int axis;
     int32_t vidx;
     uint32_t v;
-    const int r = walk_ray<false, false>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    const int r = walk_ray<false, false, PIPE>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -1914,14 +2120,14 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
 // Returns whether the pixel ran a bounce stack.
-template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
   StackRay stack[kMaxStack - 1];  // the top entry lives in `ray`
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE>(c, ray, color, k, steps, flags);
 #ifdef VRT_STAMPS
   const uint32_t st_wave = blockIdx.x * kWgWaves + (threadIdx.x >> 6);
   {
@@ -1971,15 +2177,15 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
         bool settled;
-        h = march_cert(lc, ray, color, settled, k, steps, flags);
+        h = march_cert<PIPE>(lc, ray, color, settled, k, steps, flags);
         if (settled) {
           h.found = false;  // a miss or a hit without secondary rays
           continue;
         }
-        shade<STATS, TEX, CSH>(lc, ray, h, color, k, steps, flags);
+        shade<STATS, TEX, CSH, PIPE>(lc, ray, h, color, k, steps, flags);
         continue;
       }
-      h = trace_with_shadow<STATS, TEX, false, CSH>(lc, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH, PIPE>(lc, ray, color, k, steps, flags);
     }
 #ifdef VRT_STAMPS
     {
@@ -2212,7 +2418,7 @@ __device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r)
 // under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
 // (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
 // slower, profiles/r03_s67)
-template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES>
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t lane = lane_id();
@@ -2261,7 +2467,7 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
     store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
   }
 }
@@ -2324,6 +2530,32 @@ __global__ void __launch_bounds__(256) build_scene_kernel(uint8_t* __restrict__ 
         v = 3;
     }
     vox[idx] = v;
+  }
+}
+
+// Frame assembly of block-cyclic bands (ABI v12; the re-interleave after a gather of the bands to
+// one device): band j of k holds the frame's row blocks j, j + k, ... of 2^sh rows, so its row i is
+// frame row ((i >> sh) * k + j) * 2^sh + (i & (2^sh - 1)); bands lie band_words words apart. One
+// workgroup per frame row copies the row from its band: 16-byte words when VEC (width, band_words
+// and frame_pitch multiples of 4 words, 16-byte aligned buffers), else 4-byte words. HBM-bound:
+// 8 B of traffic per pixel, no reuse.
+template <bool VEC>
+__global__ void __launch_bounds__(256) assemble_blocks_kernel(const uint32_t* __restrict__ bands,
+                                                              uint64_t band_words, int32_t k, int32_t sh,
+                                                              int32_t width, uint32_t* __restrict__ frame,
+                                                              uint64_t frame_pitch) {
+  const uint32_t y = blockIdx.x;
+  const uint32_t m = y >> sh;
+  const uint32_t j = m % uint32_t(k), mb = m / uint32_t(k);
+  const uint64_t bi = (uint64_t(mb) << sh) + (y & ((1u << sh) - 1u));
+  const uint32_t* src = bands + uint64_t(j) * band_words + bi * uint64_t(width);
+  uint32_t* dst = frame + uint64_t(y) * frame_pitch;
+  if (VEC) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (uint32_t x = threadIdx.x; x < uint32_t(width) / 4u; x += 256u) d4[x] = s4[x];
+  } else {
+    for (uint32_t x = threadIdx.x; x < uint32_t(width); x += 256u) dst[x] = src[x];
   }
 }
 
@@ -2544,6 +2776,19 @@ void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise,
   const uint64_t vol = uint64_t(n) * n * n;
   const unsigned blocks = unsigned(std::min<uint64_t>((vol + 255) / 256, 16384));
   hipLaunchKernelGGL(build_scene_kernel, dim3(blocks), dim3(256), 0, s, vox, scene, n, noise);
+}
+
+void launch_assemble_blocks(const uint32_t* bands, uint64_t band_words, int32_t k, int32_t sh, int32_t width,
+                            int32_t height, uint32_t* frame, uint64_t frame_pitch, hipStream_t s) {
+  if (height <= 0 || width <= 0) return;
+  const bool vec = width % 4 == 0 && band_words % 4 == 0 && frame_pitch % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(bands) & 15u) == 0 && (reinterpret_cast<uintptr_t>(frame) & 15u) == 0;
+  if (vec)
+    hipLaunchKernelGGL(assemble_blocks_kernel<true>, dim3(uint32_t(height)), dim3(256), 0, s, bands, band_words, k,
+                       sh, width, frame, frame_pitch);
+  else
+    hipLaunchKernelGGL(assemble_blocks_kernel<false>, dim3(uint32_t(height)), dim3(256), 0, s, bands, band_words, k,
+                       sh, width, frame, frame_pitch);
 }
 
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,

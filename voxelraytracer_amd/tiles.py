@@ -8,10 +8,9 @@ so an 8x8 pixel wave covers 8 adjacent frame rows and its rays' walks stay as co
 whole frame (the slowest of 8 bands: C3 0.0150 -> 0.0139, C4 0.0274 -> 0.0237 ms per frame,
 profiles/r03_s45, r03_s46); bands then differ by at most one block. Each rank renders its
 band into HBM. The volume is replicated once per GPU (broadcast_volume). The only exchange is the
-output: either one gather of the bands to rank 0 per frame (gather=True: RCCL over xGMI with the
-"nccl" backend, gloo on CPU for tests; rank 0 re-interleaves), or none — the bands stay on their
-ranks (gather=False, bench.py's default for N > 1) and collect() gathers one frame when the whole
-frame is wanted (SURVEY §8e's gather is output delivery, not part of the per-pixel path).
+output: one gather of the bands to rank 0 per frame (gather=True, bench.py's default for N > 1:
+SURVEY §8e's RCCL gather over xGMI; rank 0 re-interleaves the bands into the frame), or none — the
+bands stay on their ranks (gather=False) and collect() gathers one frame when it is wanted.
 
 Within a rank the band is rendered as P interleaved parts (global part q = s*N + r owns frame
 rows q, q + N*P, ...), each on its own HIP stream, and — without the per-frame gather — L frames
@@ -30,9 +29,14 @@ the renderer's row pitch, ABI v4) and filters them in place against the same row
 previous frame: no band buffers, no assembly copy. With several lanes a part reads its history
 from the previous lane's buffer and writes its own.
 
-gather=True double-buffers the band so that the gather of frame k overlaps the render of frame
-k+1 (one lane only). Bands are RGBA8 words when the renderer runs the fused temporal filter + RGB8
-store (the reference's stored frame format, main.cpp:363-393): 4 B per pixel on the wire.
+With gather=True every frame's render, gather and (rank 0) assembly are enqueued on its lane's
+stream, so frames in flight on the other lanes overlap the gather of this one, and a lane's band
+buffer is rewritten only after the gather that read it (stream order; ABI v12). The exchange is
+pluggable: GatherLib (the library's ncclGather on one RCCL communicator per lane + its assembly
+kernel, bench.py's nccl runs: three C calls per frame, no cross-stream events) or GatherTorch
+(torch.distributed.gather + index_copy_, synchronous per frame: the gloo tests). Bands are padded
+to the largest band's rows so that every rank sends the same bytes. Bands are RGBA8 words when the
+renderer runs the fused temporal filter + RGB8 store (main.cpp:363-393): 4 B per pixel on the wire.
 """
 from __future__ import annotations
 
@@ -117,6 +121,56 @@ def broadcast_volume(vox: torch.Tensor, src: int = 0, group=None) -> torch.Tenso
     return vox
 
 
+class GatherTorch:
+    """Per-frame exchange through torch.distributed: dist.gather of every rank's padded band to rank
+    0, then rank 0's re-interleave (index_copy_ into the frame). Synchronous per frame (a gloo
+    gather of CUDA tensors blocks the host; with nccl, work.wait() orders the lane stream after the
+    collective): no collective is left outstanding across frames. The exchange of the gloo tests
+    (two ranks sharing one GPU, where RCCL cannot run) and of CPU tiling."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def run(self, tiler, lane: int) -> None:
+        band = tiler.bufs[lane]
+        glist = list(tiler.gathered[lane].unbind(0)) if tiler.rank == 0 else None
+        dist.gather(band, glist, dst=0, group=self.group)
+        if tiler.rank == 0:
+            g = tiler.gathered[lane]
+            tiler.frames[lane].index_copy_(0, tiler.asm_index, g.view(-1, *g.shape[2:]))
+
+
+class GatherLib:
+    """Per-frame exchange through the C-ABI (ABI v12): ncclGather of the padded band to rank 0 on
+    one RCCL communicator per lane (vrt_gather_band_async) and, on rank 0, the assembly kernel
+    (vrt_assemble_blocks_async) — both enqueued on the lane's stream right after its render, so
+    that the next frames on the other lanes overlap them and no event crosses streams. The
+    communicators are joined (vrt_comm_join) with ids rank 0 creates and `share_ids` distributes
+    (bench.py: a broadcast over the job's process group)."""
+
+    def __init__(self, renderer, lanes: int, world: int, rank: int, share_ids):
+        import voxelraytracer_amd as vrt
+
+        ids = [vrt.comm_unique_id() for _ in range(lanes)] if rank == 0 else None
+        ids = share_ids(ids, lanes)
+        renderer.comm_join(ids, world, rank)
+        self.ren, self.lanes, self.args = renderer, lanes, None
+
+    def run(self, tiler, lane: int) -> None:
+        if self.args is None:   # per lane: (band ptr, bytes, gathered ptr, frame ptr, stream)
+            words = tiler.width * tiler.channels * tiler.dtype.itemsize // 4
+            self.words = words
+            self.args = [(tiler.bufs[g].data_ptr(), tiler.bufs[g].numel() * tiler.dtype.itemsize,
+                          tiler.gathered[g].data_ptr() if tiler.rank == 0 else 0,
+                          tiler.frames[g].data_ptr() if tiler.rank == 0 else 0,
+                          tiler.part_streams[g][0].cuda_stream) for g in range(tiler.lanes)]
+        band, nbytes, gath, frame, st = self.args[lane]
+        self.ren.gather_band_async(lane % self.lanes, band, nbytes, gath, st)
+        if tiler.rank == 0:
+            self.ren.assemble_blocks_async(gath, tiler.world, tiler.rmax, self.words, tiler.height,
+                                           tiler.row_block, frame, self.words, st)
+
+
 class FrameTiler:
     """Renders a sequence of frames across `world` ranks, `parts` streams per lane, `lanes`
     frames in flight per rank.
@@ -125,16 +179,18 @@ class FrameTiler:
     ([rows, W, channels] of `dtype` on `device`; a row-strided view, see row_pitch) on the CURRENT
     stream (the HIP kernel through the C-ABI, or the oracle in CPU tests); `prev` holds that
     part's rows of the previous frame (the temporal history; zeros before the first frame; with
-    one lane it is `out` itself: each pixel is read before it is written).
-    frame() enqueues the next frame; with gather=False (or one rank) it returns this rank's band
-    of it ([rows, W, C], the whole frame with one rank); with several ranks and gather=True the
-    gather is issued asynchronously and rank 0 returns the PREVIOUS frame, assembled on
-    `self.assembly_stream` (None on the first call and on other ranks). finish() makes the current
-    stream wait for every frame enqueued so far and returns the last frame (band) on rank 0 (the
-    last band elsewhere with gather=False); collect() (gather=False) assembles the last frame on
-    rank 0 with one gather. A returned band stays valid until `lanes` more frames are enqueued;
-    synchronise the device before reading it. independent=True declares that render_band does
-    not read `prev` (u_Alpha = 1): frames on different lanes are then not ordered at all.
+    one lane it is `out` itself: each pixel is read before it is written). Block-cyclic bands
+    (row_block > 1, and every gathered band) receive row_block= as well.
+    frame() enqueues the next frame. With gather=False (or one rank) it returns this rank's band
+    of it ([rows, W, C], the whole frame with one rank); collect() (after finish()) assembles the
+    last frame on rank 0 with one gather. With several ranks and gather=True every frame is
+    gathered to rank 0 and re-interleaved there by `exchange` (GatherTorch by default; GatherLib
+    for the library's RCCL path), in the frame's lane stream: frame() returns the new frame on
+    rank 0 (complete once that stream is synchronised) and None elsewhere. A returned band or
+    frame stays valid until `lanes` more frames are enqueued. finish() makes the current stream
+    wait for every frame enqueued so far and returns the last frame (rank 0 with gather) or band.
+    independent=True declares that render_band does not read `prev` (u_Alpha = 1): frames on
+    different lanes are then not ordered at all.
     launch (optional, CUDA): the lean form of render_band, launch(row0, rows, row_step,
     out_ptr, prev_ptr, pitch, stream_handle) with device pointers, the row pitch in pixels and the
     part's HIP stream; frames whose lanes need no event ordering (one lane, or independent) then
@@ -145,62 +201,68 @@ class FrameTiler:
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
                  channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
                  lanes: int = 1, independent: bool = False, launch: Optional[Callable] = None,
-                 world: Optional[int] = None, rank: Optional[int] = None, row_block: int = 1):
+                 world: Optional[int] = None, rank: Optional[int] = None, row_block: int = 1,
+                 exchange=None):
         # world / rank: override the process group's (one process rehearsing rank `rank` of a
         # `world`-way split on one GPU; no exchange may then be requested)
         self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         if world is not None and gather:
             raise ValueError("a rehearsed split keeps its band (gather=False)")
+        if lanes < 1:
+            raise ValueError("lanes >= 1")
         self.group = group
         self.width, self.height, self.parts = width, height, parts
         self.row_block = row_block
-        if row_block > 1:   # block-cyclic band, one part, kept on its rank (bands may be unequal)
-            if parts != 1 or gather:
-                raise ValueError("block-cyclic bands are one part per lane and stay on their rank "
-                                 "(parts=1, gather=False)")
+        self.gather = gather and self.world > 1
+        if row_block > 1 or self.gather:
+            # block-cyclic band (row_block 1: cyclic rows), one part per lane; bands may be unequal
+            if parts != 1:
+                raise ValueError("block-cyclic and gathered bands are one part per lane (parts=1)")
             self.row0, self.rows, self.step = block_band_spec(self.rank, self.world, height, row_block)
             self.specs = [(self.row0, self.rows, self.step)]
         else:
             self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
             self.specs = [part_spec(self.rank, self.world, s, parts, height) for s in range(parts)]
-        # render_band / launch receive row_block= only for block-cyclic bands
-        self.block_kw = {"row_block": row_block} if row_block > 1 else {}
+        # render_band / launch receive row_block= for block-cyclic (and gathered) bands
+        self.block_kw = {"row_block": row_block} if (row_block > 1 or self.gather) else {}
         self.rows_p = self.specs[0][1]
         self.render_band = render_band
         self.cuda = torch.device(device).type == "cuda"
-        self.gather = gather and self.world > 1
-        if lanes < 1 or (self.gather and lanes > 1):
-            raise ValueError("lanes >= 1; frames in flight keep their bands on the ranks "
-                             "(gather=False)")
         self.lanes, self.independent = lanes, independent
         self.channels, self.dtype = channels, dtype
-        shape = (parts, self.rows_p, width, channels)
-        self.bufs = None
-        self.bands = None
-        if not self.gather:
+        self.exchange = None
+        self.exchange_on = True   # bench.py's render-only pass switches the per-frame gather off
+        self.latest = None
+        if self.gather:
+            # every rank's band padded to the largest band's rows: equal gather sizes
+            specs = [block_band_spec(r, self.world, height, row_block) for r in range(self.world)]
+            self.rmax = max(sp[1] for sp in specs)
+            self.bufs = [torch.zeros((self.rmax, width, channels), dtype=dtype, device=device)
+                         for _ in range(lanes)]
+            self.gathered = self.frames = None
+            if self.rank == 0:
+                self.gathered = [torch.empty((self.world, self.rmax, width, channels), dtype=dtype,
+                                             device=device) for _ in range(lanes)]
+                # frame row of every gathered row; padding rows land in a scratch row `height`
+                idx = torch.full((self.world, self.rmax), height, dtype=torch.int64)
+                for r, (r0, rows, step) in enumerate(specs):
+                    idx[r, :rows] = band_frame_rows(r0, rows, step, row_block)
+                self.asm_index = idx.reshape(-1).to(device)
+                self.frames = [torch.zeros((height + 1, width, channels), dtype=dtype, device=device)
+                               for _ in range(lanes)]
+            self.exchange = exchange or GatherTorch(group)
+        else:
             # this rank's band per lane; part s renders band rows s, s + parts, ... in place
             self.bufs = [torch.zeros((self.rows, width, channels), dtype=dtype, device=device)
                          for _ in range(lanes)]
-        else:
-            self.bands = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(2)]
         self.part_streams = ([[torch.cuda.Stream(device=device) for _ in range(parts)]
                               for _ in range(lanes)]
-                             if self.cuda and (parts > 1 or lanes > 1) else None)
+                             if self.cuda and (parts > 1 or lanes > 1 or self.gather) else None)
         self.part_done = [[None] * parts for _ in range(lanes)]   # dependent lanes: frame events
         self.fresh = True   # the streams must first wait for the current stream's work
-        self.assembly_stream = None
-        self.gathered = None
-        self.frame_buf = None
-        if self.rank == 0 and self.gather:
-            self.frame_buf = torch.empty((height, width, channels), dtype=dtype, device=device)
-            self.gathered = [torch.empty((self.world,) + shape, dtype=dtype, device=device)
-                             for _ in range(2)]
-            if self.cuda:
-                self.assembly_stream = torch.cuda.Stream(device=device)
         self.plan = None   # lean launches: per lane, per part (row0, rows, step, out, prev, pitch, stream)
-        if (launch is not None and not self.gather and self.part_streams is not None
-                and (lanes == 1 or independent)):
+        if launch is not None and self.part_streams is not None and (lanes == 1 or independent):
             self.launch = launch
             self.plan = []
             for g in range(lanes):
@@ -211,34 +273,36 @@ class FrameTiler:
                     row.append((row0, rows, step, o.data_ptr(), pv.data_ptr(), row_pitch(o),
                                 self.part_streams[g][q].cuda_stream))
                 self.plan.append(row)
-        self.pending = [None, None]     # gather that still reads bands[b]
-        self.assembled = [None, None]   # rank 0: assembly that still reads gathered[b]
-        self.prev = None                # rank 0: buffer index of the frame awaiting assembly
         self.k = 0
 
     # ---- helpers ---------------------------------------------------------------------------
     def part_rows(self, buf: torch.Tensor, s: int) -> torch.Tensor:
-        """Part s's rows of a band buffer [rows, W, C] (band rows s, s + parts, ...)."""
+        """Part s's rows of a band buffer (band rows s, s + parts, ...; a gathered band's padding
+        rows excluded)."""
+        if self.gather:
+            return buf[:self.rows]
         return buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
 
     def last(self) -> torch.Tensor:
-        """This rank's band buffer of the last frame enqueued (gather=False)."""
-        return self.bufs[(self.k - 1) % self.lanes]
+        """This rank's band buffer of the last frame enqueued (its band rows)."""
+        b = self.bufs[(self.k - 1) % self.lanes]
+        return b[:self.rows] if self.gather else b
 
-    def _part_buffers(self, s: int, band: torch.Tensor, prev: torch.Tensor):
-        """(out, prev) of part s: its rows of the lane buffers, or its slot of the gather bands."""
-        if not self.gather:
-            return self.part_rows(band, s), self.part_rows(prev, s)
-        return band[s], prev[s]
-
-    def _render_parts(self, lane: int, band: torch.Tensor, prev: torch.Tensor, wait_work):
-        """Enqueue every part of the next frame on `lane` (each first waits for `wait_work`, the
-        gather that last read its buffer). Returns the parts' completion events (CUDA streams)."""
+    def next_stream(self):
+        """The HIP stream the next frame's (first) launch is enqueued on (CUDA), or None."""
         if self.part_streams is None:
-            if wait_work is not None:
-                wait_work.wait()
+            return torch.cuda.current_stream() if self.cuda else None
+        return self.part_streams[self.k % self.lanes][0]
+
+    def _render_parts(self, lane: int, band: torch.Tensor, prev: torch.Tensor):
+        """Enqueue every part of the next frame on `lane` (and its exchange). Returns the parts'
+        completion events (CUDA streams, dependent lanes)."""
+        if self.part_streams is None:
             for s, (row0, rows, step) in enumerate(self.specs):
-                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev), **self.block_kw)
+                self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
+                                 **self.block_kw)
+            if self.gather and self.exchange_on:
+                self.exchange.run(self, lane)
             return None
         cur = torch.cuda.current_stream()
         if self.fresh:
@@ -252,21 +316,22 @@ class FrameTiler:
         for s, (row0, rows, step) in enumerate(self.specs):
             st = self.part_streams[lane][s]
             with torch.cuda.stream(st):
-                if wait_work is not None:
-                    wait_work.wait()
                 if dep and self.part_done[prev_lane][s] is not None:
                     st.wait_event(self.part_done[prev_lane][s])   # the history rows of part s
-                self.render_band(row0, rows, step, *self._part_buffers(s, band, prev), **self.block_kw)
-                ev = st.record_event() if (dep or self.gather) else None
+                self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
+                                 **self.block_kw)
+                if self.gather and self.exchange_on:
+                    self.exchange.run(self, lane)
+                ev = st.record_event() if dep else None
                 self.part_done[lane][s] = ev
                 events.append(ev)
         return events
 
     # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
+        lane = self.k % self.lanes
+        self.k += 1
         if self.plan is not None:   # lean launches from precomputed arguments
-            lane = self.k % self.lanes
-            self.k += 1
             if self.fresh:
                 cur = torch.cuda.current_stream()
                 for ln in self.part_streams:
@@ -275,61 +340,28 @@ class FrameTiler:
                 self.fresh = False
             for args in self.plan[lane]:
                 self.launch(*args, **self.block_kw)
+            if self.gather and self.exchange_on:
+                if isinstance(self.exchange, GatherLib):
+                    self.exchange.run(self, lane)
+                else:
+                    with torch.cuda.stream(self.part_streams[lane][0]):
+                        self.exchange.run(self, lane)
+        else:
+            self._render_parts(lane, self.bufs[lane], self.bufs[(self.k - 2) % self.lanes])
+        if not self.gather:
             return self.bufs[lane]
-        if not self.gather:   # one rank, or ranks that keep their bands: no exchange
-            lane = self.k % self.lanes
-            band, prev = self.bufs[lane], self.bufs[(self.k - 1) % self.lanes]
-            self.k += 1
-            self._render_parts(lane, band, prev, None)
-            return band
-        b = self.k % 2
-        prev = self.bands[(self.k - 1) % 2]
-        self.k += 1
-        band = self.bands[b]
-        wait_work, self.pending[b] = self.pending[b], None
-        events = self._render_parts(0, band, prev, wait_work)
-        cur = torch.cuda.current_stream() if self.cuda else None
-        if events is not None:   # the gather (issued from the current stream) needs every part
-            for e in events:
-                cur.wait_event(e)
-        if self.assembled[b] is not None:   # rank 0: the assembly that read gathered[b]
-            cur.wait_event(self.assembled[b])
-            self.assembled[b] = None
-        glist = list(self.gathered[b].unbind(0)) if self.rank == 0 else None
-        work = dist.gather(band, glist, dst=0, group=self.group, async_op=True)
-        out = self._assemble_prev() if self.rank == 0 else None
-        self.pending[b] = work
-        if self.rank == 0:
-            self.prev = b
-        return out
-
-    def _assemble_prev(self) -> Optional[torch.Tensor]:
-        """Rank 0: re-interleave the previous frame's gathered parts into frame_buf once its
-        gather is done (on the assembly stream when there is one). pending[b] is left for the
-        next render into bands[b] to wait on."""
-        if self.prev is None:
-            return None
-        b = self.prev
-        self.prev = None
-        work = self.pending[b]
-        if self.assembly_stream is None:
-            work.wait()
-            return assemble_parts(self.gathered[b], self.frame_buf)
-        with torch.cuda.stream(self.assembly_stream):
-            work.wait()
-            out = assemble_parts(self.gathered[b], self.frame_buf)
-        self.assembled[b] = self.assembly_stream.record_event()
-        return out
+        self.latest = self.frames[lane][:self.height] if self.rank == 0 else None
+        return self.latest
 
     def collect(self) -> Optional[torch.Tensor]:
-        """Without the per-frame gather, after finish(): one gather of every rank's band of the
-        last frame to rank 0, re-interleaved into the whole frame (returned on rank 0, None
-        elsewhere); e.g. to display or check the last frame. Synchronous."""
-        assert not self.gather, "collect() is for gather=False tilers"
+        """After finish(): one gather of every rank's band of the last frame to rank 0 through the
+        process group, re-interleaved into the whole frame (returned on rank 0, None elsewhere);
+        e.g. to display the last frame of bands kept on their ranks, or to check a gathered frame
+        against an independent assembly. Synchronous."""
         band = self.last().contiguous()
         if self.world == 1:
             return band
-        if self.row_block == 1:
+        if self.row_block == 1 and not self.gather:   # equal cyclic bands (band_spec)
             glist = ([torch.empty_like(band) for _ in range(self.world)] if self.rank == 0 else None)
             dist.gather(band, glist, dst=0, group=self.group)
             return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
@@ -357,22 +389,12 @@ class FrameTiler:
         return [st for ln in (self.part_streams or ()) for st in ln]
 
     def finish(self) -> Optional[torch.Tensor]:
-        cur = torch.cuda.current_stream() if self.cuda else None
-        if not self.gather:
+        if self.cuda:
+            cur = torch.cuda.current_stream()
             for ln in self.part_streams or ():
                 for st in ln:
                     cur.wait_stream(st)
-            self.fresh = True
-            return self.last()
-        out = self._assemble_prev() if self.rank == 0 else None
-        for i, w in enumerate(self.pending):
-            if w is not None:
-                w.wait()
-                self.pending[i] = None
-        for ln in self.part_streams or ():
-            for st in ln:
-                cur.wait_stream(st)
-        if self.assembly_stream is not None:
-            cur.wait_stream(self.assembly_stream)
         self.fresh = True
-        return out
+        if self.gather:
+            return self.latest
+        return self.last()

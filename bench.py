@@ -800,8 +800,13 @@ def main():
             "gather": (None if world == 1 else
                        {"per_frame": tiler.gather, "how": gather_how,
                         "band_rows_padded": getattr(tiler, "rmax", None),
-                        "bytes_to_rank0_per_frame": (tiler.rmax * w * (4 if rgba8 else 16) * (world - 1)
-                                                     if tiler.gather else None),
+                        "bytes_to_rank0_per_frame": (
+                            (tiler.exchange.bytes_per_rank(tiler) if isinstance(tiler.exchange, GatherLib)
+                             else tiler.rmax * w * (4 if rgba8 else 16)) * (world - 1)
+                            if tiler.gather else None),
+                        "wire": (("RGB8, 3 B per pixel" if tiler.exchange.rgb8 else "RGBA8/float as rendered")
+                                 if isinstance(tiler.exchange, GatherLib) and tiler.exchange.args else
+                                 ("as rendered" if tiler.gather else None)),
                         "render_only": render_only}),
             "latency": latency,
             "device_warmup": device_warmup,

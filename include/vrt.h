@@ -456,6 +456,16 @@ int vrt_gather_band_async(vrt_ctx* ctx, int32_t comm, const void* d_band, uint64
 int vrt_assemble_blocks_async(vrt_ctx* ctx, const uint32_t* d_bands, int32_t k, int32_t band_rows_cap,
                               int32_t width, int32_t height, int32_t row_block, uint32_t* d_frame,
                               int64_t frame_pitch, void* hip_stream);
+/* RGB8 wire format of a gathered band: the RGBA8 words' A byte is always 255, so a band can cross
+ * xGMI as 3 bytes per pixel (25 % fewer bytes into rank 0). vrt_pack_rgb8_async packs `pixels`
+ * RGBA8 words (a multiple of 4; 16-byte aligned) into 3-byte pixels (4-byte aligned);
+ * vrt_assemble_blocks_rgb8_async is vrt_assemble_blocks_async from such bands (band j at
+ * d_bands + j * band_rows_cap * width * 3 bytes; width and frame_pitch multiples of 4), unpacking
+ * to RGBA8 words with A = 255. */
+int vrt_pack_rgb8_async(vrt_ctx* ctx, const uint32_t* d_rgba8, uint64_t pixels, uint8_t* d_rgb8, void* hip_stream);
+int vrt_assemble_blocks_rgb8_async(vrt_ctx* ctx, const uint8_t* d_bands, int32_t k, int32_t band_rows_cap,
+                                   int32_t width, int32_t height, int32_t row_block, uint32_t* d_frame,
+                                   int64_t frame_pitch, void* hip_stream);
 
 #ifdef __cplusplus
 }

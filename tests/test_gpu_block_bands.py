@@ -81,3 +81,22 @@ def test_block_band_float_output_and_arguments(built):
             b0, brows, bstep, blk = bad
             with pytest.raises(vrt.VrtError):
                 r.render_rows_async(cam, p, b0, brows, bstep, band.data_ptr(), stream=st, row_block=blk)
+
+
+def test_c4_eight_way_split_at_full_size(built):
+    """configs[4] at its full size: _TERRAIN 512^3, 3840x2160, (R,T) = (4,2), split over 8 ranks
+    into 16-row block-cyclic bands (bench.py's and vrt_create(mask)'s split): every rank's band —
+    through the timed path's launches (certified pass + deferred exact pass, automatic mode) and the
+    in-lane exact path — equals its rows of the whole frame rendered by the exact STATS instance,
+    bit for bit (the u_Alpha = 1 stored frame the bench times)."""
+    n, w, h, R, T, world, block = 512, 3840, 2160, 4, 2, 8, 16
+    with vrt.Renderer(0) as r:
+        r.build_scene_device("terrain", n)
+        cam = vrt.make_camera(w, h)
+        full = band_frames(r, cam, R, T, 1.0, 0, h, 1, 1, 1, n_frames=1, counters=True)[0]
+        for rank in range(world):
+            row0, rows, step = block_band_spec(rank, world, h, block)
+            idx = band_frame_rows(row0, rows, step, block).numpy()
+            for mode in (1, 0):   # automatic deferred exact pass (the timed path), in-lane
+                got = band_frames(r, cam, R, T, 1.0, row0, rows, step, block, mode, n_frames=1)[0]
+                assert np.array_equal(got, full[idx]), (rank, mode)

@@ -1,7 +1,8 @@
 """GPU: the deferred exact pass (vrt_set_exact_pass, ABI v9). A certified pass renders the pixels
-its certified walks settle and records, per wave, the lane mask of the others; a second kernel
-renders those with the exact path, compacted into dense waves (ballot masks, a popcount scan
-across the wave, binary search + select-bit per lane: no atomics). Images must be bit-identical
+its certified walks settle and appends the others to a list (per wave a ballot of the deferred
+lanes, one atomicAdd on one of 8 XCD-local segment counters, mbcnt ranks; waves with >= 32
+deferred pixels keep an 8x8 chunk in lane order); a second kernel renders the list with the exact
+path 64 pixels to a wave (round 4: its walks pipelined in blocks of 8 steps). Images must be bit-identical
 to the in-lane fallback and to the exact STATS instance, frame after frame, on scenes where many
 pixels defer (glass cube: most pixels; random sparse volumes with every byte; near-edge cameras)
 and with the temporal filter reading its history (alpha 0.5), including bands (row steps),

@@ -42,15 +42,41 @@ def test_assemble_blocks_matches_band_placement(built, k, width, height, block):
     assert torch.equal(frame.cpu(), reference_frame(bands, k, height, block))
 
 
-def test_rank_comm_gather_one_rank(built):
+@pytest.mark.parametrize("k,width,height,block", [(3, 40, 53, 16), (8, 3840, 2160, 16), (2, 36, 9, 1)])
+def test_rgb8_wire_assembly_matches_rgba8(built, k, width, height, block):
+    """RGB8 wire format: pack each band (vrt_pack_rgb8_async), assemble from the packed bands
+    (vrt_assemble_blocks_rgb8_async): the frame equals the RGBA8 assembly of the same bands."""
+    import voxelraytracer_amd as vrt
+
+    plan, cap = vrt.block_band_plan(height, k, block)
+    g = torch.Generator().manual_seed(7 * k + width)
+    bands = torch.randint(0, 256, (k, cap, width, 4), dtype=torch.uint8, generator=g)
+    bands[..., 3] = 255   # pack_rgb8's A byte
+    bands = bands.cuda()
+    packed = torch.zeros(k * cap * width * 3, dtype=torch.uint8, device="cuda")
+    frame = torch.zeros((height, width, 4), dtype=torch.uint8, device="cuda")
+    with vrt.Renderer(0) as ren:
+        st = torch.cuda.current_stream().cuda_stream
+        for j in range(k):
+            ren.pack_rgb8_async(bands[j].data_ptr(), cap * width, packed[j * cap * width * 3:].data_ptr(), st)
+        ren.assemble_blocks_rgb8_async(packed.data_ptr(), k, cap, width, height, block, frame.data_ptr(), width, st)
+        torch.cuda.synchronize()
+    assert torch.equal(packed.view(k, cap, width, 3).cpu(), bands[..., :3].cpu())
+    assert torch.equal(frame.cpu(), reference_frame(bands, k, height, block))
+
+
+@pytest.mark.parametrize("wire", ["rgb8", "rgba8"])
+def test_rank_comm_gather_one_rank(built, wire):
     import voxelraytracer_amd as vrt
     from voxelraytracer_amd.tiles import GatherLib
 
     w, h, block, lanes = 96, 40, 16, 2
     with vrt.Renderer(0) as ren:
-        ex = GatherLib(ren, lanes, 1, 0, lambda ids, n: ids)   # a one-rank job: the ids stay here
+        ex = GatherLib(ren, lanes, 1, 0, lambda ids, n: ids, wire=wire)   # one rank: the ids stay here
         st = [torch.cuda.Stream() for _ in range(lanes)]
         bufs = [torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)]
+        for b in bufs:
+            b[..., 3] = 255   # rendered RGBA8 words: A = 255
         tiler = types.SimpleNamespace(
             width=w, height=h, channels=4, dtype=torch.uint8, world=1, rank=0, rmax=h, row_block=block,
             lanes=lanes, bufs=bufs, part_streams=[[s] for s in st],
@@ -59,8 +85,10 @@ def test_rank_comm_gather_one_rank(built):
         for lane in range(lanes):
             ex.run(tiler, lane)
         torch.cuda.synchronize()
+        assert ex.rgb8 == (wire == "rgb8")
         for lane in range(lanes):
-            assert torch.equal(tiler.gathered[lane][0], bufs[lane])      # ncclGather of one rank
+            if not ex.rgb8:
+                assert torch.equal(tiler.gathered[lane][0], bufs[lane])  # ncclGather of one rank
             assert torch.equal(tiler.frames[lane][:h], bufs[lane])       # assembly of one band
         with pytest.raises(vrt.VrtError):
             ren.gather_band_async(lanes, bufs[0].data_ptr(), bufs[0].numel(), 0, 0)  # no such comm

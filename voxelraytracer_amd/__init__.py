@@ -485,6 +485,18 @@ class Renderer:
                                                         row_block, d_frame, frame_pitch, stream or None),
                     "vrt_assemble_blocks_async")
 
+    def pack_rgb8_async(self, d_rgba8: int, pixels: int, d_rgb8: int, stream: int):
+        """vrt_pack_rgb8_async: RGBA8 words -> 3-byte pixels (the RGB8 wire format of a gather)."""
+        self._check(self._lib.vrt_pack_rgb8_async(self._h, d_rgba8, pixels, d_rgb8, stream or None),
+                    "vrt_pack_rgb8_async")
+
+    def assemble_blocks_rgb8_async(self, d_bands: int, k: int, band_rows_cap: int, width: int, height: int,
+                                   row_block: int, d_frame: int, frame_pitch: int, stream: int):
+        """vrt_assemble_blocks_rgb8_async: the frame's RGBA8 rows from k gathered RGB8 bands."""
+        self._check(self._lib.vrt_assemble_blocks_rgb8_async(self._h, d_bands, k, band_rows_cap, width, height,
+                                                             row_block, d_frame, frame_pitch, stream or None),
+                    "vrt_assemble_blocks_rgb8_async")
+
     def build_scene_device(self, scene: str, n: int, seed: int = 0, stream: int = 0):
         """Build a scene's volume on the device (vrt_build_scene_device) and make it current."""
         self._check(self._lib.vrt_build_scene_device(self._h, SCENES[scene], n, seed,

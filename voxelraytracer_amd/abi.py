@@ -111,6 +111,9 @@ SIGNATURES = {
     "vrt_gather_band_async": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "vrt_assemble_blocks_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
                                             C.c_int32, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p]),
+    "vrt_pack_rgb8_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "vrt_assemble_blocks_rgb8_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                                 C.c_int32, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p]),
     "vrt_destroy": (None, [C.c_void_p]),
     "vrt_last_error": (C.c_char_p, [C.c_void_p]),
     "vrt_upload_volume": (C.c_int, [C.c_void_p, C.POINTER(Volume)]),

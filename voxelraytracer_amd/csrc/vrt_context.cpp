@@ -44,9 +44,12 @@ constexpr int kOrderSlots = 16;        // tile-order buffers per device (band ge
 constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 65536 16x8 tiles (4096 x 2048 pixels)
 constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 2u * vrt::kOrdClasses;  // KArgs::order
 // KArgs::defer: two sets of segment counters, then the list: a pixel per word, 8 segments of
-// ceil(tiles / 8) tiles' pixels each
-constexpr size_t kDeferSegWords = size_t(kOrderMaxTiles) / vrt::kOrdClasses * vrt::kWgThreads;
-constexpr size_t kDeferSlotWords = vrt::kDeferHdr + vrt::kOrdClasses * kDeferSegWords;
+// ceil(tiles / 8) tiles' pixels each. Allocated per tile-order slot at its first deferred launch,
+// sized for that band (a 1080p band: 8.3 MB; until r03 every slot was sized for 65 536 tiles up
+// front, 537 MB per device).
+size_t defer_words(uint32_t tiles) {
+  return vrt::kDeferHdr + size_t(vrt::kOrdClasses) * ((tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * vrt::kWgThreads;
+}
 // first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
 // 8160 tiles are heavy)
 #if (defined(VRT_DEV_NOQUERY) || defined(VRT_DEV_NOCONSUME) || defined(VRT_DEV_NOCSWAIT)) && \
@@ -77,6 +80,8 @@ struct OrderSlot {
   uint64_t epoch = 0, tick = 0;
   uint64_t defer_epoch = 0;    // deferred-pass launches since the slot's counters were zeroed
   bool last_defer = false;     // the slot's last launch was a deferred-pass launch
+  uint32_t* defer = nullptr;   // the deferred pass's counters + list (lazily allocated)
+  size_t defer_cap = 0;        // its words
 };
 
 struct Shard {
@@ -116,9 +121,8 @@ struct Shard {
   // textured mode's atlas (RGBA8 words)
   uint32_t* d_atlas = nullptr;
   int32_t atlas_size = 0;
-  // heavy-first tile order, and the deferred exact pass's per-wave masks (same slots)
+  // heavy-first tile order, and the deferred exact pass's lists (same slots)
   uint32_t* d_order_pool = nullptr;
-  uint32_t* d_defer_pool = nullptr;
   OrderSlot order[kOrderSlots];
   uint64_t order_tick = 0;
 };
@@ -275,7 +279,8 @@ void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
   std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats,
                              (void*)s.d_cnt, (void*)s.d_cnt_rep, (void*)s.d_out, (void*)s.d_hit,
-                             (void*)s.d_atlas, (void*)s.d_order_pool, (void*)s.d_defer_pool};
+                             (void*)s.d_atlas, (void*)s.d_order_pool};
+  for (OrderSlot& o : s.order) bufs.push_back(o.defer);
   for (int r = 0; r < kRing; ++r) {
     bufs.push_back(s.d_ring[r]);
     bufs.push_back(s.d_rawbuf[r]);
@@ -329,8 +334,6 @@ hipError_t shard_init(Shard& s, int device) {
   if (e == hipSuccess) e = hipMalloc(&s.d_cnt_rep, rep_bytes);
   if (e == hipSuccess) e = hipMemset(s.d_cnt_rep, 0, rep_bytes);
   if (e == hipSuccess) e = hipMalloc(&s.d_order_pool, pool_words * sizeof(uint32_t));
-  if (e == hipSuccess)
-    e = hipMalloc(&s.d_defer_pool, size_t(kOrderSlots) * kDeferSlotWords * sizeof(uint32_t));
   for (int i = 0; i < kOrderSlots && e == hipSuccess; ++i) s.order[i].d = s.d_order_pool + size_t(i) * kOrderSlotWords;
   return e;
 }
@@ -490,7 +493,20 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
   OrderSlot* slot = acquire_slot(s, a, st);
   if (!slot) return;
   if (defer) {  // both counter sets zeroed whenever the slot's previous launch was not one
-    uint32_t* d = s.d_defer_pool + size_t(slot - s.order) * kDeferSlotWords;
+    const size_t need = defer_words(a.tiles);
+    if (slot->defer_cap < need) {  // first deferred launch of this band on the slot (or a larger band)
+      // earlier launches with the slot run on st (its stream) and may still read the old list
+      if (slot->defer && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->defer) != hipSuccess)) return;
+      slot->defer = nullptr;
+      slot->defer_cap = 0;
+      if (hipMalloc(&slot->defer, need * sizeof(uint32_t)) != hipSuccess) {
+        slot->defer = nullptr;
+        return;  // no list: the launch keeps the exact path in lane
+      }
+      slot->defer_cap = need;
+      slot->last_defer = false;
+    }
+    uint32_t* d = slot->defer;
     if (!slot->last_defer) {
       if (hipMemsetAsync(d, 0, vrt::kDeferHdr * sizeof(uint32_t), st) != hipSuccess) return;
       slot->defer_epoch = 0;
@@ -1452,6 +1468,15 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
     // stream holds the whole frame), and the host stays at most kRing frames ahead.
     if (ctx->slot_valid[slot] && hipEventQuery(ctx->ev_slot[slot]) != hipSuccess)
       VRT_HIP(ctx, hipEventSynchronize(ctx->ev_slot[slot]));
+    // a caller that switched from its own stream to NULL: the frame this slot held may still be
+    // read there (its consumption was enqueued before call f - kRing + 1)
+    if (f >= kRing) {
+      const int rs = int((f - kRing + 1) % kRing);
+      if (ctx->consumed_valid[rs]) {
+        if (hipEventQuery(ctx->ev_consumed[rs]) != hipSuccess) VRT_HIP(ctx, hipEventSynchronize(ctx->ev_consumed[rs]));
+        ctx->consumed_valid[rs] = false;
+      }
+    }
     if ((st = launch_frame(ctx, cam, p, alpha, true, false, counting, stats != nullptr, true, nullptr, true)) !=
         VRT_OK)
       return st;
@@ -1559,6 +1584,40 @@ int vrt_gather_band_async(vrt_ctx* ctx, int32_t comm, const void* d_band, uint64
   VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
   VRT_NCCL(ctx, ncclGather(d_band, ctx->rank_id == 0 ? d_gathered : nullptr, size_t(bytes), ncclUint8, 0,
                            ctx->rank_comms[size_t(comm)], static_cast<hipStream_t>(hip_stream)));
+  return VRT_OK;
+}
+
+int vrt_pack_rgb8_async(vrt_ctx* ctx, const uint32_t* d_rgba8, uint64_t pixels, uint8_t* d_rgb8, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!d_rgba8 || !d_rgb8 || pixels % 4 != 0 || (reinterpret_cast<uintptr_t>(d_rgba8) & 15u) ||
+      (reinterpret_cast<uintptr_t>(d_rgb8) & 3u))
+    return fail(ctx, VRT_ERR_INVALID, "vrt_pack_rgb8_async: pixels % 4, 16-byte RGBA8 and 4-byte RGB8 alignment");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  vrt::launch_pack_rgb8(d_rgba8, pixels, d_rgb8, static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_assemble_blocks_rgb8_async(vrt_ctx* ctx, const uint8_t* d_bands, int32_t k, int32_t band_rows_cap,
+                                   int32_t width, int32_t height, int32_t row_block, uint32_t* d_frame,
+                                   int64_t frame_pitch, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  int32_t sh = 0;
+  while (sh < 7 && (1 << sh) != row_block) ++sh;
+  if (sh == 7) return fail(ctx, VRT_ERR_INVALID, "row_block must be a power of two in [1, 64]");
+  if (!d_bands || !d_frame || k < 1 || width < 4 || width % 4 || height < 1 || frame_pitch < width ||
+      frame_pitch % 4 || (reinterpret_cast<uintptr_t>(d_frame) & 15u) || (reinterpret_cast<uintptr_t>(d_bands) & 3u))
+    return fail(ctx, VRT_ERR_INVALID,
+                "vrt_assemble_blocks_rgb8_async: width and pitch multiples of 4, 16-byte frame, 4-byte bands");
+  const int32_t nb = (height + row_block - 1) / row_block;
+  if (int64_t((nb + k - 1) / k) * row_block > band_rows_cap)
+    return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_rgb8_async: band_rows_cap below the largest band");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  vrt::launch_assemble_blocks_rgb8(d_bands, uint64_t(band_rows_cap) * uint64_t(width), k, sh, width, height, d_frame,
+                                   uint64_t(frame_pitch), static_cast<hipStream_t>(hip_stream));
+  VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
 }
 

@@ -116,6 +116,11 @@ void launch_randomize(const float* dir, const float* pos, int n, float randomnes
 // (band j's row i = frame row ((i >> sh) k + j) 2^sh + i % 2^sh), rows frame_pitch words apart
 void launch_assemble_blocks(const uint32_t* bands, uint64_t band_words, int32_t k, int32_t sh, int32_t width,
                             int32_t height, uint32_t* frame, uint64_t frame_pitch, hipStream_t s);
+// RGB8 wire format: RGBA8 words (A = 255) -> 3 bytes per pixel (pixels % 4 == 0, 16-byte aligned)
+void launch_pack_rgb8(const uint32_t* rgba, uint64_t pixels, uint8_t* rgb, hipStream_t s);
+// launch_assemble_blocks from RGB8 bands (band_px pixels apart), unpacked to RGBA8 words (width % 4 == 0)
+void launch_assemble_blocks_rgb8(const uint8_t* bands, uint64_t band_px, int32_t k, int32_t sh, int32_t width,
+                                 int32_t height, uint32_t* frame, uint64_t frame_pitch, hipStream_t s);
 
 }  // namespace vrt
 

@@ -2374,32 +2374,6 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 #endif
 }
 
-// The r-th (from 0) set bit of m (r < popcount(m)): binary search on popcounts
-__device__ __forceinline__ uint32_t select_bit(unsigned long long m, uint32_t r) {
-  uint32_t pos = 0;
-  uint32_t lo = uint32_t(m);
-  const uint32_t nlo = uint32_t(__builtin_popcount(lo));
-  uint32_t w = lo;
-  if (r >= nlo) {
-    r -= nlo;
-    pos = 32;
-    w = uint32_t(m >> 32);
-  }
-#pragma unroll
-  for (uint32_t half = 16; half > 0; half >>= 1) {
-    const uint32_t low = w & ((1u << half) - 1u);
-    const uint32_t n = uint32_t(__builtin_popcount(low));
-    if (r >= n) {
-      r -= n;
-      pos += half;
-      w >>= half;
-    } else {
-      w = low;
-    }
-  }
-  return pos;
-}
-
 // The deferred exact pass: the pixels a certified pass (render_kernel<..., DEFER>) left to it,
 // rendered with the exact path 64 to a wave — the certified pass's waves end with their certified
 // pixels, and the exact walks that would each have held a sparse wave of them run densely here
@@ -2556,6 +2530,40 @@ __global__ void __launch_bounds__(256) assemble_blocks_kernel(const uint32_t* __
     for (uint32_t x = threadIdx.x; x < uint32_t(width) / 4u; x += 256u) d4[x] = s4[x];
   } else {
     for (uint32_t x = threadIdx.x; x < uint32_t(width); x += 256u) dst[x] = src[x];
+  }
+}
+
+// RGB8 wire format of a gathered band (ABI v12): the RGBA8 words' alpha byte is always 255
+// (pack_rgb8), so a band crosses xGMI as 3 bytes per pixel — 25 % fewer bytes into rank 0, whose
+// ingress bounds the per-frame gather. Four pixels per work-item: one 16-byte load,
+// three 4-byte stores (pixels is a multiple of 4).
+__global__ void __launch_bounds__(256) pack_rgb8_kernel(const uint4* __restrict__ rgba, uint64_t quads,
+                                                        uint32_t* __restrict__ rgb) {
+  for (uint64_t q = uint64_t(blockIdx.x) * 256 + threadIdx.x; q < quads; q += uint64_t(gridDim.x) * 256) {
+    const uint4 p = rgba[q];
+    const uint32_t a = p.x & 0xFFFFFFu, b = p.y & 0xFFFFFFu, c = p.z & 0xFFFFFFu, d = p.w & 0xFFFFFFu;
+    rgb[3 * q + 0] = a | (b << 24);
+    rgb[3 * q + 1] = (b >> 8) | (c << 16);
+    rgb[3 * q + 2] = (c >> 16) | (d << 8);
+  }
+}
+
+// assemble_blocks_kernel for RGB8 bands (band_px pixels apart, 3 bytes each): each frame row from
+// its band, unpacked to RGBA8 words (A = 255); four pixels per work-item (width % 4 == 0)
+__global__ void __launch_bounds__(256) assemble_blocks_rgb8_kernel(const uint32_t* __restrict__ bands,
+                                                                   uint64_t band_px, int32_t k, int32_t sh,
+                                                                   int32_t width, uint4* __restrict__ frame,
+                                                                   uint64_t frame_pitch) {
+  const uint32_t y = blockIdx.x;
+  const uint32_t m = y >> sh;
+  const uint32_t j = m % uint32_t(k), mb = m / uint32_t(k);
+  const uint64_t bi = (uint64_t(mb) << sh) + (y & ((1u << sh) - 1u));
+  const uint32_t* src = bands + (uint64_t(j) * band_px + bi * uint64_t(width)) * 3u / 4u;
+  uint4* dst = frame + uint64_t(y) * frame_pitch / 4u;
+  for (uint32_t x = threadIdx.x; x < uint32_t(width) / 4u; x += 256u) {
+    const uint32_t u = src[3 * x], v = src[3 * x + 1], w = src[3 * x + 2];
+    dst[x] = make_uint4(0xFF000000u | (u & 0xFFFFFFu), 0xFF000000u | (u >> 24) | ((v & 0xFFFFu) << 8),
+                        0xFF000000u | (v >> 16) | ((w & 0xFFu) << 16), 0xFF000000u | (w >> 8));
   }
 }
 
@@ -2789,6 +2797,22 @@ void launch_assemble_blocks(const uint32_t* bands, uint64_t band_words, int32_t 
   else
     hipLaunchKernelGGL(assemble_blocks_kernel<false>, dim3(uint32_t(height)), dim3(256), 0, s, bands, band_words, k,
                        sh, width, frame, frame_pitch);
+}
+
+void launch_pack_rgb8(const uint32_t* rgba, uint64_t pixels, uint8_t* rgb, hipStream_t s) {
+  const uint64_t quads = pixels / 4u;
+  if (quads == 0) return;
+  const unsigned blocks = unsigned(std::min<uint64_t>((quads + 255) / 256, 16384));
+  hipLaunchKernelGGL(pack_rgb8_kernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint4*>(rgba), quads,
+                     reinterpret_cast<uint32_t*>(rgb));
+}
+
+void launch_assemble_blocks_rgb8(const uint8_t* bands, uint64_t band_px, int32_t k, int32_t sh, int32_t width,
+                                 int32_t height, uint32_t* frame, uint64_t frame_pitch, hipStream_t s) {
+  if (height <= 0 || width <= 0) return;
+  hipLaunchKernelGGL(assemble_blocks_rgb8_kernel, dim3(uint32_t(height)), dim3(256), 0, s,
+                     reinterpret_cast<const uint32_t*>(bands), band_px, k, sh, width, reinterpret_cast<uint4*>(frame),
+                     frame_pitch);
 }
 
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,

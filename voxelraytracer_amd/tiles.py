@@ -144,28 +144,61 @@ class GatherLib:
     """Per-frame exchange through the C-ABI (ABI v12): ncclGather of the padded band to rank 0 on
     one RCCL communicator per lane (vrt_gather_band_async) and, on rank 0, the assembly kernel
     (vrt_assemble_blocks_async) — both enqueued on the lane's stream right after its render, so
-    that the next frames on the other lanes overlap them and no event crosses streams. The
-    communicators are joined (vrt_comm_join) with ids rank 0 creates and `share_ids` distributes
-    (bench.py: a broadcast over the job's process group)."""
+    that the next frames on the other lanes overlap them and no event crosses streams. RGBA8 bands
+    cross xGMI in the RGB8 wire format (wire="rgb8", the default for them: the A byte is always
+    255, so 3 of 4 bytes; vrt_pack_rgb8_async before the gather, the assembly unpacks): rank 0's
+    ingress bounds the gather. The communicators are joined (vrt_comm_join) with ids rank 0
+    creates and `share_ids` distributes (bench.py: a broadcast over the job's process group)."""
 
-    def __init__(self, renderer, lanes: int, world: int, rank: int, share_ids):
+    def __init__(self, renderer, lanes: int, world: int, rank: int, share_ids, wire: str = "rgb8"):
         import voxelraytracer_amd as vrt
 
         ids = [vrt.comm_unique_id() for _ in range(lanes)] if rank == 0 else None
         ids = share_ids(ids, lanes)
         renderer.comm_join(ids, world, rank)
-        self.ren, self.lanes, self.args = renderer, lanes, None
+        self.ren, self.lanes, self.wire, self.args = renderer, lanes, wire, None
+
+    def _setup(self, tiler) -> None:
+        self.rgb8 = (self.wire == "rgb8" and tiler.dtype == torch.uint8 and tiler.channels == 4
+                     and tiler.width % 4 == 0)
+        self.words = tiler.width * tiler.channels * tiler.dtype.itemsize // 4
+        self.packed = self.gpacked = None
+        dev = tiler.bufs[0].device
+        if self.rgb8:   # per lane: the packed band, and (rank 0) the gathered packed bands
+            px = tiler.rmax * tiler.width
+            self.packed = [torch.empty(px * 3, dtype=torch.uint8, device=dev) for _ in range(tiler.lanes)]
+            if tiler.rank == 0:
+                self.gpacked = [torch.empty(tiler.world * px * 3, dtype=torch.uint8, device=dev)
+                                for _ in range(tiler.lanes)]
+        self.args = []
+        for g in range(tiler.lanes):   # (band, pixels, packed, gathered, frame, stream)
+            self.args.append((tiler.bufs[g].data_ptr(), tiler.bufs[g].numel() // tiler.channels,
+                              self.packed[g].data_ptr() if self.rgb8 else 0,
+                              (self.gpacked[g] if self.rgb8 else tiler.gathered[g]).data_ptr()
+                              if tiler.rank == 0 else 0,
+                              tiler.frames[g].data_ptr() if tiler.rank == 0 else 0,
+                              tiler.part_streams[g][0].cuda_stream))
+
+    def bytes_per_rank(self, tiler) -> int:
+        """Bytes every rank sends per frame."""
+        if self.args is None:
+            self._setup(tiler)
+        px = tiler.rmax * tiler.width
+        return px * 3 if self.rgb8 else px * tiler.channels * tiler.dtype.itemsize
 
     def run(self, tiler, lane: int) -> None:
-        if self.args is None:   # per lane: (band ptr, bytes, gathered ptr, frame ptr, stream)
-            words = tiler.width * tiler.channels * tiler.dtype.itemsize // 4
-            self.words = words
-            self.args = [(tiler.bufs[g].data_ptr(), tiler.bufs[g].numel() * tiler.dtype.itemsize,
-                          tiler.gathered[g].data_ptr() if tiler.rank == 0 else 0,
-                          tiler.frames[g].data_ptr() if tiler.rank == 0 else 0,
-                          tiler.part_streams[g][0].cuda_stream) for g in range(tiler.lanes)]
-        band, nbytes, gath, frame, st = self.args[lane]
-        self.ren.gather_band_async(lane % self.lanes, band, nbytes, gath, st)
+        if self.args is None:
+            self._setup(tiler)
+        band, px, packed, gath, frame, st = self.args[lane]
+        comm = lane % self.lanes
+        if self.rgb8:
+            self.ren.pack_rgb8_async(band, px, packed, st)
+            self.ren.gather_band_async(comm, packed, px * 3, gath, st)
+            if tiler.rank == 0:
+                self.ren.assemble_blocks_rgb8_async(gath, tiler.world, tiler.rmax, tiler.width, tiler.height,
+                                                    tiler.row_block, frame, tiler.width, st)
+            return
+        self.ren.gather_band_async(comm, band, px * tiler.channels * tiler.dtype.itemsize, gath, st)
         if tiler.rank == 0:
             self.ren.assemble_blocks_async(gath, tiler.world, tiler.rmax, self.words, tiler.height,
                                            tiler.row_block, frame, self.words, st)

@@ -237,8 +237,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        if name.startswith("vrt_debug_") and not hasattr(lib, name):
-            continue   # diagnostics may be absent from older A/B variant builds
+        if not hasattr(lib, name) and (name.startswith("vrt_debug_") or os.environ.get("VRT_LIB")):
+            continue   # diagnostics, or an A/B variant build (VRT_LIB) older than this ABI
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

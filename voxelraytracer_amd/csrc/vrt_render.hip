@@ -514,7 +514,10 @@ constexpr float kSkipMargin = 1.0f / 256.0f;
 
 // LEN0Z: the caller guarantees len0 == +0 (the primary ray, voxel.glsl:430), so
 // s = rayLength - ray.rayLength is rayLength itself (x - (+0) == x): one VALU less per step.
-template <bool SHADOW, bool STATS, bool LEN0Z = false>
+// REGSEL: the crossed axis' operands by register selects (8 v_cndmask) instead of the LDS table
+// (2 v_cndmask + a ds_read_b128 whose round trip sits on the step's dependency chain): more VALU,
+// less latency — for waves that run alone (the deferred exact pass), not for full SIMDs
+template <bool SHADOW, bool STATS, bool LEN0Z = false, bool REGSEL = false>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
@@ -591,7 +594,11 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
       const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
       // the crossed axis' entry address straight from the masks: two v_cndmask, no index math
-      const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+      const float4 ae = REGSEL ? make_float4(sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x)),
+                                             sel_mask(mez, dir.z, sel_mask(mey, dir.y, dir.x)),
+                                             sel_mask(mez, rcp.z, sel_mask(mey, rcp.y, rcp.x)),
+                                             sel_mask(mez, step.z, sel_mask(mey, step.y, step.x)))
+                               : lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
       const float ca = pa + s * da;  // == cur on that axis: the same two ops
       const float num = (ca + sa) - pa;
@@ -704,14 +711,27 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #error "VRT_PIPE_K is an A/B knob of make variant builds"
 #endif
 #ifndef VRT_PIPE_K
-#define VRT_PIPE_K 8
+#define VRT_PIPE_K 0
+#endif
+#if defined(VRT_PIPE_KB) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_PIPE_KB is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_PIPE_KB  // block size of the walks inside the bounce stacks (0: skip_walk)
+#define VRT_PIPE_KB VRT_PIPE_K
+#endif
+#if defined(VRT_PIPE_INLANE) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_PIPE_INLANE is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_PIPE_INLANE  // block size of the in-lane exact path of stats-free render_kernel instances
+#define VRT_PIPE_INLANE 0
 #endif
 
 template <bool SHADOW, int KB>
 __device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
-  static_assert(KB >= 2 && KB <= 8, "flag bytes hold at most 8 steps");
+  static_assert(KB >= 2 && KB <= 15, "flag bytes hold at most 8 steps");
+  static_assert(KB <= 8, "flag bytes hold at most 8 steps");
   const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
                      __builtin_copysignf(1.0f, dir.z));
   const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
@@ -862,7 +882,8 @@ __device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 di
 }
 
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant).
-// PIPE: block size of pipe_walk (stats-free instances of the deferred exact pass), 0: skip_walk.
+// PIPE (stats-free instances): bits 0-3 the block size of pipe_walk (0: skip_walk), bit 4 register
+// selects of the crossed axis' operands (skip_walk's REGSEL).
 template <bool STATS, bool LEN0Z = false, int PIPE = 0>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
@@ -870,9 +891,9 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
   static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    if constexpr (PIPE > 0) return pipe_walk<false, PIPE>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    if constexpr ((PIPE & 15) > 0) return pipe_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
     // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
-    return skip_walk<false, STATS, false>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS, false, (PIPE & 16) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -885,8 +906,8 @@ __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len
   int32_t vidx;
   uint32_t v;
   if (__builtin_expect(fast_path_ok(c.sun_n), 1)) {
-    if constexpr (PIPE > 0) return pipe_walk<true, PIPE>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
-    return skip_walk<true, STATS>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    if constexpr ((PIPE & 15) > 0) return pipe_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    return skip_walk<true, STATS, false, (PIPE & 16) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   }
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
@@ -1996,6 +2017,8 @@ constexpr int kMaxStampWaves = 1 << 18;
 __device__ unsigned long long g_stamps[kMaxStampWaves][3];
 // {time after the certified attempt (all lanes reconverged), lanes that took the exact path}
 __device__ unsigned long long g_stamps2[kMaxStampWaves][2];
+// exact_pass_kernel, per workgroup: {start, end, XCC_ID << 32 | HW_ID, pixels | dense << 16}
+__device__ unsigned long long g_stamps4[kMaxStampWaves][4];
 
 __device__ __forceinline__ uint32_t hw_id() {
   uint32_t v;
@@ -2120,7 +2143,7 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
 // Returns whether the pixel ran a bounce stack.
-template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0>
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0, int PIPE_B = PIPE>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
                                             int32_t& hit_vidx, float& hit_len) {
@@ -2177,15 +2200,15 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
         bool settled;
-        h = march_cert<PIPE>(lc, ray, color, settled, k, steps, flags);
+        h = march_cert<PIPE_B>(lc, ray, color, settled, k, steps, flags);
         if (settled) {
           h.found = false;  // a miss or a hit without secondary rays
           continue;
         }
-        shade<STATS, TEX, CSH, PIPE>(lc, ray, h, color, k, steps, flags);
+        shade<STATS, TEX, CSH, PIPE_B>(lc, ray, h, color, k, steps, flags);
         continue;
       }
-      h = trace_with_shadow<STATS, TEX, false, CSH, PIPE>(lc, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH, PIPE_B>(lc, ray, color, k, steps, flags);
     }
 #ifdef VRT_STAMPS
     {
@@ -2306,7 +2329,8 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     } else if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
       heavy = true;
-      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2, STATS ? 0 : VRT_PIPE_INLANE>(a, c, ray, color, k, steps,
+                                                                                     flags, hit_vidx, hit_len);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2));
@@ -2392,7 +2416,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 // under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
 // (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
 // slower, profiles/r03_s67)
-template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K>
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K, int PIPE_B = VRT_PIPE_KB>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t lane = lane_id();
@@ -2412,6 +2436,10 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
   }
   const uint32_t batches = total_d + (total_s + 63u) / 64u;
   if (blockIdx.x >= batches) return;
+#ifdef VRT_STAMPS
+  const unsigned long long xt0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t xlanes = 0;
+#endif
   Ctx c;
   init_ctx(c, a, vox);
   __shared__ float4 ax_tab[64 * 3];
@@ -2441,9 +2469,23 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE, PIPE_B>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
     store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
+#ifdef VRT_STAMPS
+    xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);
+#endif
   }
+#ifdef VRT_STAMPS
+  {
+    const unsigned long long xt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < uint32_t(kMaxStampWaves)) {
+      g_stamps4[blockIdx.x][0] = xt0;
+      g_stamps4[blockIdx.x][1] = xt1;
+      g_stamps4[blockIdx.x][2] = (unsigned long long)xcc_id() << 32 | hw_id();
+      g_stamps4[blockIdx.x][3] = xlanes;
+    }
+  }
+#endif
 }
 
 // Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
@@ -2843,6 +2885,11 @@ int vrt_debug_stamps(uint64_t* out, uint64_t count) {
 int vrt_debug_stamps2(uint64_t* out, uint64_t count) {
   if (!out || count > 2ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps2), count * 8) == hipSuccess ? VRT_OK
+                                                                                     : VRT_ERR_DEVICE;
+}
+int vrt_debug_stamps4(uint64_t* out, uint64_t count) {
+  if (!out || count > 4ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps4), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
 int vrt_debug_stamps3(uint64_t* out, uint64_t count) {

@@ -75,6 +75,12 @@ def main():
            "span_us": round(float(end.max()), 2),
            "wave_us_quantiles": {q: round(float(np.quantile(dur, q)), 2) for q in (0.5, 0.9, 0.99, 1.0)},
            "dense_waves": int((dense > 0).sum()), "pixels": int(px.sum()), "longest": []}
+    for kind, m in (("dense", dense > 0), ("sparse", dense == 0)):
+        if m.any():
+            pr = np.where(prim[m] >= s4[busy[m], 0], (prim[m] - s4[busy[m], 0]).astype(np.float64) * 10e-3, np.nan)
+            out[kind] = {"waves": int(m.sum()),
+                         "wave_us": {q: round(float(np.quantile(dur[m], q)), 2) for q in (0.5, 0.9, 1.0)},
+                         "primary_trace_us": {q: round(float(np.nanquantile(pr, q)), 2) for q in (0.5, 0.9, 1.0)}}
     for i in np.argsort(-dur)[:args.top]:
         p = (float(prim[i] - s4[busy[i], 0]) * 10e-3) if prim[i] >= s4[busy[i], 0] else None
         b = (float(bounce[i] - prim[i]) * 10e-3) if bounce[i] >= prim[i] > 0 else None

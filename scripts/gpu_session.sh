@@ -3,7 +3,7 @@
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
 # steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
-#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
+#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT]] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -48,8 +48,8 @@ for st in "$@"; do
     trace) run trace_${arg:-C3} 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${arg:-C3}" -o run --output-format csv -- \
              python3 "$ROOT/bench.py" --config ${arg:-C3} --steps 20 --warmup 3 --cpu-seconds 0 ;;
     xstamps)  # exact-pass wave timeline (build/diag/libvrt_stamps.so: make variant NAME=stamps DEFS=-DVRT_STAMPS)
-      IFS=, read xc xk <<< "$arg"
-      VRT_LIB=$ROOT/build/diag/libvrt_stamps.so run xstamps_${xc}_k${xk:-1} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} ;;
+      IFS=, read xc xk xv <<< "$arg"
+      VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} ;;
     py) run py_$(echo $arg | tr -c 'a-zA-Z0-9' '_' | cut -c1-40) 600 python -u $arg ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

@@ -234,6 +234,12 @@ BandGeom block_band(int32_t height, int32_t k, int32_t block, int32_t j) {
   if (own > 0 && (nb - 1) % k == j) rows -= nb * block - height;
   return BandGeom{j * block, rows, k * block, sh};
 }
+// rows of the largest of the k bands (band 0 unless it also owns the short last block)
+int32_t largest_band(int32_t height, int32_t k, int32_t block) {
+  int32_t m = 0;
+  for (int32_t j = 0; j < k; ++j) m = std::max(m, block_band(height, k, block, j).rows);
+  return m;
+}
 int32_t frame_block(int32_t k) { return k > 1 ? kFrameRowBlock : 1; }
 int32_t band_rows(int32_t height, int32_t k, int32_t j) { return block_band(height, k, frame_block(k), j).rows; }
 // rows of the largest band (band 0's): every band buffer and the gather's per-device slice
@@ -1610,8 +1616,7 @@ int vrt_assemble_blocks_rgb8_async(vrt_ctx* ctx, const uint8_t* d_bands, int32_t
       frame_pitch % 4 || (reinterpret_cast<uintptr_t>(d_frame) & 15u) || (reinterpret_cast<uintptr_t>(d_bands) & 3u))
     return fail(ctx, VRT_ERR_INVALID,
                 "vrt_assemble_blocks_rgb8_async: width and pitch multiples of 4, 16-byte frame, 4-byte bands");
-  const int32_t nb = (height + row_block - 1) / row_block;
-  if (int64_t((nb + k - 1) / k) * row_block > band_rows_cap)
+  if (largest_band(height, k, row_block) > band_rows_cap)
     return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_rgb8_async: band_rows_cap below the largest band");
   DeviceGuard guard;
   VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
@@ -1630,9 +1635,7 @@ int vrt_assemble_blocks_async(vrt_ctx* ctx, const uint32_t* d_bands, int32_t k, 
   if (sh == 7) return fail(ctx, VRT_ERR_INVALID, "row_block must be a power of two in [1, 64]");
   if (!d_bands || !d_frame || k < 1 || width < 1 || height < 1 || frame_pitch < width)
     return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_async: bad buffers or sizes");
-  // every band must fit its slice: band 0 holds the most rows
-  const int32_t nb = (height + row_block - 1) / row_block;
-  if (int64_t((nb + k - 1) / k) * row_block > band_rows_cap)
+  if (largest_band(height, k, row_block) > band_rows_cap)   // every band must fit its slice
     return fail(ctx, VRT_ERR_INVALID, "vrt_assemble_blocks_async: band_rows_cap below the largest band");
   DeviceGuard guard;
   VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));

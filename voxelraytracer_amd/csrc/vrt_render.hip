@@ -719,6 +719,18 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #ifndef VRT_PIPE_KB  // block size of the walks inside the bounce stacks (0: skip_walk)
 #define VRT_PIPE_KB VRT_PIPE_K
 #endif
+#if defined(VRT_SPEC_SPARSE) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_SPEC_SPARSE is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_SPEC_SPARSE  // walks of the primary trace of the exact pass's sparse batches (32 | M: spec_walk)
+#define VRT_SPEC_SPARSE (32 | 4)
+#endif
+#if defined(VRT_SPARSE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_SPARSE_BATCH is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
+#define VRT_SPARSE_BATCH 64
+#endif
 #if defined(VRT_PIPE_INLANE) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_PIPE_INLANE is an A/B knob of make variant builds"
 #endif
@@ -881,9 +893,207 @@ __device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 di
   return result;
 }
 
+// ------------------------------------------------------- speculative-window exact walk --
+//
+// What bounds the deferred exact pass is its sparse batches: 64 unrelated pixels per wave, each an
+// exact walk of ~110-170 steps (exact_stamps.py: those waves are the pass's longest, 50-70 us, and
+// 90 % of that is the primary walk). skip_walk waits for a sampled step's texel before the next
+// step (its skip distance decides whether that step samples), and with 64 unrelated lanes some lane
+// samples at nearly every step, so the wave pays a cache-miss round trip per step (545 cycles for an
+// Infinity Cache hit, 900 for HBM, MI355X_MICROARCH.md) against ~100 cycles of the step's VALU.
+// pipe_walk (above) issued the loads of every step after a block's first sample and became bound
+// by the misses in flight instead. spec_walk keeps skip_walk's loads — one per sampled step — and
+// stops waiting for them: a lane that samples issues the texel load and goes on for M - 1 more
+// steps as if they lay inside the skip window the texel will open (they do unless the window is
+// short: the octant volume's boxes reach up to 127 cells ahead); M iterations later the texel is
+// there (one load per iteration for the whole wave, so the wait is a static vmcnt(M - 1)) and the
+// lane settles it:
+//  - an event byte: the walk stops at the sampled step — the lane restores the state saved there
+//    (t, len, steps, crossed axis, cell) and leaves, exactly as skip_walk stops there;
+//  - otherwise the texel's window s_lim (skip_walk's formula); if the last speculative step has
+//    s < s_lim, every speculative step lay inside it (s grows with each step) and skip_walk would
+//    have skipped them all; else the lane restores the sampled step's state and steps on from
+//    there with s_lim known, sampling where skip_walk samples.
+// Outside samples stop at once (they read 0; no texel needed); a sampled step that fails the
+// length test waits for its texel and stops (its byte still decides hit or miss). Every step's
+// state update is exact_step's (the reference's ops in order), so state, exit record and step
+// count equal skip_walk's. The caller uses it only when the step cap is out of reach (spec_ok).
+// Lanes that sample nothing issue a dummy load of the volume's first texel (one cache line).
+template <bool SHADOW, int M>
+__device__ __forceinline__ int spec_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
+                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
+                                         int32_t& vidx_out, uint32_t& v_out) {
+  static_assert(M >= 2 && M <= 8, "speculation depth");
+  const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
+                     __builtin_copysignf(1.0f, dir.z));
+  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
+  const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
+  const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
+  c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
+  c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
+  c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
+  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
+  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));
+  const bool skip_ok = SHADOW || medium == 0u;
+  const uint32_t obase =
+      ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
+  const float s_len = c.max_len - len0;
+  f3 t = w.t;
+  float len = w.len;
+  uint32_t it = w.it;
+  bool check = w.check_cube;
+  int result;
+  for (;;) {
+    // loop-top tests of the reference (as skip_walk); the cap cannot be reached (spec_ok)
+    if (!(len < c.max_len)) {
+      result = WALK_MISS;
+      break;
+    }
+    if (check) {
+      const float sc = len - len0;
+      if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
+        result = WALK_MISS;
+        break;
+      }
+    }
+    uint32_t kl = 0;  // this lane's steps of this inner walk
+    uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;
+    int32_t x_vidx = -1;
+    float s_lim = -1.0f;
+    float s_last = 0.0f;  // s of the lane's last step (the speculative steps' largest)
+    // the pending sample: due = the iteration it is settled in (0: none); its step's state
+    uint32_t due = 0u, fin = 0u;  // fin: the sampled step failed the length test (stop when settled)
+    f3 t_cp = t;
+    float len_cp = len;
+    uint32_t kl_cp = 0u, ax_cp = 0u, ci = 0u, cj = 0u, ck = 0u;
+    uint32_t slot[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) slot[j] = 0u;
+    uint32_t iter = 0;  // wave-uniform
+    bool done = false;
+    for (;;) {
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        ++iter;  // iteration iter uses slot j (iter % M == (j + 1) % M, fixed by the unroll)
+        // 1. settle the sample issued M iterations ago, due now
+        if (due == iter) {
+          const uint32_t tex = slot[j];
+          const uint32_t v_raw = tex & kVoxMask, g = tex >> kDistShift;
+          const bool ev = SHADOW ? ((v_raw & ~2u) != 0u) : (v_raw != medium);
+          due = 0u;
+          if (ev | (fin != 0u)) {  // the walk stops at the sampled step
+            t = t_cp;
+            len = len_cp;
+            kl = kl_cp;
+            x_v = v_raw;
+            x_axis = ax_cp;
+            x_out = 0u;
+            x_vidx = int32_t(canonical_index(c, ci, cj, ck));
+            asm volatile("" : "+v"(kl), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
+            done = true;
+          } else {
+            const float fd = float(g) - kSkipMargin;
+            const float lx = __builtin_fmaf(float(ci), rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
+            const float ly = __builtin_fmaf(float(cj), rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
+            const float lz = __builtin_fmaf(float(ck), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
+            const bool open = skip_ok & (v_raw == 0u) & (g >= 2u);
+            s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
+            if (!(s_last < s_lim)) {  // a speculative step left the window: step on from the sample
+              t = t_cp;
+              len = len_cp;
+              kl = kl_cp;
+            }
+          }
+        }
+        // 2. the lane's next step (none after a sampled step that failed the length test)
+        uint32_t addr = 0u;  // the dummy load's texel
+        if (!done && ((fin == 0u) | (due == 0u))) {
+          f3 tp;
+          unsigned long long mey, mez;
+          const float s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
+          ++kl;
+          s_last = s;
+          // 3. a sampled step (none while a sample is pending: its steps are speculative)
+          if ((due == 0u) & !(s < s_lim)) {
+            const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
+            const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
+                              cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
+            const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
+            const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
+            const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
+            const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
+            const uint32_t axis = tp.z == 0.0f ? 2u : (tp.y == 0.0f ? 1u : 0u);
+            if (!inb) {  // outside: reads 0, stop here (TestCube / the caller decide)
+              x_v = 0u;
+              x_out = 1u;
+              x_axis = axis;
+              x_vidx = -1;
+              asm volatile("" : "+v"(kl), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
+              done = true;
+            } else {
+              ci = cvt_flr(qx);
+              cj = cvt_flr(qy);
+              ck = cvt_flr(qz);
+              addr = mad24(mad24(ck, c.p, cj), c.p, ci);
+              due = iter + uint32_t(M);
+              fin = len < c.max_len ? 0u : 1u;
+              t_cp = t;
+              len_cp = len;
+              kl_cp = kl;
+              ax_cp = axis;
+            }
+          }
+        }
+        // 4. one load per iteration for the whole wave: the sample, or the dummy texel
+        slot[j] = load_u16_at(c.vox, addr, obase);
+        if (done) break;
+      }
+      if (done) break;
+      if (iter >= uint32_t(VRT_MAX_STEPS)) {  // unreachable (spec_ok); bounds the loop regardless
+        kl = uint32_t(VRT_MAX_STEPS);
+        x_v = SHADOW ? 0u : medium;
+        x_out = 0u;
+        break;
+      }
+    }
+    it += kl;
+    const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
+    asm volatile("" : "+v"(x_out));
+    check = x_out != 0u;
+    if (event) {
+      axis_out = int(x_axis);
+      vidx_out = x_vidx;
+      v_out = x_v;
+      result = WALK_EVENT;
+      break;
+    }
+    if (it >= uint32_t(VRT_MAX_STEPS)) {
+      result = WALK_CAP;
+      break;
+    }
+  }
+  const float s_end = len - len0;
+  w.t = t;
+  w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
+  w.len = len;
+  w.it = it;
+  w.ties = 0;
+  w.check_cube = check;
+  return result;
+}
+
+// spec_walk needs the step cap out of reach: a walk of parameter length s crosses at most
+// s |d|_1 + 3 planes, and a tie step (two t's zero together) adds at most one zero-length step per
+// crossing, so it takes at most 2 (s |d|_1 + 3) steps; with a wide margin
+__device__ __forceinline__ bool spec_ok(const Ctx& c, const f3 dir, float len, uint32_t it) {
+  const float l1 = __builtin_fabsf(dir.x) + __builtin_fabsf(dir.y) + __builtin_fabsf(dir.z);
+  const float bound = 2.0f * (c.max_len - len) * l1 + 64.0f;
+  return bound < float(VRT_MAX_STEPS / 2) && it < uint32_t(VRT_MAX_STEPS / 2);
+}
+
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant).
 // PIPE (stats-free instances): bits 0-3 the block size of pipe_walk (0: skip_walk), bit 4 register
-// selects of the crossed axis' operands (skip_walk's REGSEL).
+// selects of the crossed axis' operands (skip_walk's REGSEL), bit 5 spec_walk with M = bits 0-3.
 template <bool STATS, bool LEN0Z = false, int PIPE = 0>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
@@ -891,7 +1101,11 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
   static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    if constexpr ((PIPE & 15) > 0) return pipe_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    if constexpr ((PIPE & 32) != 0) {
+      if (spec_ok(c, dir, w.len, w.it)) return spec_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    } else if constexpr ((PIPE & 15) > 0) {
+      return pipe_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    }
     // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
     return skip_walk<false, STATS, false, (PIPE & 16) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
@@ -906,7 +1120,12 @@ __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len
   int32_t vidx;
   uint32_t v;
   if (__builtin_expect(fast_path_ok(c.sun_n), 1)) {
-    if constexpr ((PIPE & 15) > 0) return pipe_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    if constexpr ((PIPE & 32) != 0) {
+      if (spec_ok(c, c.sun_n, w.len, w.it))
+        return spec_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    } else if constexpr ((PIPE & 15) > 0) {
+      return pipe_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    }
     return skip_walk<true, STATS, false, (PIPE & 16) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   }
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
@@ -2143,14 +2362,19 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
 // Returns whether the pixel ran a bounce stack.
-template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0, int PIPE_B = PIPE>
+// PIPE / PIPE_B: walks of the primary trace / of the bounce stack (walk_ray's code); PIPE_P: the
+// primary trace's walks when alt_primary (the exact pass's sparse batches: spec_walk)
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0, int PIPE_B = PIPE,
+          int PIPE_P = PIPE>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
-                                            int32_t& hit_vidx, float& hit_len) {
+                                            int32_t& hit_vidx, float& hit_len, bool alt_primary = false) {
   StackRay stack[kMaxStack - 1];  // the top entry lives in `ray`
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE>(c, ray, color, k, steps, flags);
+  Hit h0;
+  if (PIPE_P != PIPE && alt_primary) h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE_P>(c, ray, color, k, steps, flags);
+  else h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE>(c, ray, color, k, steps, flags);
 #ifdef VRT_STAMPS
   const uint32_t st_wave = blockIdx.x * kWgWaves + (threadIdx.x >> 6);
   {
@@ -2416,26 +2640,32 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 // under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
 // (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
 // slower, profiles/r03_s67)
-template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K, int PIPE_B = VRT_PIPE_KB>
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K, int PIPE_B = VRT_PIPE_KB,
+          int PIPE_P = VRT_SPEC_SPARSE>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
-  const uint32_t lane = lane_id();
   const uint32_t* ctr = a.defer;
-  if (blockIdx.x == 0 && lane < 2u * kOrdClasses)  // both kinds of the other set, for the next launch
-    a.defer[(((lane / kOrdClasses) * 2u + (a.defer_e ^ 1u)) * kOrdClasses + lane % kOrdClasses) * kOrdCtrStride] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < 2u * kOrdClasses) {  // both kinds of the other set, for the next launch
+    const uint32_t l = threadIdx.x;
+    a.defer[(((l / kOrdClasses) * 2u + (a.defer_e ^ 1u)) * kOrdClasses + l % kOrdClasses) * kOrdCtrStride] = 0u;
+  }
 #ifdef VRT_DIAG_SKIP_EXACT  // diagnostic bound (wrong images): the frame without its deferred pixels
   return;
 #endif
   uint32_t ns[kOrdClasses], nd[kOrdClasses], total_s = 0, total_d = 0;
 #pragma unroll
   for (uint32_t q = 0; q < kOrdClasses; ++q) {
-    ns[q] = ctr[(a.defer_e * kOrdClasses + q) * kOrdCtrStride];
-    nd[q] = ctr[((2u + a.defer_e) * kOrdClasses + q) * kOrdCtrStride];
+    // wave-uniform: kept in SGPRs (as VGPRs they were spilled to scratch by every workgroup,
+    // idle ones included, before the early exit below)
+    ns[q] = uint32_t(__builtin_amdgcn_readfirstlane(int(ctr[(a.defer_e * kOrdClasses + q) * kOrdCtrStride])));
+    nd[q] = uint32_t(__builtin_amdgcn_readfirstlane(int(ctr[((2u + a.defer_e) * kOrdClasses + q) * kOrdCtrStride])));
     total_s += ns[q];
     total_d += nd[q];
   }
-  const uint32_t batches = total_d + (total_s + 63u) / 64u;
-  if (blockIdx.x >= batches) return;
+  constexpr uint32_t SB = VRT_SPARSE_BATCH;  // pixels of a sparse batch (lanes SB.. idle)
+  const uint32_t batches = total_d + (total_s + SB - 1u) / SB;
+  if (blockIdx.x >= batches) return;  // idle workgroups leave before touching scratch
+  const uint32_t lane = lane_id();
 #ifdef VRT_STAMPS
   const unsigned long long xt0 = __builtin_amdgcn_s_memrealtime();
   uint32_t xlanes = 0;
@@ -2447,8 +2677,8 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
   for (uint32_t b = blockIdx.x; b < batches; b += gridDim.x) {
     // batch b: dense chunk b (in segment order), else sparse entries [64 (b - total_d), + 64)
     const bool dense = b < total_d;
-    uint32_t idx = dense ? b : (b - total_d) * 64u + lane;
-    if (!dense && idx >= total_s) continue;
+    uint32_t idx = dense ? b : (b - total_d) * SB + lane;
+    if (!dense && (lane >= SB || idx >= total_s)) continue;
     uint32_t seg = 0;
 #pragma unroll
     for (uint32_t q = 0; q + 1u < kOrdClasses; ++q) {
@@ -2469,7 +2699,9 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE, PIPE_B>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    // sparse batches (64 unrelated pixels) walk their primaries speculatively (spec_walk)
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE, PIPE_B, PIPE_P>(a, c, ray, color, k, steps, flags,
+                                                                                    hit_vidx, hit_len, !dense);
     store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
 #ifdef VRT_STAMPS
     xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);

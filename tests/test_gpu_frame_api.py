@@ -5,9 +5,9 @@ row parts on two context-owned streams with the fast (certified, uncounted) inst
 alone (vrt_stats.kernel_ms) no longer selects the exact-walk instance, counting does
 (VRT_STATS_COUNTERS). Checked here:
   - frames are bit-identical to the exact instance's, over consecutive frames with alpha < 1;
-  - a context over a device list splits the frame into cyclic row bands (vrt_create_devices with
-    a repeated ordinal rehearses a k-device split on one GPU): identical frames, float frames and
-    hit records;
+  - a context over a device list splits the frame into 16-row block-cyclic bands (ABI v12;
+    vrt_create_devices with a repeated ordinal rehearses a k-device split on one GPU; 121 rows:
+    a short last block): identical frames, float frames and hit records;
   - vrt_render_frame_device assembles the same frame on the first device;
   - the C++ host (examples/headless_app.cpp) gets the bench's per-frame GPU time through the ABI.
 The RCCL paths (ncclBroadcast of the volume, ncclGather of the bands) between distinct GPUs need

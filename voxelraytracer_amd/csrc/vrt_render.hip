@@ -511,13 +511,22 @@ static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
 constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F (G = F - 1 in 8 bits): 128 vs 64 C4 -1.4 %, C1-C3 +-0.3 % (r03_s42)
 static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
+constexpr float kPfAhead = 2.0f;   // prefetch lead without a skip window (ray-parameter units)
+constexpr float kPfPast = 0.5f;    // prefetch point past a window's end
 
 // LEN0Z: the caller guarantees len0 == +0 (the primary ray, voxel.glsl:430), so
 // s = rayLength - ray.rayLength is rayLength itself (x - (+0) == x): one VALU less per step.
 // REGSEL: the crossed axis' operands by register selects (8 v_cndmask) instead of the LDS table
 // (2 v_cndmask + a ds_read_b128 whose round trip sits on the step's dependency chain): more VALU,
 // less latency — for waves that run alone (the deferred exact pass), not for full SIMDs
-template <bool SHADOW, bool STATS, bool LEN0Z = false, bool REGSEL = false>
+// PF: software prefetch of the next sample's texel line (the exact pass's sparse batches, whose
+// 64 unrelated lanes make the wave wait for some lane's texel at nearly every step): each sampled
+// step also loads the texel where the lane's next sample will land — just past the window it opens,
+// or kPfAhead further along the ray without a window — so that sample finds its line in L2 / L1
+// rather than paying an Infinity Cache / HBM round trip. The prefetched value is only folded into
+// a sink at the lane's next sampled step, after that step's own load returned (loads return in
+// order), so the prefetch never adds a wait.
+template <bool SHADOW, bool STATS, bool LEN0Z = false, bool REGSEL = false, bool PF = false>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
@@ -550,6 +559,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   bool check = w.check_cube;
   int result;
   constexpr uint32_t kOutside = 0x100u;
+  [[maybe_unused]] uint32_t pf = 0u, pf_sink = 0u;  // PF: the pending prefetch's texel, and the sink it is folded into
   for (;;) {
     // loop-top tests of the reference, in its order: length, TestCube, then our step cap.
     // check is only set after an outside sample; currentPos is that step's (len unchanged since),
@@ -630,6 +640,14 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const float lz = __builtin_fmaf(float(vk), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
         const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
         s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
+        if constexpr (PF) {
+          pf_sink += pf;  // the previous prefetch: issued before this step's load, so it is back
+          const float sp = open ? s_lim + kPfPast : s + kPfAhead;
+          const uint32_t fi = cvt_flr(__builtin_amdgcn_fmed3f(pos.x + sp * dir.x, 0.0f, c.fn));
+          const uint32_t fj = cvt_flr(__builtin_amdgcn_fmed3f(pos.y + sp * dir.y, 0.0f, c.fn));
+          const uint32_t fk = cvt_flr(__builtin_amdgcn_fmed3f(pos.z + sp * dir.z, 0.0f, c.fn));
+          pf = load_u16_at(c.vox, mad24(mad24(fk, c.p, fj), c.p, fi), obase);
+        }
         // stop the inner loop on: outside sample, a byte that is an event, the length. Only a
         // sampled step can stop it: a skipped one reads an empty in-volume texel and has
         // s < s_len, hence len < max_len (see s_len).
@@ -659,6 +677,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       break;
     }
   }
+  if constexpr (PF) asm volatile("" ::"v"(pf_sink), "v"(pf));  // keeps the prefetches
   const float s_end = LEN0Z ? len : len - len0;  // currentPos of the last step (the hit point on an event)
   w.t = t;
   w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
@@ -690,16 +709,27 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
 // One exact DDA step (voxel.glsl:275-281 / :323-327, then the crossed axis' t, :296 / :381) with the
 // crossed axis' operands from the lane's LDS table: skip_walk's step, factored for pipe_walk's
 // main and replay loops (identical ops). Returns s = len - len0; tp, mey, mez as in skip_walk.
+// REGSEL: the operands by register selects (AX: pos, dir, rcp, step per axis) instead of the table.
+template <bool REGSEL = false>
 __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0, const uint32_t ax_a0,
                                             const uint32_t ax_a1, const uint32_t ax_a2, f3& tp,
-                                            unsigned long long& mey, unsigned long long& mez) {
+                                            unsigned long long& mey, unsigned long long& mez,
+                                            const float4* AX = nullptr) {
   const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
   tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
   len += tmin;
   const float s = len - len0;
   mey = __builtin_amdgcn_ballot_w64(tp.y == 0.0f);
   mez = __builtin_amdgcn_ballot_w64(tp.z == 0.0f);
-  const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+  float4 ae;
+  if constexpr (REGSEL) {
+    ae = make_float4(sel_mask(mez, AX[2].x, sel_mask(mey, AX[1].x, AX[0].x)),
+                     sel_mask(mez, AX[2].y, sel_mask(mey, AX[1].y, AX[0].y)),
+                     sel_mask(mez, AX[2].z, sel_mask(mey, AX[1].z, AX[0].z)),
+                     sel_mask(mez, AX[2].w, sel_mask(mey, AX[1].w, AX[0].w)));
+  } else {
+    ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+  }
   const float ca = ae.x + s * ae.y;
   const float num = (ca + ae.w) - ae.x;
   const float q = div_rn(num, ae.y, ae.z) - s;
@@ -723,7 +753,7 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #error "VRT_SPEC_SPARSE is an A/B knob of make variant builds"
 #endif
 #ifndef VRT_SPEC_SPARSE  // walks of the primary trace of the exact pass's sparse batches (32 | M: spec_walk)
-#define VRT_SPEC_SPARSE (32 | 4)
+#define VRT_SPEC_SPARSE 0
 #endif
 #if defined(VRT_SPARSE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_SPARSE_BATCH is an A/B knob of make variant builds"
@@ -764,6 +794,7 @@ __device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 di
   bool check = w.check_cube;
   int result;
   constexpr uint32_t kOutside = 0x100u;
+  [[maybe_unused]] uint32_t pf = 0u, pf_sink = 0u;  // PF: the pending prefetch's texel, and the sink it is folded into
   for (;;) {
     // loop-top tests of the reference (as skip_walk)
     if (!(len < c.max_len)) {
@@ -919,11 +950,14 @@ __device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 di
 // state update is exact_step's (the reference's ops in order), so state, exit record and step
 // count equal skip_walk's. The caller uses it only when the step cap is out of reach (spec_ok).
 // Lanes that sample nothing issue a dummy load of the volume's first texel (one cache line).
-template <bool SHADOW, int M>
+template <bool SHADOW, int M, bool REGSEL = false>
 __device__ __forceinline__ int spec_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
   static_assert(M >= 2 && M <= 8, "speculation depth");
+  const float4 AX[3] = {make_float4(pos.x, dir.x, rcp.x, __builtin_copysignf(1.0f, dir.x)),
+                        make_float4(pos.y, dir.y, rcp.y, __builtin_copysignf(1.0f, dir.y)),
+                        make_float4(pos.z, dir.z, rcp.z, __builtin_copysignf(1.0f, dir.z))};
   const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
                      __builtin_copysignf(1.0f, dir.z));
   const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
@@ -1010,7 +1044,7 @@ __device__ __forceinline__ int spec_walk(const Ctx& c, const f3 pos, const f3 di
         if (!done && ((fin == 0u) | (due == 0u))) {
           f3 tp;
           unsigned long long mey, mez;
-          const float s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
+          const float s = exact_step<REGSEL>(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez, AX);
           ++kl;
           s_last = s;
           // 3. a sampled step (none while a sample is pending: its steps are speculative)
@@ -1093,7 +1127,8 @@ __device__ __forceinline__ bool spec_ok(const Ctx& c, const f3 dir, float len, u
 
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant).
 // PIPE (stats-free instances): bits 0-3 the block size of pipe_walk (0: skip_walk), bit 4 register
-// selects of the crossed axis' operands (skip_walk's REGSEL), bit 5 spec_walk with M = bits 0-3.
+// selects of the crossed axis' operands (skip_walk's REGSEL), bit 5 spec_walk with M = bits 0-3,
+// bit 6 skip_walk's texel prefetch (PF).
 template <bool STATS, bool LEN0Z = false, int PIPE = 0>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
@@ -1102,12 +1137,12 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
     if constexpr ((PIPE & 32) != 0) {
-      if (spec_ok(c, dir, w.len, w.it)) return spec_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+      if (spec_ok(c, dir, w.len, w.it)) return spec_walk<false, PIPE & 15, (PIPE & 16) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
     } else if constexpr ((PIPE & 15) > 0) {
       return pipe_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
     }
     // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
-    return skip_walk<false, STATS, false, (PIPE & 16) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS, false, (PIPE & 16) != 0, (PIPE & 64) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -1122,11 +1157,11 @@ __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len
   if (__builtin_expect(fast_path_ok(c.sun_n), 1)) {
     if constexpr ((PIPE & 32) != 0) {
       if (spec_ok(c, c.sun_n, w.len, w.it))
-        return spec_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+        return spec_walk<true, PIPE & 15, (PIPE & 16) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
     } else if constexpr ((PIPE & 15) > 0) {
       return pipe_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
     }
-    return skip_walk<true, STATS, false, (PIPE & 16) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
+    return skip_walk<true, STATS, false, (PIPE & 16) != 0, (PIPE & 64) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   }
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }

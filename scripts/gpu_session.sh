@@ -3,7 +3,7 @@
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
 # steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
-#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT]] | trace[:CFG] | stamps[:CFGS] | py:<script args...> (quoted)
+#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT]] | trace[:CFG] | strong[:CFG] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -50,6 +50,14 @@ for st in "$@"; do
     xstamps)  # exact-pass wave timeline (build/diag/libvrt_stamps.so: make variant NAME=stamps DEFS=-DVRT_STAMPS)
       IFS=, read xc xk xv <<< "$arg"
       VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} ;;
+    strong)  # strong-scaling rehearsal: every rank's band of the K-way split for K = 2, 4, 8
+      for k in 2 4 8; do
+        for ((r = 0; r < k; r++)); do
+          TAILN=0 run strong_${arg:-C3}_k${k}_r$r 200 python bench.py --config ${arg:-C3} --rehearse-ranks $k \
+            --rehearse-rank $r --steps 400 --warmup 100 --cpu-seconds 0 --no-verify
+          echo "strong ${arg:-C3} k$k r$r $(grep -o '"kernel_ms": [0-9.]*' $OUT/strong_${arg:-C3}_k${k}_r$r.log | head -1)"
+        done
+      done ;;
     py) run py_$(echo $arg | tr -c 'a-zA-Z0-9' '_' | cut -c1-40) 600 python -u $arg ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

@@ -755,11 +755,14 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #ifndef VRT_SPEC_SPARSE  // walks of the primary trace of the exact pass's sparse batches (32 | M: spec_walk)
 #define VRT_SPEC_SPARSE 0
 #endif
-#if defined(VRT_SPARSE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
+#if (defined(VRT_SPARSE_BATCH) || defined(VRT_SPARSE_BATCH_FAT)) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_SPARSE_BATCH is an A/B knob of make variant builds"
 #endif
 #ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
 #define VRT_SPARSE_BATCH 64
+#endif
+#ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
+#define VRT_SPARSE_BATCH_FAT 16
 #endif
 #if defined(VRT_PIPE_INLANE) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_PIPE_INLANE is an A/B knob of make variant builds"
@@ -2675,8 +2678,12 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 // under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
 // (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
 // slower, profiles/r03_s67)
+// SB: pixels per sparse batch. 64 for whole frames; 16 in the 4-wave instance of short bands,
+// whose frame time includes this pass's span: a sparse wave's span is its slowest walk, and a lone
+// wave's walks cost the same per step with 16 lanes as with 64 (C4 k = 8 band 0.0222 -> 0.0200 ms,
+// exact-pass span 58 -> 49 us; whole frames +1-3 %: more waves, profiles/r04_exact/)
 template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K, int PIPE_B = VRT_PIPE_KB,
-          int PIPE_P = VRT_SPEC_SPARSE>
+          int PIPE_P = VRT_SPEC_SPARSE, uint32_t SB = VRT_SPARSE_BATCH>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t* ctr = a.defer;
@@ -2697,7 +2704,7 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     total_s += ns[q];
     total_d += nd[q];
   }
-  constexpr uint32_t SB = VRT_SPARSE_BATCH;  // pixels of a sparse batch (lanes SB.. idle)
+  static_assert(SB >= 1 && SB <= 64, "lanes SB.. of a sparse batch idle");
   const uint32_t batches = total_d + (total_s + SB - 1u) / SB;
   if (blockIdx.x >= batches) return;  // idle workgroups leave before touching scratch
   const uint32_t lane = lane_id();
@@ -3026,7 +3033,8 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1>
-                         : (a.exact_fat ? exact_pass_kernel<false, 2, 4> : exact_pass_kernel<false, 2>);
+                         : (a.exact_fat ? exact_pass_kernel<false, 2, 4, VRT_PIPE_K, VRT_PIPE_KB, VRT_SPEC_SPARSE, VRT_SPARSE_BATCH_FAT>
+                                       : exact_pass_kernel<false, 2>);
     if (ev_begin)
       hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);
     else

@@ -3,7 +3,7 @@
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
 # steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
-#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT]] | trace[:CFG] | strong[:CFG] | py:<script args...> (quoted)
+#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT[,RANK]]] | trace[:CFG] | strong[:CFG] | drvab[:CFG[,ROUNDS]] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -48,8 +48,18 @@ for st in "$@"; do
     trace) run trace_${arg:-C3} 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${arg:-C3}" -o run --output-format csv -- \
              python3 "$ROOT/bench.py" --config ${arg:-C3} --steps 20 --warmup 3 --cpu-seconds 0 ;;
     xstamps)  # exact-pass wave timeline (build/diag/libvrt_stamps.so: make variant NAME=stamps DEFS=-DVRT_STAMPS)
-      IFS=, read xc xk xv <<< "$arg"
-      VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} ;;
+      IFS=, read xc xk xv xr <<< "$arg"
+      VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1}_r${xr:-0} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} --rank ${xr:-0} ;;
+    drvab)  # the driver's 20-frame command, ROUNDS alternating rounds over base + build/variants/*.so
+      IFS=, read dc dr <<< "$arg"
+      for ((i = 1; i <= ${dr:-4}; i++)); do
+        for lib in $(libs); do
+          ln=$(basename $lib .so)
+          if [ $lib = base ]; then unset VRT_LIB; else export VRT_LIB=$ROOT/$lib; fi
+          TAILN=0 run drvab_${ln}_${dc:-C3}_$i 120 python bench.py --config ${dc:-C3} --steps 20 --warmup 5 --cpu-seconds 0 --no-verify
+          echo "drvab ${ln} ${dc:-C3} $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/drvab_${ln}_${dc:-C3}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/drvab_${ln}_${dc:-C3}_$i.log | head -1)"
+        done
+      done; unset VRT_LIB ;;
     strong)  # strong-scaling rehearsal: every rank's band of the K-way split for K = 2, 4, 8
       for k in 2 4 8; do
         for ((r = 0; r < k; r++)); do

@@ -761,6 +761,16 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
 #define VRT_SPARSE_BATCH 64
 #endif
+#if defined(VRT_EXACT_PRIO) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_EXACT_PRIO is an A/B knob of make variant builds"
+#endif
+// wave priority of the whole exact pass (0: only its bounce stacks raise it): its few long waves
+// share SIMDs with the next frames' certified waves; at 2 their chains issue first (C3 0.0395 ->
+// 0.0387 ms per frame, C4 -1 %, the driver's 20-frame run 0.0531 -> 0.0509; 3: C3 0.0389,
+// profiles/r04_exact/)
+#ifndef VRT_EXACT_PRIO
+#define VRT_EXACT_PRIO 2
+#endif
 #ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
 #define VRT_SPARSE_BATCH_FAT 16
 #endif
@@ -2707,6 +2717,7 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
   static_assert(SB >= 1 && SB <= 64, "lanes SB.. of a sparse batch idle");
   const uint32_t batches = total_d + (total_s + SB - 1u) / SB;
   if (blockIdx.x >= batches) return;  // idle workgroups leave before touching scratch
+  if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
   const uint32_t lane = lane_id();
 #ifdef VRT_STAMPS
   const unsigned long long xt0 = __builtin_amdgcn_s_memrealtime();

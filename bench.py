@@ -470,7 +470,8 @@ def main():
             tiler.frame()
             if events:
                 e = torch.cuda.Event(enable_timing=True)
-                e.record(lane_st[(i_ % tiler.lanes) * len(tiler.specs) % len(lane_st)])
+                # on the stream of the frame just enqueued (its lane counts the warm-up frames too)
+                e.record(tiler.part_streams[(tiler.k - 1) % tiler.lanes][-1])
                 fev_.append(e)
         for e, st in zip(ev1, lane_st):
             e.record(st)

@@ -771,6 +771,12 @@ __device__ __forceinline__ float exact_step(f3& t, float& len, const float len0,
 #ifndef VRT_EXACT_PRIO
 #define VRT_EXACT_PRIO 2
 #endif
+#if defined(VRT_FORCE_FAT) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_FORCE_FAT is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_FORCE_FAT  // the 4-wave exact-pass instance for every colour-only band (A/B only)
+#define VRT_FORCE_FAT 0
+#endif
 #ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
 #define VRT_SPARSE_BATCH_FAT 16
 #endif
@@ -3044,7 +3050,7 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1>
-                         : (a.exact_fat ? exact_pass_kernel<false, 2, 4, VRT_PIPE_K, VRT_PIPE_KB, VRT_SPEC_SPARSE, VRT_SPARSE_BATCH_FAT>
+                         : ((a.exact_fat || VRT_FORCE_FAT) ? exact_pass_kernel<false, 2, 4, VRT_PIPE_K, VRT_PIPE_KB, VRT_SPEC_SPARSE, VRT_SPARSE_BATCH_FAT>
                                        : exact_pass_kernel<false, 2>);
     if (ev_begin)
       hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);

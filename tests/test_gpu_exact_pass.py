@@ -2,7 +2,9 @@
 its certified walks settle and appends the others to a list (per wave a ballot of the deferred
 lanes, one atomicAdd on one of 8 XCD-local segment counters, mbcnt ranks; waves with >= 32
 deferred pixels keep an 8x8 chunk in lane order); a second kernel renders the list with the exact
-path 64 pixels to a wave (round 4: its walks pipelined in blocks of 8 steps). Images must be bit-identical
+path, a chunk or a batch of list entries to a wave (these band sizes are under four dispatch rounds:
+the 4-wave instance with 16-pixel sparse batches; whole frames, 64-pixel batches at 7 waves, are
+checked frame by frame in test_gpu_bench_path.py). Images must be bit-identical
 to the in-lane fallback and to the exact STATS instance, frame after frame, on scenes where many
 pixels defer (glass cube: most pixels; random sparse volumes with every byte; near-edge cameras)
 and with the temporal filter reading its history (alpha 0.5), including bands (row steps),

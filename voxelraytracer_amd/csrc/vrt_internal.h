@@ -91,6 +91,13 @@ constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave
 // batches beyond it): 8 covers textured frames' deferred pixels in one batch per workgroup (textured
 // C3 0.0843 -> 0.0713 ms against 32; 4 no better; profiles/r03_s11, r03_s12)
 constexpr uint32_t kDeferGridDiv = VRT_DEFER_GRID_DIV;
+#if defined(VRT_DEFER_GRID_DIV_COLOR) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEFER_GRID_DIV_COLOR is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_DEFER_GRID_DIV_COLOR
+#define VRT_DEFER_GRID_DIV_COLOR VRT_DEFER_GRID_DIV
+#endif
+constexpr uint32_t kDeferGridDivColor = VRT_DEFER_GRID_DIV_COLOR;  // the same for colour-only frames
 
 // ---- launches (vrt_render.hip); all asynchronous on `s` ------------------------------------
 

@@ -3044,9 +3044,9 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     // certified pass, then the exact pass over the pixels it deferred (no tile order: the
     // certified pass has no long waves)
 #ifdef VRT_TPW
-    const dim3 g1((a.tiles + VRT_TPW - 1) / VRT_TPW), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+    const dim3 g1((a.tiles + VRT_TPW - 1) / VRT_TPW), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #else
-    const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / kDeferGridDiv));
+    const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1>

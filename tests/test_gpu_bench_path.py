@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_path_c3_three_frames(built, alpha):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C3", "--steps", "20",
            "--warmup", "5", "--alpha", str(alpha), "--verify-frames", "3", "--cpu-seconds", "0",
-           "--oracle-check"]
+           "--oracle-check", "--frame-events"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -37,6 +37,10 @@ def test_bench_path_c3_three_frames(built, alpha):
     assert v["verified"] and v["mismatched_elements"] == 0 and out["verified"]
     oc = out["oracle_check"]
     assert oc["frames"] == 3 and oc["ok"] and oc["max_lsb"] <= 1
+    # per-frame completion events on each frame's own stream: one per frame, each after the
+    # lanes' start and by the end of the timed frames
+    ev = out["frame_events_ms"]
+    assert len(ev) == 20 and all(0 < e <= 20 * out["roofline"]["kernel_ms"] * 1.01 + 1e-3 for e in ev)
     # alpha 1: frames independent, four in flight (lanes); else one lane of two parts in place
     par = out["config"]["parallelism"]
     if alpha == 1.0:

@@ -82,6 +82,8 @@ struct OrderSlot {
   bool last_defer = false;     // the slot's last launch was a deferred-pass launch
   uint32_t* defer = nullptr;   // the deferred pass's counters + list (lazily allocated)
   size_t defer_cap = 0;        // its words
+  uint32_t* h_batches = nullptr;  // host-mapped: an earlier exact pass's batch count (~0u: none)
+  uint32_t* d_batches = nullptr;  // its device address
 };
 
 struct Shard {
@@ -286,7 +288,10 @@ void shard_free(Shard& s) {
   std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats,
                              (void*)s.d_cnt, (void*)s.d_cnt_rep, (void*)s.d_out, (void*)s.d_hit,
                              (void*)s.d_atlas, (void*)s.d_order_pool};
-  for (OrderSlot& o : s.order) bufs.push_back(o.defer);
+  for (OrderSlot& o : s.order) {
+    bufs.push_back(o.defer);
+    if (o.h_batches) (void)hipHostFree(o.h_batches);
+  }
   for (int r = 0; r < kRing; ++r) {
     bufs.push_back(s.d_ring[r]);
     bufs.push_back(s.d_rawbuf[r]);
@@ -436,6 +441,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.defer = nullptr;
   a.defer_e = a.defer_seg = 0;
   a.exact_fat = 0;
+  a.exact_grid = 0;
+  a.batches_out = nullptr;
   return a;
 }
 
@@ -522,6 +529,26 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
     a.defer_seg = uint32_t((a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * uint32_t(vrt::kWgThreads);
     // bands of under 4 rounds: the exact pass's latency follows a short certified pass
     a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
+    if (VRT_EXACT_GRID_ADAPT) {
+      // the grid from an earlier frame's batch count on this slot (frames in flight: a few frames
+      // old) plus a margin; a larger frame loops its workgroups over the rest. Idle workgroups
+      // are not free: each waits for a register and LDS slot among the next frames' waves.
+      if (!slot->h_batches) {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+          slot->h_batches = static_cast<uint32_t*>(h);
+          *slot->h_batches = ~0u;
+          void* d = nullptr;
+          if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) slot->d_batches = static_cast<uint32_t*>(d);
+        }
+      }
+      if (slot->d_batches) {
+        const uint32_t full = std::max(64u, a.tiles * uint32_t(vrt::kWgWaves) / vrt::kDeferGridDiv);
+        const uint32_t prev = *static_cast<volatile uint32_t*>(slot->h_batches);
+        a.batches_out = slot->d_batches;
+        if (prev != ~0u) a.exact_grid = std::min(full, std::max(64u, prev + prev / 4u + 64u));
+      }
+    }
     slot->defer_epoch++;
     slot->last_defer = true;
     return;

@@ -57,7 +57,17 @@ struct KArgs {
   uint32_t* defer;
   uint32_t defer_e, defer_seg;
   int32_t exact_fat;  // the exact pass's 4-wave instance (colour-only bands of < 4 rounds of waves)
+  // adaptive exact-pass grid (VRT_EXACT_GRID_ADAPT): workgroups of this launch's exact pass (0: the
+  // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
+  uint32_t exact_grid;
+  uint32_t* batches_out;
 };
+#if defined(VRT_EXACT_GRID_ADAPT) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_EXACT_GRID_ADAPT is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_EXACT_GRID_ADAPT
+#define VRT_EXACT_GRID_ADAPT 1
+#endif
 
 // Waves per workgroup, each rendering an 8x8 pixel tile. Two (a 16x8 tile): a finished
 // workgroup frees its slots two waves at a time, so the dispatcher refills them sooner than with

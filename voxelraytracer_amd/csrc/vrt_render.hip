@@ -2722,6 +2722,8 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
   }
   static_assert(SB >= 1 && SB <= 64, "lanes SB.. of a sparse batch idle");
   const uint32_t batches = total_d + (total_s + SB - 1u) / SB;
+  if (VRT_EXACT_GRID_ADAPT && a.batches_out && blockIdx.x == 0 && threadIdx.x == 0)
+    *a.batches_out = batches;  // for the grid of a later launch on this slot (host-mapped word)
   if (blockIdx.x >= batches) return;  // idle workgroups leave before touching scratch
   if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
   const uint32_t lane = lane_id();
@@ -3046,7 +3048,9 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
 #ifdef VRT_TPW
     const dim3 g1((a.tiles + VRT_TPW - 1) / VRT_TPW), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #else
-    const dim3 g1(a.tiles), g2(std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
+    const dim3 g1(a.tiles),
+        g2(a.exact_grid ? a.exact_grid
+                        : std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1>

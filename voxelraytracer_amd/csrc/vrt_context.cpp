@@ -529,10 +529,12 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
     a.defer_seg = uint32_t((a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * uint32_t(vrt::kWgThreads);
     // bands of under 4 rounds: the exact pass's latency follows a short certified pass
     a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
-    if (VRT_EXACT_GRID_ADAPT) {
+    if (VRT_EXACT_GRID_ADAPT && !a.exact_fat) {
       // the grid from an earlier frame's batch count on this slot (frames in flight: a few frames
       // old) plus a margin; a larger frame loops its workgroups over the rest. Idle workgroups
-      // are not free: each waits for a register and LDS slot among the next frames' waves.
+      // are not free: each waits for a register and LDS slot among the next frames' waves. Not for
+      // short bands, whose frame time is this pass's span (C4 8-way band 0.0196 -> 0.0200 ms with
+      // it, profiles/r04_s26)
       if (!slot->h_batches) {
         void* h = nullptr;
         if (hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {

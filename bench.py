@@ -14,7 +14,7 @@ Frames in flight: at u_Alpha = 1 (the slider default) a frame does not read its 
 consecutive frames are independent; the timed frames rotate over --lanes (default 4) lanes, each
 with its own HIP stream and output buffer, so up to four frames are in flight and the next frames'
 waves fill the wave slots one frame's longest (exact-path) waves hold (voxelraytracer_amd/tiles.py;
-scripts/diag/strong_pipe.py). At u_Alpha != 1 frames depend on their history: one lane, two
+profiles/r03_pipe). At u_Alpha != 1 frames depend on their history: one lane, two
 interleaved row parts on two streams, filtered in place (the round-2 scheme).
 
 Multi-GPU (one process per GPU, torchrun): voxelraytracer_amd/tiles.py splits the frame into
@@ -134,10 +134,10 @@ def parse():
                     help="N > 1: keep the bands on their ranks in the timed frames (no per-frame "
                          "gather; one gather of the last frame after the timed region); default: "
                          "every frame gathered to rank 0 and assembled there inside the timed region")
-    ap.add_argument("--watchdog-s", type=float, default=0.0,
-                    help="dump every thread's Python stack to stderr after this many seconds if the "
-                         "run is still going (0: off; the two-rank GPU test sets it). SIGUSR1 dumps "
-                         "them at any time")
+    ap.add_argument("--watchdog-s", type=float, default=-1.0,
+                    help="dump every thread's Python stack to stderr and exit non-zero after this "
+                         "many seconds if the run is still going (0: off; default -1: 300 s when "
+                         "WORLD_SIZE > 1, off for one process). SIGUSR1 dumps the stacks at any time")
     ap.add_argument("--pre-idle-ms", type=float, default=0.0,
                     help="diagnostic: idle the synchronised device this long before the timed "
                          "region (clock-ramp experiments)")
@@ -269,9 +269,13 @@ def main():
     # (the two-rank test sends it before killing the job) and after --watchdog-s
     faulthandler.enable()
     faulthandler.register(signal.SIGUSR1, all_threads=True)
-    if args.watchdog_s > 0:
-        faulthandler.dump_traceback_later(args.watchdog_s, exit=False)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # multi-rank runs are bounded by default: a hang (a collective that never completes) ends the
+    # process with every thread's stack on stderr and a non-zero exit, never a silent wait or an
+    # in-place restart
+    watchdog_s = args.watchdog_s if args.watchdog_s >= 0 else (300.0 if world > 1 else 0.0)
+    if watchdog_s > 0:
+        faulthandler.dump_traceback_later(watchdog_s, exit=True)
     lanes, queues = pipeline_shape(args, world)
     if args.queues or queues != 4:   # before HIP initialises (the GPU box exports 4)
         os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
@@ -469,10 +473,16 @@ def main():
         for i_ in range(steps):
             tiler.frame()
             if events:
-                e = torch.cuda.Event(enable_timing=True)
-                # on the stream of the frame just enqueued (its lane counts the warm-up frames too)
-                e.record(tiler.part_streams[(tiler.k - 1) % tiler.lanes][-1])
-                fev_.append(e)
+                # one event on every stream of the frame just enqueued (its lane counts the warm-up
+                # frames too; no part streams: the current stream); its completion is the last of them
+                sts = (tiler.part_streams[(tiler.k - 1) % tiler.lanes] if tiler.part_streams
+                       else [torch.cuda.current_stream(dev)])
+                evs = []
+                for st_ in sts:
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record(st_)
+                    evs.append(e)
+                fev_.append(evs)
         for e, st in zip(ev1, lane_st):
             e.record(st)
         torch.cuda.synchronize(dev)
@@ -481,7 +491,8 @@ def main():
         el = time.perf_counter() - t0_
         tiler.finish()   # host bookkeeping: every lane is already complete
         gpu_ms = max(a.elapsed_time(b) for a in ev0 for b in ev1) / steps
-        return el, gpu_ms, [round(min(a.elapsed_time(e) for a in ev0), 4) for e in fev_] or None
+        return el, gpu_ms, [round(max(min(a.elapsed_time(e) for a in ev0) for e in evs), 4)
+                            for evs in fev_] or None
 
     elapsed, frame_gpu_ms, frame_events_ms = timed_frames(args.steps, args.frame_events)
     # The same frames without the per-frame gather (labelled "render_only"): what the split alone
@@ -600,7 +611,18 @@ def main():
                              "history, every part of this rank"}
         if gather_bad is not None:
             verify["gathered_frame_mismatched_elements"] = gather_bad
-        ok = torch.tensor([1 if bad == 0 and not gather_bad else 0], device=dev)
+        seq_ok = True
+        if tiler.gather:
+            # every rank enqueued lane g's gather for the same frames, in the same order per lane
+            # communicator (a mismatch would pair different frames' bands, or hang)
+            xl = torch.tensor(tiler.exchange_log(), dtype=torch.int64, device=dev)
+            x_lo, x_hi = xl.clone(), xl.clone()
+            dist.all_reduce(x_lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(x_hi, op=dist.ReduceOp.MAX)
+            seq_ok = bool(torch.equal(x_lo, x_hi))
+            verify["gather_sequence_equal_all_ranks"] = seq_ok
+            verify["gathers_per_lane"] = xl[0::2].tolist()
+        ok = torch.tensor([1 if bad == 0 and not gather_bad and seq_ok else 0], device=dev)
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         verify["verified_all_ranks"] = bool(ok.item())

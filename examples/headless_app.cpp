@@ -135,6 +135,9 @@ int main(int argc, char** argv) {
   // second parts, the gather stream) beside the caller's: with HIP's default of 4 hardware queues
   // the caller's stream shares a queue with a lane and its per-frame waits stall that lane's next
   // frame (C3 0.071 vs 0.061 ms per frame). Set before the first HIP call.
+  // (bench.py keeps HIP's 4: it enqueues its frames on its own four lane streams with no caller
+  // stream waiting on them, one stream per queue, and 4 queues is fastest for that shape — DESIGN
+  // §6 "Frames in flight"; this app's shape is vrt_render_frame_device's, a different topology.)
   setenv("GPU_MAX_HW_QUEUES", "16", 0);
   Options o;
   if (!parse(argc, argv, o)) {

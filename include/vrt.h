@@ -403,7 +403,9 @@ void vrt_params_default(vrt_params* out);
  * row0 + i*row_step (i < rows) that the part renders, written to band-buffer row
  * band_row0 + i*parts. out[(j*parts + p)*4 + 0..3] = {row0, rows, row_step, band_row0}; a band
  * holds ceil((height - j) / k) rows, band row r = frame row j + r*k. Returns the largest band's
- * rows. Used by the whole-frame entry points; exported for tests. */
+ * rows. LEGACY (cyclic rows): since ABI v12 the whole-frame entry points split a frame of
+ * k > 1 devices into block-cyclic bands (vrt_block_band_plan) and use this plan only for the
+ * interleaved parts of one device's frame (k = 1); kept exported for tests. */
 int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out);
 
 /* ABI v10: the k strided copies that assemble a frame of `height` rows x `width` pixels of
@@ -411,7 +413,8 @@ int vrt_band_plan(int32_t height, int32_t k, int32_t parts, int32_t* out);
  * the pinned host staging of vrt_render / vrt_render_frame over k devices and the device-frame
  * gather use exactly these. out[j*5 + 0..4] = {destination byte offset, destination pitch, source
  * pitch, row bytes, rows} of one 2-D copy (hipMemcpy2D). Host arithmetic, no GPU; returns k.
- * Exported for tests (unequal bands when height % k != 0). */
+ * LEGACY (cyclic rows, as vrt_band_plan): the k > 1 whole-frame paths use vrt_block_copy_plan's
+ * copies since ABI v12. Exported for tests (unequal bands when height % k != 0). */
 int vrt_band_copy_plan(int32_t width, int32_t height, int32_t k, int32_t elem_bytes, int64_t* out);
 
 /* ABI v12: rows per block of the bands the whole-frame entry points split a frame into over k

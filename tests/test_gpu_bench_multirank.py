@@ -72,6 +72,11 @@ def test_bench_two_ranks_json(built, scaling, gather):
         assert out["collect"] is None and "every frame" in out["config"]["parallelism"]
         assert out["gather"]["per_frame"] is True and out["gather"]["render_only"]["value"] > 0
         assert out["verify"]["gathered_frame_mismatched_elements"] == 0
+        # every rank enqueued each lane's gathers for the same frames (per-lane communicators)
+        assert out["verify"]["gather_sequence_equal_all_ranks"] is True
+        assert sum(out["verify"]["gathers_per_lane"]) > 0
+        ro = out["gather"]["render_only"]
+        assert ro["ms_per_step"] > 0 and ro["kernel_ms_max_over_ranks"] > 0
         assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * 4
     else:   # one gather of the last frame after the timed region
         assert out["collect"]["rows"] == rows and out["collect"]["bytes"] == rows * 1920 * 4

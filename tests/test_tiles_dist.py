@@ -75,6 +75,12 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
     f = tiler.finish()
     if gather and rank == 0:
         assert np.array_equal(f.numpy(), got[-1])
+    if gather:   # every rank enqueued the same frames' exchanges on every lane (bench.py checks it)
+        xl = torch.tensor(tiler.exchange_log(), dtype=torch.int64)
+        lo, hi = xl.clone(), xl.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        assert torch.equal(lo, hi) and int(xl[0::2].sum()) == frames, xl.tolist()
     if rank == 0:
         q.put((got, bytes(vox_np)))
     dist.barrier()

@@ -237,8 +237,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        if not hasattr(lib, name) and (name.startswith("vrt_debug_") or os.environ.get("VRT_LIB")):
-            continue   # diagnostics, or an A/B variant build (VRT_LIB) older than this ABI
+        if not hasattr(lib, name) and name.startswith("vrt_debug_"):
+            continue   # diagnostic entry points exist only in diagnostic builds (make variant)
+        # every other symbol must be there: A/B variants (VRT_LIB) are built from this tree, and an
+        # ABI/build mismatch fails here, at load time, not at the first call
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

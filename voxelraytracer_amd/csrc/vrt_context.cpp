@@ -35,7 +35,7 @@ constexpr int kParts = 2;              // interleaved row parts of a frame that 
 // its history, so consecutive device-output frames are independent and up to kLanes of them are in
 // flight: the light waves of the next frames fill the wave slots one frame's exact-path waves hold
 // (C3 0.0618 -> 0.0599 ms per frame on one GPU, C3's band at k = 8 GPUs 0.0416 -> 0.0112 ms;
-// scripts/diag/strong_pipe.py, profiles/r03_pipe). Such frames are one launch (a second part
+// profiles/r03_pipe). Such frames are one launch (a second part
 // only adds launch overhead once other frames fill the tail); frames that run alone (synchronous
 // calls) or read their history (u_Alpha != 1: part q of frame f waits for part q of frame f - 1)
 // are kParts interleaved parts, whose launches overlap each other's tails.
@@ -84,6 +84,10 @@ struct OrderSlot {
   size_t defer_cap = 0;        // its words
   uint32_t* h_batches = nullptr;  // host-mapped: an earlier exact pass's batch count (~0u: none)
   uint32_t* d_batches = nullptr;  // its device address
+  // end of the slot's last launch (recorded once the pool is under pressure, see acquire_slot):
+  // evicting the slot waits for it instead of the whole device
+  hipEvent_t ev_last = nullptr;
+  bool ev_last_valid = false;
 };
 
 struct Shard {
@@ -127,6 +131,7 @@ struct Shard {
   uint32_t* d_order_pool = nullptr;
   OrderSlot order[kOrderSlots];
   uint64_t order_tick = 0;
+  uint32_t order_assigned = 0;  // (band, stream) pairs assigned to slots so far
 };
 
 }  // namespace
@@ -291,6 +296,7 @@ void shard_free(Shard& s) {
   for (OrderSlot& o : s.order) {
     bufs.push_back(o.defer);
     if (o.h_batches) (void)hipHostFree(o.h_batches);
+    if (o.ev_last) (void)hipEventDestroy(o.ev_last);
   }
   for (int r = 0; r < kRing; ++r) {
     bufs.push_back(s.d_ring[r]);
@@ -448,11 +454,14 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
 
 // The tile-order slot of this launch's band and stream, from the shard's pool (no allocation, no
 // host sync in the steady state). A slot stays with its (band, stream): launches on one stream are
-// ordered, so no marker is needed per launch. Reassigning the least recently used slot to another
-// band or stream (more than kOrderSlots pairs in use) first synchronises the device: the old
-// stream's last launch with the slot may still run, and that stream may already have been
-// destroyed by its owner, so no event is recorded on it. Then the slot is zeroed on this stream
-// (no heavy tiles yet). Not while the stream is being captured into a graph (a replayed node
+// ordered, so no marker is needed per launch while the pool has room (a frame loop uses one slot per
+// lane). Reassigning the least recently used slot to another band or stream (more pairs than
+// kOrderSlots) must first wait for the old stream's last launch with the slot, and that stream may
+// already have been destroyed by its owner, so nothing can be recorded on it then: once half the
+// pool has been assigned, every launch with a slot records the slot's ev_last after it
+// (slot_launched), and eviction waits for that event; a slot evicted before any such record (the
+// pool filled in one burst) falls back to a device synchronisation. Then the slot is zeroed on this
+// stream (no heavy tiles yet). Not while the stream is being captured into a graph (a replayed node
 // would reuse one list / counter set): dispatch order then.
 OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
   if (a.tiles == 0 || a.tiles > kOrderMaxTiles) return nullptr;
@@ -467,7 +476,12 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
     slot = &s.order[0];
     for (auto& o : s.order)
       if (!o.used || (slot->used && o.tick < slot->tick)) slot = &o;
-    if (slot->used && slot->stream != st && hipDeviceSynchronize() != hipSuccess) return nullptr;
+    if (slot->used && slot->stream != st) {
+      const hipError_t e = slot->ev_last_valid ? hipEventSynchronize(slot->ev_last) : hipDeviceSynchronize();
+      if (e != hipSuccess) return nullptr;
+    }
+    slot->ev_last_valid = false;
+    ++s.order_assigned;
     // zero the list counters, the wave counters and both rank sets (no heavy tiles yet)
     if (hipMemsetAsync(slot->d, 0, (vrt::kOrdHdr + size_t(3) * a.tiles) * sizeof(uint32_t), st) != hipSuccess)
       return nullptr;
@@ -495,33 +509,43 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
 // bounds the band's frame rate (C3's band at k = 4 / 8 GPUs: 0.025 / 0.0235 ms per frame deferred,
 // 0.0155 / 0.0114 in-lane; the whole frame: 0.0445 deferred, 0.060 in-lane; C4's band at k = 8,
 // 16 200 waves: 0.0281 deferred, 0.0297 in-lane; profiles/r03_s18, r03_s19).
-void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
+// After a launch with slot `o` on st: under pool pressure, mark its end for a later eviction.
+void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
+  if (!o || s.order_assigned * 2u < uint32_t(kOrderSlots)) return;
+  if (!o->ev_last && hipEventCreateWithFlags(&o->ev_last, hipEventDisableTiming) != hipSuccess) {
+    o->ev_last = nullptr;
+    return;
+  }
+  o->ev_last_valid = hipEventRecord(o->ev_last, st) == hipSuccess;
+}
+
+OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
   const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 &&
                      (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
   // every tile is heavy, keep dispatch order: C1 +3.4 %)
   const bool order = !defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass;
-  if (!defer && !order) return;
+  if (!defer && !order) return nullptr;
   OrderSlot* slot = acquire_slot(s, a, st);
-  if (!slot) return;
+  if (!slot) return nullptr;
   if (defer) {  // both counter sets zeroed whenever the slot's previous launch was not one
     const size_t need = defer_words(a.tiles);
     if (slot->defer_cap < need) {  // first deferred launch of this band on the slot (or a larger band)
       // earlier launches with the slot run on st (its stream) and may still read the old list
-      if (slot->defer && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->defer) != hipSuccess)) return;
+      if (slot->defer && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->defer) != hipSuccess)) return slot;
       slot->defer = nullptr;
       slot->defer_cap = 0;
       if (hipMalloc(&slot->defer, need * sizeof(uint32_t)) != hipSuccess) {
         slot->defer = nullptr;
-        return;  // no list: the launch keeps the exact path in lane
+        return slot;  // no list: the launch keeps the exact path in lane
       }
       slot->defer_cap = need;
       slot->last_defer = false;
     }
     uint32_t* d = slot->defer;
     if (!slot->last_defer) {
-      if (hipMemsetAsync(d, 0, vrt::kDeferHdr * sizeof(uint32_t), st) != hipSuccess) return;
+      if (hipMemsetAsync(d, 0, vrt::kDeferHdr * sizeof(uint32_t), st) != hipSuccess) return slot;
       slot->defer_epoch = 0;
     }
     a.defer = d;
@@ -530,6 +554,7 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
     // bands of under 4 rounds: the exact pass's latency follows a short certified pass
     a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
     if (VRT_EXACT_GRID_ADAPT && !a.exact_fat) {
+      const uint32_t div = a.textured ? vrt::kDeferGridDiv : vrt::kDeferGridDivColor;  // launch_render's
       // the grid from an earlier frame's batch count on this slot (frames in flight: a few frames
       // old) plus a margin; a larger frame loops its workgroups over the rest. Idle workgroups
       // are not free: each waits for a register and LDS slot among the next frames' waves. Not for
@@ -545,7 +570,7 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
         }
       }
       if (slot->d_batches) {
-        const uint32_t full = std::max(64u, a.tiles * uint32_t(vrt::kWgWaves) / vrt::kDeferGridDiv);
+        const uint32_t full = std::max(64u, a.tiles * uint32_t(vrt::kWgWaves) / div);
         const uint32_t prev = *static_cast<volatile uint32_t*>(slot->h_batches);
         a.batches_out = slot->d_batches;
         if (prev != ~0u) a.exact_grid = std::min(full, std::max(64u, prev + prev / 4u + 64u));
@@ -553,7 +578,7 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
     }
     slot->defer_epoch++;
     slot->last_defer = true;
-    return;
+    return slot;
   }
   slot->last_defer = false;
   a.order = slot->d;
@@ -564,6 +589,7 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
   a.ctr_z = (a.ctr_r + 2u) % 3u;
   a.ord_q = (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
   slot->epoch++;
+  return slot;
 }
 
 // One band launch on `st` (heavy-first tile order for uncounted launches), then, when counting,
@@ -572,8 +598,9 @@ void launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
             hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr, bool allow_defer = true) {
   const bool stats = hit || cnt;
-  if (!stats) launch_state_begin(ctx, s, a, st, allow_defer);
+  OrderSlot* slot = stats ? nullptr : launch_state_begin(ctx, s, a, st, allow_defer);
   vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
+  slot_launched(s, slot, st);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
 }
 
@@ -1537,7 +1564,7 @@ int vrt_render_frame_device(vrt_ctx* ctx, const vrt_camera* cam, const vrt_param
   // call f - kRing + 1 consumed: E_{f-kRing+1}. The host waits for it when it is not done yet
   // (the caller's stream is more than kRing - 1 frames behind): a swapchain's back-pressure, with
   // no ordering packet on the GPU. (Waiting for it on the lane's stream cost 0.016 ms per C3 frame:
-  // the cross-queue wait packets stalled the lanes; scripts/diag/devframe_ab.py, profiles/r03_s14.)
+  // the cross-queue wait packets stalled the lanes; profiles/r03_s14; the one-off script is in git history.)
   hipEvent_t reuse = nullptr;
   if (f >= kRing) {
     const int rs = int((f - kRing + 1) % kRing);

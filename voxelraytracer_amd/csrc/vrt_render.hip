@@ -511,22 +511,10 @@ static_assert(kDistCap >= 2 && kDistCap <= 255, "D is stored in 8 bits");
 constexpr uint32_t kFwdCap = VRT_FWD_CAP;  // cap of F (G = F - 1 in 8 bits): 128 vs 64 C4 -1.4 %, C1-C3 +-0.3 % (r03_s42)
 static_assert(kFwdCap >= 3 && kFwdCap <= 255, "F and G are stored in 8 bits");
 constexpr float kSkipMargin = 1.0f / 256.0f;
-constexpr float kPfAhead = 2.0f;   // prefetch lead without a skip window (ray-parameter units)
-constexpr float kPfPast = 0.5f;    // prefetch point past a window's end
 
 // LEN0Z: the caller guarantees len0 == +0 (the primary ray, voxel.glsl:430), so
 // s = rayLength - ray.rayLength is rayLength itself (x - (+0) == x): one VALU less per step.
-// REGSEL: the crossed axis' operands by register selects (8 v_cndmask) instead of the LDS table
-// (2 v_cndmask + a ds_read_b128 whose round trip sits on the step's dependency chain): more VALU,
-// less latency — for waves that run alone (the deferred exact pass), not for full SIMDs
-// PF: software prefetch of the next sample's texel line (the exact pass's sparse batches, whose
-// 64 unrelated lanes make the wave wait for some lane's texel at nearly every step): each sampled
-// step also loads the texel where the lane's next sample will land — just past the window it opens,
-// or kPfAhead further along the ray without a window — so that sample finds its line in L2 / L1
-// rather than paying an Infinity Cache / HBM round trip. The prefetched value is only folded into
-// a sink at the lane's next sampled step, after that step's own load returned (loads return in
-// order), so the prefetch never adds a wait.
-template <bool SHADOW, bool STATS, bool LEN0Z = false, bool REGSEL = false, bool PF = false>
+template <bool SHADOW, bool STATS, bool LEN0Z = false>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
                                          int32_t& vidx_out, uint32_t& v_out) {
@@ -559,7 +547,6 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   bool check = w.check_cube;
   int result;
   constexpr uint32_t kOutside = 0x100u;
-  [[maybe_unused]] uint32_t pf = 0u, pf_sink = 0u;  // PF: the pending prefetch's texel, and the sink it is folded into
   for (;;) {
     // loop-top tests of the reference, in its order: length, TestCube, then our step cap.
     // check is only set after an outside sample; currentPos is that step's (len unchanged since),
@@ -604,11 +591,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       const unsigned long long mey = __builtin_amdgcn_ballot_w64(ey);
       const unsigned long long mez = __builtin_amdgcn_ballot_w64(ez);
       // the crossed axis' entry address straight from the masks: two v_cndmask, no index math
-      const float4 ae = REGSEL ? make_float4(sel_mask(mez, pos.z, sel_mask(mey, pos.y, pos.x)),
-                                             sel_mask(mez, dir.z, sel_mask(mey, dir.y, dir.x)),
-                                             sel_mask(mez, rcp.z, sel_mask(mey, rcp.y, rcp.x)),
-                                             sel_mask(mez, step.z, sel_mask(mey, step.y, step.x)))
-                               : lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
+      const float4 ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
       const float pa = ae.x, da = ae.y, ra = ae.z, sa = ae.w;
       const float ca = pa + s * da;  // == cur on that axis: the same two ops
       const float num = (ca + sa) - pa;
@@ -640,14 +623,6 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const float lz = __builtin_fmaf(float(vk), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
         const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
         s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
-        if constexpr (PF) {
-          pf_sink += pf;  // the previous prefetch: issued before this step's load, so it is back
-          const float sp = open ? s_lim + kPfPast : s + kPfAhead;
-          const uint32_t fi = cvt_flr(__builtin_amdgcn_fmed3f(pos.x + sp * dir.x, 0.0f, c.fn));
-          const uint32_t fj = cvt_flr(__builtin_amdgcn_fmed3f(pos.y + sp * dir.y, 0.0f, c.fn));
-          const uint32_t fk = cvt_flr(__builtin_amdgcn_fmed3f(pos.z + sp * dir.z, 0.0f, c.fn));
-          pf = load_u16_at(c.vox, mad24(mad24(fk, c.p, fj), c.p, fi), obase);
-        }
         // stop the inner loop on: outside sample, a byte that is an event, the length. Only a
         // sampled step can stop it: a skipped one reads an empty in-volume texel and has
         // s < s_len, hence len < max_len (see s_len).
@@ -677,7 +652,6 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
       break;
     }
   }
-  if constexpr (PF) asm volatile("" ::"v"(pf_sink), "v"(pf));  // keeps the prefetches
   const float s_end = LEN0Z ? len : len - len0;  // currentPos of the last step (the hit point on an event)
   w.t = t;
   w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
@@ -688,500 +662,29 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   return result;
 }
 
-// ------------------------------------------------------------ block-pipelined skip walk --
-//
-// skip_walk waits for each sampled step's texel before the next step: the texel's skip distance
-// decides whether the next step samples. A wave whose 64 lanes walk unrelated rays (the deferred
-// exact pass's compacted pixels) then waits for a texel round trip at nearly every step — some
-// lane samples at almost every step — where a coherent 8x8 wave waits only at its ~10 % sampled
-// steps. pipe_walk runs the same exact steps in blocks of KB: within a block no lane waits (a step
-// beyond the lane's skip window issues its texel load and goes on), and at the block's end the
-// wave waits once for all of the block's loads and then decides, per lane, in step order:
-//  - the first sampled step that stops the reference's walk (an event byte, an outside sample,
-//    the length test) ends the walk there: the lane restores the block's start state and replays
-//    the exact steps up to that one (the steps after it were speculative; state and exit record are
-//    then the ones skip_walk leaves at that step);
-//  - otherwise the block's last sampled step opens the next skip window, as in skip_walk.
-// A step inside a window is still a step of an empty in-volume voxel, so skipping it is exact; the
-// pipelined walk only samples more steps (those after the block's first sample) and never fewer
-// reference decisions. The state update of every step is the reference's, op for op (exact_step).
-
-// One exact DDA step (voxel.glsl:275-281 / :323-327, then the crossed axis' t, :296 / :381) with the
-// crossed axis' operands from the lane's LDS table: skip_walk's step, factored for pipe_walk's
-// main and replay loops (identical ops). Returns s = len - len0; tp, mey, mez as in skip_walk.
-// REGSEL: the operands by register selects (AX: pos, dir, rcp, step per axis) instead of the table.
-template <bool REGSEL = false>
-__device__ __forceinline__ float exact_step(f3& t, float& len, const float len0, const uint32_t ax_a0,
-                                            const uint32_t ax_a1, const uint32_t ax_a2, f3& tp,
-                                            unsigned long long& mey, unsigned long long& mez,
-                                            const float4* AX = nullptr) {
-  const float tmin = __builtin_fminf(t.x, __builtin_fminf(t.y, t.z));
-  tp = mk(t.x - tmin, t.y - tmin, t.z - tmin);
-  len += tmin;
-  const float s = len - len0;
-  mey = __builtin_amdgcn_ballot_w64(tp.y == 0.0f);
-  mez = __builtin_amdgcn_ballot_w64(tp.z == 0.0f);
-  float4 ae;
-  if constexpr (REGSEL) {
-    ae = make_float4(sel_mask(mez, AX[2].x, sel_mask(mey, AX[1].x, AX[0].x)),
-                     sel_mask(mez, AX[2].y, sel_mask(mey, AX[1].y, AX[0].y)),
-                     sel_mask(mez, AX[2].z, sel_mask(mey, AX[1].z, AX[0].z)),
-                     sel_mask(mez, AX[2].w, sel_mask(mey, AX[1].w, AX[0].w)));
-  } else {
-    ae = lds_load(sel_mask_u(mez, ax_a2, sel_mask_u(mey, ax_a1, ax_a0)));
-  }
-  const float ca = ae.x + s * ae.y;
-  const float num = (ca + ae.w) - ae.x;
-  const float q = div_rn(num, ae.y, ae.z) - s;
-  t = mk(sel_mask(mey | mez, tp.x, q), sel_mask(mey & ~mez, q, tp.y), sel_mask(mez, q, tp.z));
-  return s;
-}
-
-#if defined(VRT_PIPE_K) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_PIPE_K is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_PIPE_K
-#define VRT_PIPE_K 0
-#endif
-#if defined(VRT_PIPE_KB) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_PIPE_KB is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_PIPE_KB  // block size of the walks inside the bounce stacks (0: skip_walk)
-#define VRT_PIPE_KB VRT_PIPE_K
-#endif
-#if defined(VRT_SPEC_SPARSE) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_SPEC_SPARSE is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_SPEC_SPARSE  // walks of the primary trace of the exact pass's sparse batches (32 | M: spec_walk)
-#define VRT_SPEC_SPARSE 0
-#endif
-#if (defined(VRT_SPARSE_BATCH) || defined(VRT_SPARSE_BATCH_FAT)) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_SPARSE_BATCH is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
-#define VRT_SPARSE_BATCH 64
-#endif
-#if defined(VRT_EXACT_PRIO) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_EXACT_PRIO is an A/B knob of make variant builds"
-#endif
-// wave priority of the whole exact pass (0: only its bounce stacks raise it): its few long waves
-// share SIMDs with the next frames' certified waves; at 2 their chains issue first (C3 0.0395 ->
-// 0.0387 ms per frame, C4 -1 %, the driver's 20-frame run 0.0531 -> 0.0509; 3: C3 0.0389,
-// profiles/r04_exact/)
-#ifndef VRT_EXACT_PRIO
-#define VRT_EXACT_PRIO 2
-#endif
-#if defined(VRT_FORCE_FAT) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_FORCE_FAT is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_FORCE_FAT  // the 4-wave exact-pass instance for every colour-only band (A/B only)
-#define VRT_FORCE_FAT 0
-#endif
-#ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
-#define VRT_SPARSE_BATCH_FAT 16
-#endif
-#if defined(VRT_PIPE_INLANE) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_PIPE_INLANE is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_PIPE_INLANE  // block size of the in-lane exact path of stats-free render_kernel instances
-#define VRT_PIPE_INLANE 0
-#endif
-
-template <bool SHADOW, int KB>
-__device__ __forceinline__ int pipe_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
-                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
-                                         int32_t& vidx_out, uint32_t& v_out) {
-  static_assert(KB >= 2 && KB <= 15, "flag bytes hold at most 8 steps");
-  static_assert(KB <= 8, "flag bytes hold at most 8 steps");
-  const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
-                     __builtin_copysignf(1.0f, dir.z));
-  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
-  const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
-  const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
-  c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
-  c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
-  c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
-  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
-  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));
-  const bool skip_ok = SHADOW || medium == 0u;
-  const uint32_t obase =
-      ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
-  const float s_len = c.max_len - len0;
-  f3 t = w.t;
-  float len = w.len;
-  uint32_t it = w.it;
-  bool check = w.check_cube;
-  int result;
-  constexpr uint32_t kOutside = 0x100u;
-  [[maybe_unused]] uint32_t pf = 0u, pf_sink = 0u;  // PF: the pending prefetch's texel, and the sink it is folded into
-  for (;;) {
-    // loop-top tests of the reference (as skip_walk)
-    if (!(len < c.max_len)) {
-      result = WALK_MISS;
-      break;
-    }
-    if (check) {
-      const float sc = len - len0;
-      if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
-        result = WALK_MISS;
-        break;
-      }
-    }
-    if (it >= VRT_MAX_STEPS) {
-      result = WALK_CAP;
-      break;
-    }
-    const uint32_t k_max = VRT_MAX_STEPS - active_max(it);
-    const uint32_t it0 = it;
-    uint32_t k = 0;  // wave-uniform (SGPR): steps of this inner walk
-    uint32_t k_exit = k_max;
-    uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;
-    int32_t x_vidx = -1;
-    float s_lim = -1.0f;
-    for (;;) {
-      if (k >= k_max) break;  // wave-uniform step bound
-      // block start: the state a stopping lane replays from
-      const f3 t_cp = t;
-      const float len_cp = len;
-      const uint32_t k_cp = k;
-      uint32_t pk[KB];
-      // bit j: step j sampled; 8 + j: its sample was outside; 16 + j: len >= max_len after it
-      uint32_t fl = 0u;
-      float wvi = 0.0f, wvj = 0.0f, wvk = 0.0f;  // the last sampled step's cell (window)
-#pragma unroll
-      for (int j = 0; j < KB; ++j) {
-        pk[j] = 0u;
-        if (k >= k_max) break;
-        ++k;
-        f3 tp;
-        unsigned long long mey, mez;
-        const float s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
-        if (!(s < s_lim)) {  // sampled: issue the texel load, consume it at the block's end
-          const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
-          const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
-                            cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
-          const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
-          const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
-          const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
-          const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
-          const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
-          pk[j] = load_u16_at(c.vox, mad24(mad24(vk, c.p, vj), c.p, vi), obase);
-          fl |= (1u << j) | (inb ? 0u : 1u << (8 + j)) | (len < c.max_len ? 0u : 1u << (16 + j));
-          wvi = float(vi);
-          wvj = float(vj);
-          wvk = float(vk);
-        }
-      }
-      // block end: one wait for the block's loads; the first stopping step, the last sample
-      uint32_t jst = uint32_t(KB), pst = 0u, plast = 0u;
-#pragma unroll
-      for (int j = KB - 1; j >= 0; --j) {
-        const uint32_t v_ev = (fl >> (8 + j)) & 1u ? kOutside : (pk[j] & kVoxMask);
-        const bool stop = ((fl >> j) & 1u) &&
-                          ((SHADOW ? ((v_ev & ~2u) != 0u) : (v_ev != medium)) || ((fl >> (16 + j)) & 1u));
-        jst = stop ? uint32_t(j) : jst;
-        pst = stop ? pk[j] : pst;
-      }
-      const uint32_t sm = fl & 0xFFu;
-      const uint32_t jl = sm ? 31u - uint32_t(__builtin_clz(sm)) : 0u;
-#pragma unroll
-      for (int j = 0; j < KB; ++j) plast = jl == uint32_t(j) ? pk[j] : plast;
-      if (jst < uint32_t(KB)) {
-        // the walk stops at step jst of this block: replay the exact steps from the block start
-        t = t_cp;
-        len = len_cp;
-        f3 tp = mk(0.0f, 0.0f, 0.0f);
-        float s = 0.0f;
-        for (uint32_t r = 0; r <= jst; ++r) {
-          unsigned long long mey, mez;
-          s = exact_step(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez);
-        }
-        const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
-        const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
-                          cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
-        const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
-        const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
-        const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
-        const bool out = (fl >> (8 + jst)) & 1u;
-        k_exit = k_cp + jst + 1u;
-        x_v = out ? 0u : (pst & kVoxMask);  // outside samples read 0 (GetVoxel :151-152)
-        x_out = out ? 1u : 0u;
-        x_axis = tp.z == 0.0f ? 2u : (tp.y == 0.0f ? 1u : 0u);  // axis_index of the step's masks
-        x_vidx = out ? -1 : int32_t(canonical_index(c, cvt_flr(qx), cvt_flr(qy), cvt_flr(qz)));
-        asm volatile("" : "+v"(k_exit), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
-        break;
-      }
-      if (sm) {  // the next skip window from the block's last sample (as skip_walk's)
-        const uint32_t dist = plast >> kDistShift;
-        const float fd = float(dist) - kSkipMargin;
-        const float lx = __builtin_fmaf(wvi, rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
-        const float ly = __builtin_fmaf(wvj, rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
-        const float lz = __builtin_fmaf(wvk, rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
-        const bool open = skip_ok & (((fl >> (8 + jl)) & 1u) == 0u) & ((plast & kVoxMask) == 0u) & (dist >= 2u);
-        s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
-      }
-    }
-    it = it0 + k_exit;
-    const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
-    asm volatile("" : "+v"(x_out));
-    check = x_out != 0u;
-    if (event) {
-      axis_out = int(x_axis);
-      vidx_out = x_vidx;
-      v_out = x_v;
-      result = WALK_EVENT;
-      break;
-    }
-  }
-  const float s_end = len - len0;
-  w.t = t;
-  w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
-  w.len = len;
-  w.it = it;
-  w.ties = 0;
-  w.check_cube = check;
-  return result;
-}
-
-// ------------------------------------------------------- speculative-window exact walk --
-//
-// What bounds the deferred exact pass is its sparse batches: 64 unrelated pixels per wave, each an
-// exact walk of ~110-170 steps (exact_stamps.py: those waves are the pass's longest, 50-70 us, and
-// 90 % of that is the primary walk). skip_walk waits for a sampled step's texel before the next
-// step (its skip distance decides whether that step samples), and with 64 unrelated lanes some lane
-// samples at nearly every step, so the wave pays a cache-miss round trip per step (545 cycles for an
-// Infinity Cache hit, 900 for HBM, MI355X_MICROARCH.md) against ~100 cycles of the step's VALU.
-// pipe_walk (above) issued the loads of every step after a block's first sample and became bound
-// by the misses in flight instead. spec_walk keeps skip_walk's loads — one per sampled step — and
-// stops waiting for them: a lane that samples issues the texel load and goes on for M - 1 more
-// steps as if they lay inside the skip window the texel will open (they do unless the window is
-// short: the octant volume's boxes reach up to 127 cells ahead); M iterations later the texel is
-// there (one load per iteration for the whole wave, so the wait is a static vmcnt(M - 1)) and the
-// lane settles it:
-//  - an event byte: the walk stops at the sampled step — the lane restores the state saved there
-//    (t, len, steps, crossed axis, cell) and leaves, exactly as skip_walk stops there;
-//  - otherwise the texel's window s_lim (skip_walk's formula); if the last speculative step has
-//    s < s_lim, every speculative step lay inside it (s grows with each step) and skip_walk would
-//    have skipped them all; else the lane restores the sampled step's state and steps on from
-//    there with s_lim known, sampling where skip_walk samples.
-// Outside samples stop at once (they read 0; no texel needed); a sampled step that fails the
-// length test waits for its texel and stops (its byte still decides hit or miss). Every step's
-// state update is exact_step's (the reference's ops in order), so state, exit record and step
-// count equal skip_walk's. The caller uses it only when the step cap is out of reach (spec_ok).
-// Lanes that sample nothing issue a dummy load of the volume's first texel (one cache line).
-template <bool SHADOW, int M, bool REGSEL = false>
-__device__ __forceinline__ int spec_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
-                                         float len0, uint32_t medium, WalkState& w, int& axis_out,
-                                         int32_t& vidx_out, uint32_t& v_out) {
-  static_assert(M >= 2 && M <= 8, "speculation depth");
-  const float4 AX[3] = {make_float4(pos.x, dir.x, rcp.x, __builtin_copysignf(1.0f, dir.x)),
-                        make_float4(pos.y, dir.y, rcp.y, __builtin_copysignf(1.0f, dir.y)),
-                        make_float4(pos.z, dir.z, rcp.z, __builtin_copysignf(1.0f, dir.z))};
-  const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
-                     __builtin_copysignf(1.0f, dir.z));
-  const f3 hs = mk(0.5f * step.x, 0.5f * step.y, 0.5f * step.z);
-  const f3 c0 = mk(dir.x > 0.0f ? 0.0f : 1.0f, dir.y > 0.0f ? 0.0f : 1.0f, dir.z > 0.0f ? 0.0f : 1.0f);
-  const f3 boff = mk((c0.x - pos.x) * rcp.x, (c0.y - pos.y) * rcp.y, (c0.z - pos.z) * rcp.z);
-  c.ax[0] = make_float4(pos.x, dir.x, rcp.x, step.x);
-  c.ax[kAxStride] = make_float4(pos.y, dir.y, rcp.y, step.y);
-  c.ax[2 * kAxStride] = make_float4(pos.z, dir.z, rcp.z, step.z);
-  uint32_t ax_a0 = lds_addr(c.ax), ax_a1 = ax_a0 + 16u * kAxStride, ax_a2 = ax_a0 + 32u * kAxStride;
-  asm volatile("" : "+v"(ax_a0), "+v"(ax_a1), "+v"(ax_a2));
-  const bool skip_ok = SHADOW || medium == 0u;
-  const uint32_t obase =
-      ((dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u)) * c.ostride;
-  const float s_len = c.max_len - len0;
-  f3 t = w.t;
-  float len = w.len;
-  uint32_t it = w.it;
-  bool check = w.check_cube;
-  int result;
-  for (;;) {
-    // loop-top tests of the reference (as skip_walk); the cap cannot be reached (spec_ok)
-    if (!(len < c.max_len)) {
-      result = WALK_MISS;
-      break;
-    }
-    if (check) {
-      const float sc = len - len0;
-      if (!test_cube(mk(pos.x + sc * dir.x, pos.y + sc * dir.y, pos.z + sc * dir.z), dir, c.fn)) {
-        result = WALK_MISS;
-        break;
-      }
-    }
-    uint32_t kl = 0;  // this lane's steps of this inner walk
-    uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;
-    int32_t x_vidx = -1;
-    float s_lim = -1.0f;
-    float s_last = 0.0f;  // s of the lane's last step (the speculative steps' largest)
-    // the pending sample: due = the iteration it is settled in (0: none); its step's state
-    uint32_t due = 0u, fin = 0u;  // fin: the sampled step failed the length test (stop when settled)
-    f3 t_cp = t;
-    float len_cp = len;
-    uint32_t kl_cp = 0u, ax_cp = 0u, ci = 0u, cj = 0u, ck = 0u;
-    uint32_t slot[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) slot[j] = 0u;
-    uint32_t iter = 0;  // wave-uniform
-    bool done = false;
-    for (;;) {
-#pragma unroll
-      for (int j = 0; j < M; ++j) {
-        ++iter;  // iteration iter uses slot j (iter % M == (j + 1) % M, fixed by the unroll)
-        // 1. settle the sample issued M iterations ago, due now
-        if (due == iter) {
-          const uint32_t tex = slot[j];
-          const uint32_t v_raw = tex & kVoxMask, g = tex >> kDistShift;
-          const bool ev = SHADOW ? ((v_raw & ~2u) != 0u) : (v_raw != medium);
-          due = 0u;
-          if (ev | (fin != 0u)) {  // the walk stops at the sampled step
-            t = t_cp;
-            len = len_cp;
-            kl = kl_cp;
-            x_v = v_raw;
-            x_axis = ax_cp;
-            x_out = 0u;
-            x_vidx = int32_t(canonical_index(c, ci, cj, ck));
-            asm volatile("" : "+v"(kl), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
-            done = true;
-          } else {
-            const float fd = float(g) - kSkipMargin;
-            const float lx = __builtin_fmaf(float(ci), rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
-            const float ly = __builtin_fmaf(float(cj), rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
-            const float lz = __builtin_fmaf(float(ck), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
-            const bool open = skip_ok & (v_raw == 0u) & (g >= 2u);
-            s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
-            if (!(s_last < s_lim)) {  // a speculative step left the window: step on from the sample
-              t = t_cp;
-              len = len_cp;
-              kl = kl_cp;
-            }
-          }
-        }
-        // 2. the lane's next step (none after a sampled step that failed the length test)
-        uint32_t addr = 0u;  // the dummy load's texel
-        if (!done && ((fin == 0u) | (due == 0u))) {
-          f3 tp;
-          unsigned long long mey, mez;
-          const float s = exact_step<REGSEL>(t, len, len0, ax_a0, ax_a1, ax_a2, tp, mey, mez, AX);
-          ++kl;
-          s_last = s;
-          // 3. a sampled step (none while a sample is pending: its steps are speculative)
-          if ((due == 0u) & !(s < s_lim)) {
-            const f3 cur = mk(pos.x + s * dir.x, pos.y + s * dir.y, pos.z + s * dir.z);
-            const f3 smp = mk(cur.x + (tp.x == 0.0f ? hs.x : 0.0f), cur.y + (tp.y == 0.0f ? hs.y : 0.0f),
-                              cur.z + (tp.z == 0.0f ? hs.z : 0.0f));
-            const float qx = __builtin_amdgcn_fmed3f(smp.x, 0.0f, c.fn);
-            const float qy = __builtin_amdgcn_fmed3f(smp.y, 0.0f, c.fn);
-            const float qz = __builtin_amdgcn_fmed3f(smp.z, 0.0f, c.fn);
-            const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
-            const uint32_t axis = tp.z == 0.0f ? 2u : (tp.y == 0.0f ? 1u : 0u);
-            if (!inb) {  // outside: reads 0, stop here (TestCube / the caller decide)
-              x_v = 0u;
-              x_out = 1u;
-              x_axis = axis;
-              x_vidx = -1;
-              asm volatile("" : "+v"(kl), "+v"(x_v), "+v"(x_axis), "+v"(x_vidx), "+v"(x_out));
-              done = true;
-            } else {
-              ci = cvt_flr(qx);
-              cj = cvt_flr(qy);
-              ck = cvt_flr(qz);
-              addr = mad24(mad24(ck, c.p, cj), c.p, ci);
-              due = iter + uint32_t(M);
-              fin = len < c.max_len ? 0u : 1u;
-              t_cp = t;
-              len_cp = len;
-              kl_cp = kl;
-              ax_cp = axis;
-            }
-          }
-        }
-        // 4. one load per iteration for the whole wave: the sample, or the dummy texel
-        slot[j] = load_u16_at(c.vox, addr, obase);
-        if (done) break;
-      }
-      if (done) break;
-      if (iter >= uint32_t(VRT_MAX_STEPS)) {  // unreachable (spec_ok); bounds the loop regardless
-        kl = uint32_t(VRT_MAX_STEPS);
-        x_v = SHADOW ? 0u : medium;
-        x_out = 0u;
-        break;
-      }
-    }
-    it += kl;
-    const bool event = SHADOW ? (x_v != 0u && x_v != 2u) : (x_v != medium);
-    asm volatile("" : "+v"(x_out));
-    check = x_out != 0u;
-    if (event) {
-      axis_out = int(x_axis);
-      vidx_out = x_vidx;
-      v_out = x_v;
-      result = WALK_EVENT;
-      break;
-    }
-    if (it >= uint32_t(VRT_MAX_STEPS)) {
-      result = WALK_CAP;
-      break;
-    }
-  }
-  const float s_end = len - len0;
-  w.t = t;
-  w.cur = mk(pos.x + s_end * dir.x, pos.y + s_end * dir.y, pos.z + s_end * dir.z);
-  w.len = len;
-  w.it = it;
-  w.ties = 0;
-  w.check_cube = check;
-  return result;
-}
-
-// spec_walk needs the step cap out of reach: a walk of parameter length s crosses at most
-// s |d|_1 + 3 planes, and a tie step (two t's zero together) adds at most one zero-length step per
-// crossing, so it takes at most 2 (s |d|_1 + 3) steps; with a wide margin
-__device__ __forceinline__ bool spec_ok(const Ctx& c, const f3 dir, float len, uint32_t it) {
-  const float l1 = __builtin_fabsf(dir.x) + __builtin_fabsf(dir.y) + __builtin_fabsf(dir.z);
-  const float bound = 2.0f * (c.max_len - len) * l1 + 64.0f;
-  return bound < float(VRT_MAX_STEPS / 2) && it < uint32_t(VRT_MAX_STEPS / 2);
-}
-
 // RayMarch walk: per-ray reciprocals (RN(1/d), kept opaque so they stay loop-invariant).
-// PIPE (stats-free instances): bits 0-3 the block size of pipe_walk (0: skip_walk), bit 4 register
-// selects of the crossed axis' operands (skip_walk's REGSEL), bit 5 spec_walk with M = bits 0-3,
-// bit 6 skip_walk's texel prefetch (PF).
-template <bool STATS, bool LEN0Z = false, int PIPE = 0>
+// (The len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt;
+// round 4's pipelined, speculative, register-select and prefetching walks all measured slower
+// for the exact pass's sparse batches and were removed: DESIGN.md §6, git history before r05.)
+template <bool STATS>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v) {
-  static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    if constexpr ((PIPE & 32) != 0) {
-      if (spec_ok(c, dir, w.len, w.it)) return spec_walk<false, PIPE & 15, (PIPE & 16) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
-    } else if constexpr ((PIPE & 15) > 0) {
-      return pipe_walk<false, PIPE & 15>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
-    }
-    // (the len0 == 0 specialisation of skip_walk measured neutral: r01_v37_ab_axis_major_len0_cmpt)
-    return skip_walk<false, STATS, false, (PIPE & 16) != 0, (PIPE & 64) != 0>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
 
 // RayMarchShadow walk: the direction is normalize(u_SunDir) for every ray (uniform constants)
-template <bool STATS, int PIPE = 0>
+template <bool STATS>
 __device__ __forceinline__ int walk_shadow(const Ctx& c, const f3 pos, float len0, WalkState& w) {
-  static_assert(PIPE == 0 || !STATS, "pipelined walks keep no statistics");
   int axis;
   int32_t vidx;
   uint32_t v;
-  if (__builtin_expect(fast_path_ok(c.sun_n), 1)) {
-    if constexpr ((PIPE & 32) != 0) {
-      if (spec_ok(c, c.sun_n, w.len, w.it))
-        return spec_walk<true, PIPE & 15, (PIPE & 16) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
-    } else if constexpr ((PIPE & 15) > 0) {
-      return pipe_walk<true, PIPE & 15>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
-    }
-    return skip_walk<true, STATS, false, (PIPE & 16) != 0, (PIPE & 64) != 0>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
-  }
+  if (__builtin_expect(fast_path_ok(c.sun_n), 1))
+    return skip_walk<true, STATS>(c, pos, c.sun_n, c.sun_rcp, len0, 0u, w, axis, vidx, v);
   return dda_walk<true, true>(c, pos, c.sun_n, c.sun_n, len0, 0u, w, axis, vidx, v);
 }
 
@@ -1266,19 +769,19 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 }
 
 // RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
-template <bool STATS, int PIPE = 0>
+template <bool STATS>
 __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
   WalkState w;
   walk_init(w, ray);
-  const int r = walk_shadow<STATS, PIPE>(c, ray.pos, ray.len, w);
+  const int r = walk_shadow<STATS>(c, ray.pos, ray.len, w);
   walk_account(w, r, VRT_CNT_SHADOW_STEPS, k, steps, flags);
   return r == WALK_EVENT;
 }
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
 // PRIMARY: the primary ray (len 0, medium air: every event is a hit, no in-volume refraction)
-template <bool STATS, bool TEX, bool PRIMARY = false, int PIPE = 0>
+template <bool STATS, bool TEX, bool PRIMARY = false>
 __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -1297,7 +800,7 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk_ray<STATS, PRIMARY, PIPE>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
+    r = walk_ray<STATS>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -1381,7 +884,7 @@ __device__ __forceinline__ int cert_shadow_exact(const Ctx& c, const Hit& h);
 // (stats-free colour-only): the shadow bit by a certified walk from the exact hit point when it
 // settles it (cert_shadow_exact), and no shadow walk when it cannot change the brightness
 // (lit == ambient).
-template <bool STATS, bool TEX, bool CSH, int PIPE = 0>
+template <bool STATS, bool TEX, bool CSH>
 __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h, f3& color, Counters& k,
                                       uint32_t& steps, uint32_t& flags) {
   static_assert(!CSH || !STATS, "certified shadows in stats-free instances only");
@@ -1400,12 +903,12 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
       int blocked = 0;
       if (lit != kAmbient) {
         blocked = cert_shadow_exact(c, h);
-        if (blocked < 0) blocked = march_shadow<STATS, PIPE>(c, sr, k, steps, flags) ? 1 : 0;
+        if (blocked < 0) blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
       }
       brightness = blocked ? kAmbient : lit;
     } else {
       k.c[VRT_CNT_SHADOW_RAYS]++;
-      const bool in_shadow = march_shadow<STATS, PIPE>(c, sr, k, steps, flags);
+      const bool in_shadow = march_shadow<STATS>(c, sr, k, steps, flags);
       brightness = in_shadow ? kAmbient : lit_brightness<TEX>(h, sr.dir, ray.dir);
     }
     apply_hit_color<TEX>(c, h, ray.energy, brightness, color);
@@ -1415,11 +918,11 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
 }
 
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
-template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false, int PIPE = 0>
+template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
                                                  uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS, TEX, PRIMARY, PIPE>(c, ray, k, steps, flags);
-  shade<STATS, TEX, CSH, PIPE>(c, ray, h, color, k, steps, flags);
+  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
+  shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
   return h;
 }
 
@@ -2018,7 +1521,6 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
 // air — settled by certified walks where they can be (settled: colour updated, no secondary
 // rays); the exact march (as march()) otherwise.
 // (Out of line it costs C2-C4 +45 %, profiles/r01_v69_ab_noinline_w6.log.)
-template <int PIPE = 0>
 __device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k,
                           uint32_t& steps, uint32_t& flags) {
   Hit h;
@@ -2039,7 +1541,7 @@ __device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Coun
     int axis;
     int32_t vidx;
     uint32_t v;
-    const int r = walk_ray<false, false, PIPE>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
+    const int r = walk_ray<false>(c, ray.pos, ray.dir, ray.len, medium, w, axis, vidx, v);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -2416,19 +1918,14 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
 // Returns whether the pixel ran a bounce stack.
-// PIPE / PIPE_B: walks of the primary trace / of the bounce stack (walk_ray's code); PIPE_P: the
-// primary trace's walks when alt_primary (the exact pass's sparse batches: spec_walk)
-template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int PIPE = 0, int PIPE_B = PIPE,
-          int PIPE_P = PIPE>
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
-                                            int32_t& hit_vidx, float& hit_len, bool alt_primary = false) {
+                                            int32_t& hit_vidx, float& hit_len) {
   StackRay stack[kMaxStack - 1];  // the top entry lives in `ray`
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  Hit h0;
-  if (PIPE_P != PIPE && alt_primary) h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE_P>(c, ray, color, k, steps, flags);
-  else h0 = trace_with_shadow<STATS, TEX, true, CSH, PIPE>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
 #ifdef VRT_STAMPS
   const uint32_t st_wave = blockIdx.x * kWgWaves + (threadIdx.x >> 6);
   {
@@ -2478,15 +1975,15 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
         bool settled;
-        h = march_cert<PIPE_B>(lc, ray, color, settled, k, steps, flags);
+        h = march_cert(lc, ray, color, settled, k, steps, flags);
         if (settled) {
           h.found = false;  // a miss or a hit without secondary rays
           continue;
         }
-        shade<STATS, TEX, CSH, PIPE_B>(lc, ray, h, color, k, steps, flags);
+        shade<STATS, TEX, CSH>(lc, ray, h, color, k, steps, flags);
         continue;
       }
-      h = trace_with_shadow<STATS, TEX, false, CSH, PIPE_B>(lc, ray, color, k, steps, flags);
+      h = trace_with_shadow<STATS, TEX, false, CSH>(lc, ray, color, k, steps, flags);
     }
 #ifdef VRT_STAMPS
     {
@@ -2607,7 +2104,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     } else if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
       heavy = true;
-      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2, STATS ? 0 : VRT_PIPE_INLANE>(a, c, ray, color, k, steps,
+      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps,
                                                                                      flags, hit_vidx, hit_len);
     }
     const uint32_t l2 = lane_id();
@@ -2676,6 +2173,27 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 #endif
 }
 
+#if (defined(VRT_SPARSE_BATCH) || defined(VRT_SPARSE_BATCH_FAT) || defined(VRT_EXACT_PRIO) || \
+     defined(VRT_FORCE_FAT)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_SPARSE_BATCH / VRT_EXACT_PRIO / VRT_FORCE_FAT are A/B knobs of make variant builds"
+#endif
+#ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
+#define VRT_SPARSE_BATCH 64
+#endif
+#ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
+#define VRT_SPARSE_BATCH_FAT 16
+#endif
+// wave priority of the whole exact pass (0: only its bounce stacks raise it): its few long waves
+// share SIMDs with the next frames' certified waves; at 2 their chains issue first (C3 0.0395 ->
+// 0.0387 ms per frame, C4 -1 %, the driver's 20-frame run 0.0531 -> 0.0509; 3: C3 0.0389,
+// profiles/r04_exact/)
+#ifndef VRT_EXACT_PRIO
+#define VRT_EXACT_PRIO 2
+#endif
+#ifndef VRT_FORCE_FAT  // the 4-wave exact-pass instance for every colour-only band (A/B only)
+#define VRT_FORCE_FAT 0
+#endif
+
 // The deferred exact pass: the pixels a certified pass (render_kernel<..., DEFER>) left to it,
 // rendered with the exact path 64 to a wave — the certified pass's waves end with their certified
 // pixels, and the exact walks that would each have held a sparse wave of them run densely here
@@ -2698,8 +2216,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 // whose frame time includes this pass's span: a sparse wave's span is its slowest walk, and a lone
 // wave's walks cost the same per step with 16 lanes as with 64 (C4 k = 8 band 0.0222 -> 0.0200 ms,
 // exact-pass span 58 -> 49 us; whole frames +1-3 %: more waves, profiles/r04_exact/)
-template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, int PIPE = VRT_PIPE_K, int PIPE_B = VRT_PIPE_KB,
-          int PIPE_P = VRT_SPEC_SPARSE, uint32_t SB = VRT_SPARSE_BATCH>
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, uint32_t SB = VRT_SPARSE_BATCH>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t* ctr = a.defer;
@@ -2760,9 +2277,8 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    // sparse batches (64 unrelated pixels) walk their primaries speculatively (spec_walk)
-    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, PIPE, PIPE_B, PIPE_P>(a, c, ray, color, k, steps, flags,
-                                                                                    hit_vidx, hit_len, !dense);
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX>(a, c, ray, color, k, steps, flags, hit_vidx,
+                                                                hit_len);
     store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
 #ifdef VRT_STAMPS
     xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);
@@ -3054,7 +2570,7 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
 #endif
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
     auto k2 = a.textured ? exact_pass_kernel<true, 1>
-                         : ((a.exact_fat || VRT_FORCE_FAT) ? exact_pass_kernel<false, 2, 4, VRT_PIPE_K, VRT_PIPE_KB, VRT_SPEC_SPARSE, VRT_SPARSE_BATCH_FAT>
+                         : ((a.exact_fat || VRT_FORCE_FAT) ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>
                                        : exact_pass_kernel<false, 2>);
     if (ev_begin)
       hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);

@@ -266,6 +266,10 @@ class FrameTiler:
         self.channels, self.dtype = channels, dtype
         self.exchange = None
         self.exchange_on = True   # bench.py's render-only pass switches the per-frame gather off
+        # per lane: exchanges enqueued and the sum of their frame indices. A lane's collective runs
+        # on that lane's own communicator in enqueue order, so every rank must enqueue the same
+        # frames on every lane: exchange_log() is compared across ranks (bench.py)
+        self.xlog = [[0, 0] for _ in range(lanes)]
         self.latest = None
         if self.gather:
             # every rank's band padded to the largest band's rows: equal gather sizes
@@ -335,6 +339,7 @@ class FrameTiler:
                 self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
                                  **self.block_kw)
             if self.gather and self.exchange_on:
+                self._log_exchange(lane)
                 self.exchange.run(self, lane)
             return None
         cur = torch.cuda.current_stream()
@@ -354,11 +359,22 @@ class FrameTiler:
                 self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
                                  **self.block_kw)
                 if self.gather and self.exchange_on:
+                    if s == 0:
+                        self._log_exchange(lane)
                     self.exchange.run(self, lane)
                 ev = st.record_event() if dep else None
                 self.part_done[lane][s] = ev
                 events.append(ev)
         return events
+
+    def _log_exchange(self, lane: int) -> None:
+        self.xlog[lane][0] += 1
+        self.xlog[lane][1] += self.k - 1   # the index of the frame being enqueued
+
+    def exchange_log(self):
+        """Per lane [exchanges enqueued, sum of their frame indices] (a flat list of 2 x lanes ints):
+        equal on every rank iff every rank enqueued the same frames' gathers on every lane."""
+        return [v for row in self.xlog for v in row]
 
     # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
@@ -374,6 +390,7 @@ class FrameTiler:
             for args in self.plan[lane]:
                 self.launch(*args, **self.block_kw)
             if self.gather and self.exchange_on:
+                self._log_exchange(lane)
                 if isinstance(self.exchange, GatherLib):
                     self.exchange.run(self, lane)
                 else:

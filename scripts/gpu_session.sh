@@ -2,7 +2,7 @@
 # One gpurun call built from named steps (each under its own time limit; the call stops at the
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
-# steps: tests | smoke | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
+# steps: tests | smoke | pyt:FILES(,) | modes:CFG,STEPS,ROUNDS,M1/M2 | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
 #        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT[,RANK]]] | trace[:CFG] | strong[:CFG] | drvab[:CFG[,ROUNDS]] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
@@ -30,6 +30,15 @@ for st in "$@"; do
   case ${st%%:*} in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pyt) run pyt_$(echo $arg | tr -c 'a-zA-Z0-9' '_' | cut -c1-40) 600 python -u -m pytest ${arg//,/ } -x -v --timeout 200 --timeout-method thread ;;
+    modes)  # bench A/B over vrt_set_exact_pass modes: modes:CFG,STEPS,ROUNDS,M1/M2/... (driver shape: STEPS 20)
+      IFS=, read mc ms mr mm <<< "$arg"
+      for ((i = 1; i <= ${mr:-2}; i++)); do
+        for m in ${mm//\// }; do
+          TAILN=0 run modes_${mc}_s${ms}_m${m}_$i 150 python bench.py --config $mc --steps ${ms:-20} --warmup 5 --cpu-seconds 0 --no-verify --exact-pass $m
+          echo "modes $mc steps ${ms} ep$m $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/modes_${mc}_s${ms}_m${m}_$i.log | head -1) $(grep -o '"kernel_ms": [0-9.]*' $OUT/modes_${mc}_s${ms}_m${m}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/modes_${mc}_s${ms}_m${m}_$i.log | head -1)"
+        done
+      done ;;
     bench) run bench_${arg:-C3} 300 python bench.py --config ${arg:-C3} ;;
     drv) run drv_${arg:-C3} 300 python bench.py --config ${arg:-C3} --steps 20 --warmup 5 ;;
     ab) run ab 600 python -u scripts/ab.py --rounds 8 --configs ${arg:-C1,C2,C3,C4} ;;

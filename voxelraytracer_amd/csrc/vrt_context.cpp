@@ -88,6 +88,14 @@ struct OrderSlot {
   // evicting the slot waits for it instead of the whole device
   hipEvent_t ev_last = nullptr;
   bool ev_last_valid = false;
+  // the fused frame's queue (KArgs::queue; lazily allocated, entries zeroed once), its entry
+  // capacity, the last entry tag used, launches since its counters were zeroed, and whether the
+  // slot's last launch was a fused one
+  uint32_t* queue = nullptr;
+  uint32_t queue_cap = 0;
+  uint32_t q_epoch = 0;
+  uint64_t q_launches = 0;
+  bool last_queue = false;
 };
 
 struct Shard {
@@ -144,7 +152,7 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
-  int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 always
+  int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 two-kernel, 3 fused
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
   // timestamps (2 per launch, created up front), and how many are in use since the last read
   std::vector<hipEvent_t> lt_ev;
@@ -295,6 +303,7 @@ void shard_free(Shard& s) {
                              (void*)s.d_atlas, (void*)s.d_order_pool};
   for (OrderSlot& o : s.order) {
     bufs.push_back(o.defer);
+    bufs.push_back(o.queue);
     if (o.h_batches) (void)hipHostFree(o.h_batches);
     if (o.ev_last) (void)hipEventDestroy(o.ev_last);
   }
@@ -449,6 +458,8 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_fat = 0;
   a.exact_grid = 0;
   a.batches_out = nullptr;
+  a.queue = nullptr;
+  a.q_set = a.q_epoch = a.q_cap = 0;
   return a;
 }
 
@@ -493,6 +504,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
     slot->stream = st;
     slot->epoch = 0;
     slot->last_defer = false;
+    slot->last_queue = false;
     slot->used = true;
   }
   slot->tick = ++s.order_tick;
@@ -520,16 +532,23 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 }
 
 OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
-  const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 &&
-                     (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
+  const bool big = a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots;
+  // the fused frame (frame_kernel): colour-only certified bands of >= 2 rounds (exact_pass 1), or
+  // every colour-only certified band (3)
+  const bool fused = allow_defer && a.cert == 2 && !a.textured &&
+                     (ctx->exact_pass == 3 || (ctx->exact_pass == 1 && big));
+  const bool defer = !fused && allow_defer && (ctx->exact_pass == 1 || ctx->exact_pass == 2) && a.cert == 2 &&
+                     (ctx->exact_pass == 2 || big);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
-  // every tile is heavy, keep dispatch order: C1 +3.4 %)
-  const bool order = !defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass;
+  // every tile is heavy, keep dispatch order: C1 +3.4 %); the fused frame always keeps the order's
+  // bookkeeping (its first pass is empty with the tile order off)
+  const bool order = fused || (!defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass);
   if (!defer && !order) return nullptr;
   OrderSlot* slot = acquire_slot(s, a, st);
   if (!slot) return nullptr;
-  if (defer) {  // both counter sets zeroed whenever the slot's previous launch was not one
+  if (defer) {
+    slot->last_queue = false;  // both counter sets zeroed whenever the slot's previous launch was not one
     const size_t need = defer_words(a.tiles);
     if (slot->defer_cap < need) {  // first deferred launch of this band on the slot (or a larger band)
       // earlier launches with the slot run on st (its stream) and may still read the old list
@@ -581,13 +600,54 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     return slot;
   }
   slot->last_defer = false;
+  if (fused) {
+    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place)
+    const uint32_t need = a.tiles * uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
+    if (slot->queue_cap < need) {
+      // earlier launches with the slot run on st (its stream) and may still read the old queue
+      if (slot->queue && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->queue) != hipSuccess)) {
+        slot->last_queue = false;
+        return slot;
+      }
+      slot->queue = nullptr;
+      slot->queue_cap = 0;
+      const size_t bytes = (size_t(vrt::kQueueHdr) + 2u * size_t(need)) * sizeof(uint32_t);
+      if (hipMalloc(&slot->queue, bytes) != hipSuccess) {
+        slot->queue = nullptr;
+        slot->last_queue = false;
+        return slot;  // no queue: the in-lane path (order only) below
+      }
+      // entries start with tag 0, which no launch uses
+      if (hipMemsetAsync(slot->queue, 0, bytes, st) != hipSuccess) {
+        slot->last_queue = false;
+        return slot;
+      }
+      slot->queue_cap = need;
+      slot->last_queue = false;
+    }
+    if (!slot->last_queue) {  // both counter sets zeroed whenever the slot's last launch was not fused
+      if (hipMemsetAsync(slot->queue, 0, vrt::kQueueHdr * sizeof(uint32_t), st) != hipSuccess) return slot;
+      slot->q_launches = 0;
+    }
+    if (++slot->q_epoch == 0u) slot->q_epoch = 1u;  // (a wrap would take 2^32 frames)
+    a.queue = slot->queue;
+    a.q_set = uint32_t(slot->q_launches & 1u);
+    a.q_epoch = slot->q_epoch;
+    a.q_cap = need;
+    slot->q_launches++;
+    slot->last_queue = true;
+  } else {
+    slot->last_queue = false;
+  }
   a.order = slot->d;
   a.ord_r = uint32_t(slot->epoch & 1u);
   a.ord_w = a.ord_r ^ 1u;
   a.ctr_r = uint32_t(slot->epoch % 3u);
   a.ctr_w = (a.ctr_r + 1u) % 3u;
   a.ctr_z = (a.ctr_r + 2u) % 3u;
-  a.ord_q = (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+  a.ord_q = fused && !ctx->tile_order
+                ? 0u
+                : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
   slot->epoch++;
   return slot;
 }
@@ -1320,7 +1380,7 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
 
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
-  if (on < 0 || on > 2) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0, 1 or 2");
+  if (on < 0 || on > 3) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0, 1, 2 or 3");
   ctx->exact_pass = on;
   ctx->err.clear();
   return VRT_OK;

@@ -2297,6 +2297,201 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
 #endif
 }
 
+// ------------------------------------------------------------------------ fused frame --
+//
+// frame_kernel: one launch per frame for stats-free colour-only bands of >= 2 dispatch rounds (the
+// vrt_set_exact_pass default there). The two-launch scheme (render_kernel<DEFER>, then
+// exact_pass_kernel on the same stream) starts the exact work only after the last certified wave:
+// a frame's latency is the certified pass plus the exact pass's longest waves (C3: ~45 + ~75 us,
+// profiles/r04_exact/). Here the exact work starts while the certified work of the same frame runs:
+//  - tiles in heavy-first order (ordered_tile: the tiles that needed exact work in an earlier frame
+//    are dispatched first), so the exact work is known early;
+//  - a wave with >= kDeferDense pixels the certified walks cannot settle (a glass region: a
+//    coherent 8x8 tile of exact work) renders them in place at once, after publishing its
+//    progress;
+//  - a wave with fewer appends them to the launch's queue (ballot, one reservation atomic, mbcnt
+//    ranks: the north_star's __ballot compaction), and every wave, once its own tile is done,
+//    claims queued pixels in batches of kQueueBatch and renders them with the exact path: full
+//    batches at any time; a partial batch once the heavy-first pass has finished its certified
+//    phase (the queue then only grows by pixels of tiles that needed no exact work last frame) or
+//    every wave of the launch has (the last one drains the rest).
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the counters are device-scope atomics;
+// an entry is ONE 8-byte {epoch, pixel} granule written by one agent-scope (sc1, write-through)
+// store, read by agent-scope loads that wait for this launch's tag (bounded; entries of earlier
+// launches carry older tags), so no fence is needed and entries are never cleared. No wave ever
+// waits for another wave except for a reserved entry, which its producer stores right after the
+// reservation: the launch cannot deadlock at any residency. Every pixel is rendered exactly once by
+// the same exact path and epilogue as the other instances, so images are identical.
+#if defined(VRT_QUEUE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_QUEUE_BATCH is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_QUEUE_BATCH  // pixels per claimed batch of queued exact work (<= 64)
+#define VRT_QUEUE_BATCH 64
+#endif
+constexpr uint32_t kQueueBatch = VRT_QUEUE_BATCH;
+static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
+constexpr uint32_t kQTail = 0, kQHead = 1, kQDone = 2, kQHDone = 3;
+constexpr uint32_t kQueueSpinMax = 1u << 22;  // bound of an entry wait (a bug, never a normal case)
+
+__device__ __forceinline__ uint32_t* qctr(const KArgs& a, uint32_t set, uint32_t c) {
+  return a.queue + (set * kQCtrs + c) * kOrdCtrStride;
+}
+__device__ __forceinline__ uint32_t q_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// waits for the wave's outstanding vector-memory operations (an atomic's return included), so
+// that a later atomic is performed after an earlier one
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// The batch this wave claims next, as (first entry, count); count 0: nothing to claim now (the
+// wave exits). Lane 0 decides, the wave follows (uniform). total: waves that will publish `done`;
+// heavy_total: those of the heavy-first pass.
+__device__ __forceinline__ uint2 queue_claim(const KArgs& a, uint32_t total, uint32_t heavy_total) {
+  uint32_t h = 0, want = 0;
+  if (lane_id() == 0) {
+    // progress, not a spin: a failed claim means another wave advanced head, which only grows
+    // up to the final tail (the bound only guards against a bug)
+    for (uint32_t tries = 0; tries < (1u << 20); ++tries) {
+      const uint32_t dn = q_load(qctr(a, a.q_set, kQDone));
+      const uint32_t hd = q_load(qctr(a, a.q_set, kQHDone));
+      vm_drain();  // tail read after done: done == total implies the final tail
+      const uint32_t t = q_load(qctr(a, a.q_set, kQTail));
+      h = q_load(qctr(a, a.q_set, kQHead));
+      const uint32_t avail = t - h;
+      uint32_t w = avail >= kQueueBatch ? kQueueBatch : 0u;
+      if (avail != 0u && w == 0u && (dn >= total || hd >= heavy_total)) w = avail;
+      if (w == 0u) break;
+      uint32_t expect = h;
+      if (__hip_atomic_compare_exchange_strong(qctr(a, a.q_set, kQHead), &expect, h + w, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        want = w;
+        break;
+      }
+    }
+  }
+  return make_uint2(uint32_t(__builtin_amdgcn_readfirstlane(int(h))),
+                    uint32_t(__builtin_amdgcn_readfirstlane(int(want))));
+}
+
+__global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs a, const uint16_t* __restrict__ vox,
+                                                                           float4* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x < kQCtrs)  // the other set, for the next launch on the stream
+    *qctr(a, a.q_set ^ 1u, threadIdx.x) = 0u;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+  const uint32_t first_cap = kOrdClasses * a.ord_q;
+  uint32_t tile = ordered_tile(a, blockIdx.x);
+  if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  const bool heavy_pass = blockIdx.x < first_cap;
+  const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  __shared__ float4 ax_tab[kWgThreads * 3];
+  bool deferred = false;
+  {
+    const int px = pixel_x(tx, wave, lane_id());
+    const int li = pixel_row(ty, wave, lane_id());
+    if (px < a.width && li < a.rows) {
+      Ctx c;
+      init_ctx(c, a, vox);
+      c.ax = &ax_tab[threadIdx.x * kAxLane];
+      const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+      f3 color = mk(0.0f, 0.0f, 0.0f);
+      deferred = !cert_pixel<false>(c, ray, color);
+      const uint32_t l2 = lane_id();
+      if (!deferred)
+        store_pixel(a, out, size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2)), color);
+    }
+  }
+  const unsigned long long m = __ballot(deferred);
+  const uint32_t cnt = uint32_t(__builtin_popcountll(m));
+  const bool in_place = cnt >= kDeferDense;
+  const uint32_t l3 = lane_id();
+  const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
+  if (cnt != 0u && !in_place) {  // append: one reservation, mbcnt ranks, one granule per pixel
+    const uint32_t first = uint32_t(__builtin_ctzll(m));
+    uint32_t base = 0;
+    if (l3 == first) base = q_add(qctr(a, a.q_set, kQTail), cnt);
+    base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
+    if (deferred) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+      const uint32_t i = base + rank;
+      if (i < a.q_cap)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr) + i,
+                           (static_cast<unsigned long long>(a.q_epoch) << 32) | my_id, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (l3 == 0) {
+    vm_drain();  // the reservation is performed before this wave counts as done
+    q_add(qctr(a, a.q_set, kQDone), 1u);
+    if (heavy_pass) q_add(qctr(a, a.q_set, kQHDone), 1u);
+    order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
+  }
+  // the exact phase: this wave's own pixels in place, then claimed batches until none is left
+  const uint32_t total = a.tiles * uint32_t(kWgWaves);
+  uint32_t heavy_total = 0;  // waves of the heavy-first pass (read lazily: only a claim needs it)
+  bool heavy_known = false;
+  bool own = in_place;
+  bool prio = false;
+  for (;;) {
+    bool act = false;
+    uint32_t e = 0;
+    if (own) {
+      own = false;
+      act = deferred;
+      e = my_id;
+    } else {
+      if (!heavy_known) {
+        uint32_t ht = 0;
+        if (l3 < kOrdClasses) ht = min(*ord_ctr(a, a.ctr_r, l3), a.ord_q);
+        for (int off = 1; off < int(kOrdClasses); off <<= 1) ht += __shfl_xor(ht, off, 64);
+        heavy_total = uint32_t(__builtin_amdgcn_readfirstlane(int(ht))) * uint32_t(kWgWaves);
+        heavy_known = true;
+      }
+      const uint2 b = queue_claim(a, total, heavy_total);
+      if (b.y == 0u) break;
+      act = l3 < b.y;
+      if (act) {
+        const unsigned long long* ent = reinterpret_cast<const unsigned long long*>(a.queue + kQueueHdr) + (b.x + l3);
+        unsigned long long v = 0;
+        for (uint32_t spins = 0;; ++spins) {  // the producer stores it right after its reservation
+          v = __hip_atomic_load(ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (uint32_t(v >> 32) == a.q_epoch) break;
+          if (spins >= kQueueSpinMax) {
+            v = ~0ull;  // never reached by a correct launch: the pixel stays unrendered
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        e = uint32_t(v);
+        act = e != ~0u;
+      }
+    }
+    if (!prio && VRT_EXACT_PRIO > 0) {  // exact work: few long waves, their chains issue first
+      __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
+      prio = true;
+    }
+    if (act) {
+      Ctx c;
+      init_ctx(c, a, vox);
+      c.ax = &ax_tab[threadIdx.x * kAxLane];
+      const int px = int(e & 0xFFFFu), li = int(e >> 16);
+      const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+      Counters k;
+#pragma unroll
+      for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
+      uint32_t steps = 0, flags = 0;
+      int32_t hit_vidx = -1;
+      float hit_len = 0.0f;
+      f3 color = mk(0.0f, 0.0f, 0.0f);
+      (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+      store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
+    }
+  }
+}
+
 // Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
 // one wave-reduced atomic pair per wave.
 __global__ void __launch_bounds__(256) glass_share_kernel(const uint8_t* __restrict__ vox, uint64_t total,
@@ -2558,6 +2753,13 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // ~5 %), exact walks only (0)
   // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
   // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
+  if (a.queue && a.order && !stats && a.cert == 2 && !a.textured) {  // the fused frame (one launch)
+    if (ev_begin || ev_end)
+      hipExtLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, ev_begin, ev_end, 0, a, vox, out);
+    else
+      hipLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, a, vox, out);
+    return;
+  }
   if (a.defer && !stats && a.cert == 2) {
     // certified pass, then the exact pass over the pixels it deferred (no tile order: the
     // certified pass has no long waves)

@@ -2355,12 +2355,17 @@ __device__ __forceinline__ uint2 queue_claim(const KArgs& a, uint32_t total, uin
     // progress, not a spin: a failed claim means another wave advanced head, which only grows
     // up to the final tail (the bound only guards against a bug)
     for (uint32_t tries = 0; tries < (1u << 20); ++tries) {
+      // read in this order, each after the previous one returned: done, then head, then tail.
+      // done == total implies the final tail; and head <= tail at every instant with tail
+      // monotone, so a tail read after the head read is >= it (read the other way round, other
+      // waves' appends and claims in between could put head past the tail read)
       const uint32_t dn = q_load(qctr(a, a.q_set, kQDone));
       const uint32_t hd = q_load(qctr(a, a.q_set, kQHDone));
-      vm_drain();  // tail read after done: done == total implies the final tail
-      const uint32_t t = q_load(qctr(a, a.q_set, kQTail));
+      vm_drain();
       h = q_load(qctr(a, a.q_set, kQHead));
-      const uint32_t avail = t - h;
+      vm_drain();
+      const uint32_t t = q_load(qctr(a, a.q_set, kQTail));
+      const uint32_t avail = t > h ? t - h : 0u;
       uint32_t w = avail >= kQueueBatch ? kQueueBatch : 0u;
       if (avail != 0u && w == 0u && (dn >= total || hd >= heavy_total)) w = avail;
       if (w == 0u) break;
@@ -2452,7 +2457,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
       }
       const uint2 b = queue_claim(a, total, heavy_total);
       if (b.y == 0u) break;
-      act = l3 < b.y;
+      act = l3 < b.y && b.x + l3 < a.q_cap;  // (the capacity bounds every reservation)
       if (act) {
         const unsigned long long* ent = reinterpret_cast<const unsigned long long*>(a.queue + kQueueHdr) + (b.x + l3);
         unsigned long long v = 0;
@@ -2478,16 +2483,18 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
       init_ctx(c, a, vox);
       c.ax = &ax_tab[threadIdx.x * kAxLane];
       const int px = int(e & 0xFFFFu), li = int(e >> 16);
-      const Ray ray = primary_ray(a, c, px, frame_row(a, li));
-      Counters k;
+      if (px < a.width && li < a.rows) {  // (always: ids come from this launch's pixels)
+        const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+        Counters k;
 #pragma unroll
-      for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
-      uint32_t steps = 0, flags = 0;
-      int32_t hit_vidx = -1;
-      float hit_len = 0.0f;
-      f3 color = mk(0.0f, 0.0f, 0.0f);
-      (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
-      store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
+        for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
+        uint32_t steps = 0, flags = 0;
+        int32_t hit_vidx = -1;
+        float hit_len = 0.0f;
+        f3 color = mk(0.0f, 0.0f, 0.0f);
+        (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+        store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
+      }
     }
   }
 }

@@ -64,7 +64,7 @@ struct KArgs {
   // fused frame (frame_kernel, vrt_set_exact_pass 1 / 3 on colour-only bands of >= 2 rounds): one
   // launch renders the certified pixels, runs dense exact chunks in place and queues the sparse
   // ones, which waves that finished their own tiles claim in batches (see frame_kernel). queue: the
-  // slot's counters (two sets of kQCtrs, one 256-byte line each) then q_cap 8-byte entries
+  // slot's counters (two sets of kQCtrs, one 256-byte line each: see kQCtrs) then q_cap 8-byte entries
   // {epoch << 32 | pixel id}; q_set: this launch's counter set (the kernel zeroes the other one for
   // the next launch on the stream); q_epoch: the tag of this launch's entries (never 0; entries of
   // earlier launches keep older tags, so the entries are never cleared)
@@ -100,10 +100,15 @@ constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 
 constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
 constexpr uint32_t kDeferHdr = 4 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 kinds x 2 sets
 constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave keeps its own exact-pass batch
-// fused-frame queue (KArgs::queue): counters tail (reserved entries), head (claimed entries), done
-// (waves past their certified phase), hdone (the same for the heavy-first pass's waves)
-constexpr uint32_t kQCtrs = 4;
+// fused-frame queue (KArgs::queue), per counter set one 256-byte line each: tail (reserved
+// entries), head (claimed entries), flags (1: the heavy-first pass is past its certified phase,
+// 2: every wave is), top / htop (completed shards / heavy classes), then kOrdClasses heavy-class
+// counters and kQShards completion shards (waves past their certified phase, by tile % kQShards):
+// one address per ~250 waves instead of one for all (same-address atomics serialise at ~88 per us)
+constexpr uint32_t kQShards = 64;
+constexpr uint32_t kQCtrs = 5 + kOrdClasses + kQShards;
 constexpr uint32_t kQueueHdr = 2 * kQCtrs * kOrdCtrStride;  // words before the entries (8-byte aligned)
+static_assert(kQCtrs <= 128, "one zeroing thread per counter of the other set");
 #if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_DEFER_GRID_DIV is an A/B knob of make variant builds"
 #endif

@@ -2330,7 +2330,8 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
 #endif
 constexpr uint32_t kQueueBatch = VRT_QUEUE_BATCH;
 static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
-constexpr uint32_t kQTail = 0, kQHead = 1, kQDone = 2, kQHDone = 3;
+constexpr uint32_t kQTail = 0, kQHead = 1, kQFlags = 2, kQTop = 3, kQHTop = 4, kQHCls = 5, kQShard = 5 + kOrdClasses;
+constexpr uint32_t kQFlagHeavy = 1u, kQFlagAll = 2u;
 constexpr uint32_t kQueueSpinMax = 1u << 22;  // bound of an entry wait (a bug, never a normal case)
 
 __device__ __forceinline__ uint32_t* qctr(const KArgs& a, uint32_t set, uint32_t c) {
@@ -2343,31 +2344,31 @@ __device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // waits for the wave's outstanding vector-memory operations (an atomic's return included), so
-// that a later atomic is performed after an earlier one
+// that a later atomic or load is performed after an earlier one
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // The batch this wave claims next, as (first entry, count); count 0: nothing to claim now (the
-// wave exits). Lane 0 decides, the wave follows (uniform). total: waves that will publish `done`;
-// heavy_total: those of the heavy-first pass.
-__device__ __forceinline__ uint2 queue_claim(const KArgs& a, uint32_t total, uint32_t heavy_total) {
+// wave stops polling). Lane 0 decides, the wave follows (uniform). Full batches any time; a partial
+// batch once the heavy-first pass (flag 1; always when it is empty) or every wave (flag 2) is past
+// its certified phase.
+__device__ __forceinline__ uint2 queue_claim(const KArgs& a, bool no_heavy_pass) {
   uint32_t h = 0, want = 0;
   if (lane_id() == 0) {
     // progress, not a spin: a failed claim means another wave advanced head, which only grows
     // up to the final tail (the bound only guards against a bug)
     for (uint32_t tries = 0; tries < (1u << 20); ++tries) {
-      // read in this order, each after the previous one returned: done, then head, then tail.
-      // done == total implies the final tail; and head <= tail at every instant with tail
-      // monotone, so a tail read after the head read is >= it (read the other way round, other
-      // waves' appends and claims in between could put head past the tail read)
-      const uint32_t dn = q_load(qctr(a, a.q_set, kQDone));
-      const uint32_t hd = q_load(qctr(a, a.q_set, kQHDone));
+      // read in this order, each after the previous one returned: flags, then head, then tail.
+      // Flag 2 implies the final tail; and head <= tail at every instant with tail monotone, so a
+      // tail read after the head read is >= it (read the other way round, other waves' appends and
+      // claims in between could put head past the tail read: tests/queue_model.cpp)
+      const uint32_t fl = q_load(qctr(a, a.q_set, kQFlags));
       vm_drain();
       h = q_load(qctr(a, a.q_set, kQHead));
       vm_drain();
       const uint32_t t = q_load(qctr(a, a.q_set, kQTail));
       const uint32_t avail = t > h ? t - h : 0u;
       uint32_t w = avail >= kQueueBatch ? kQueueBatch : 0u;
-      if (avail != 0u && w == 0u && (dn >= total || hd >= heavy_total)) w = avail;
+      if (avail != 0u && w == 0u && (no_heavy_pass || fl != 0u)) w = avail;
       if (w == 0u) break;
       uint32_t expect = h;
       if (__hip_atomic_compare_exchange_strong(qctr(a, a.q_set, kQHead), &expect, h + w, __ATOMIC_RELAXED,
@@ -2390,7 +2391,6 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   uint32_t tile = ordered_tile(a, blockIdx.x);
   if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
   tile = __builtin_amdgcn_readfirstlane(tile);
-  const bool heavy_pass = blockIdx.x < first_cap;
   const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   __shared__ float4 ax_tab[kWgThreads * 3];
   bool deferred = false;
@@ -2414,7 +2414,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   const bool in_place = cnt >= kDeferDense;
   const uint32_t l3 = lane_id();
   const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
-  if (cnt != 0u && !in_place) {  // append: one reservation, mbcnt ranks, one granule per pixel
+  const bool appended = cnt != 0u && !in_place;
+  if (appended) {  // append: one reservation, mbcnt ranks, one granule per pixel
     const uint32_t first = uint32_t(__builtin_ctzll(m));
     uint32_t base = 0;
     if (l3 == first) base = q_add(qctr(a, a.q_set, kQTail), cnt);
@@ -2428,17 +2429,44 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
                            __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (l3 == 0) {
-    vm_drain();  // the reservation is performed before this wave counts as done
-    q_add(qctr(a, a.q_set, kQDone), 1u);
-    if (heavy_pass) q_add(qctr(a, a.q_set, kQHDone), 1u);
-    order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
+  // the heavy-first pass's classes: tiles of class r in it (lane r), and how many classes have any
+  uint32_t ncls = 0;
+  {
+    uint32_t nr = 0;
+    if (l3 < kOrdClasses) nr = min(*ord_ctr(a, a.ctr_r, l3), a.ord_q);
+    ncls = uint32_t(__builtin_popcountll(__ballot(nr != 0u)));
+    // this workgroup's class (first-pass slots only): broadcast lane (blockIdx % 8)'s count
+    nr = uint32_t(__builtin_amdgcn_readlane(int(nr), int(blockIdx.x % kOrdClasses)));
+    if (l3 == 0) {
+      // past the certified phase (the reservation above performed first): completion shards by
+      // tile, the shard's last wave counts the shard; the last shard's last wave sets flag 2. The
+      // heavy-first pass likewise by class, flag 1.
+      vm_drain();
+      const uint32_t shard = tile % kQShards;
+      const uint32_t shard_waves = (a.tiles / kQShards + (shard < a.tiles % kQShards ? 1u : 0u)) * uint32_t(kWgWaves);
+      uint32_t flags = 0;
+      if (q_add(qctr(a, a.q_set, kQShard + shard), 1u) + 1u == shard_waves &&
+          q_add(qctr(a, a.q_set, kQTop), 1u) + 1u == min(a.tiles, kQShards))
+        flags |= kQFlagAll;
+      if (blockIdx.x < first_cap) {
+        const uint32_t r = blockIdx.x % kOrdClasses;
+        if (q_add(qctr(a, a.q_set, kQHCls + r), 1u) + 1u == nr * uint32_t(kWgWaves) &&
+            q_add(qctr(a, a.q_set, kQHTop), 1u) + 1u == ncls)
+          flags |= kQFlagHeavy;
+      }
+      if (flags) __hip_atomic_fetch_or(qctr(a, a.q_set, kQFlags), flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
+      ncls |= flags << 16;  // (lane 0 only: whether this wave set a flag)
+    }
   }
-  // the exact phase: this wave's own pixels in place, then claimed batches until none is left
-  const uint32_t total = a.tiles * uint32_t(kWgWaves);
-  uint32_t heavy_total = 0;  // waves of the heavy-first pass (read lazily: only a claim needs it)
-  bool heavy_known = false;
+  // the exact phase: this wave's own pixels in place, then claimed batches. A wave polls the queue
+  // only when something it did can have made a batch claimable — its appends, a flag it set, the
+  // end of a batch it rendered — so the counters see a few thousand polls per frame, not one per wave
+  const bool set_flag = (uint32_t(__builtin_amdgcn_readfirstlane(int(ncls))) >> 16) != 0u;
+  ncls &= 0xFFFFu;
+  const bool no_heavy_pass = ncls == 0u;
   bool own = in_place;
+  bool poll = appended || set_flag || in_place;
   bool prio = false;
   for (;;) {
     bool act = false;
@@ -2448,14 +2476,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
       act = deferred;
       e = my_id;
     } else {
-      if (!heavy_known) {
-        uint32_t ht = 0;
-        if (l3 < kOrdClasses) ht = min(*ord_ctr(a, a.ctr_r, l3), a.ord_q);
-        for (int off = 1; off < int(kOrdClasses); off <<= 1) ht += __shfl_xor(ht, off, 64);
-        heavy_total = uint32_t(__builtin_amdgcn_readfirstlane(int(ht))) * uint32_t(kWgWaves);
-        heavy_known = true;
-      }
-      const uint2 b = queue_claim(a, total, heavy_total);
+      if (!poll) break;
+      const uint2 b = queue_claim(a, no_heavy_pass);
       if (b.y == 0u) break;
       act = l3 < b.y && b.x + l3 < a.q_cap;  // (the capacity bounds every reservation)
       if (act) {
@@ -2496,6 +2518,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
         store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
       }
     }
+    poll = true;  // after rendering a batch
   }
 }
 

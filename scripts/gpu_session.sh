@@ -59,6 +59,9 @@ for st in "$@"; do
     xstamps)  # exact-pass wave timeline (build/diag/libvrt_stamps.so: make variant NAME=stamps DEFS=-DVRT_STAMPS)
       IFS=, read xc xk xv xr <<< "$arg"
       VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1}_r${xr:-0} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} --rank ${xr:-0} ;;
+    fstamps)  # fused-frame wave timeline (build/variants/libvrt_stamps.so): fstamps:CFG[,K[,RANK[,MODE]]]
+      IFS=, read fc fk fr fm <<< "$arg"
+      VRT_LIB=$ROOT/build/variants/libvrt_stamps.so run fstamps_${fc}_k${fk:-1}_r${fr:-0}_m${fm:-3} 120 python -u scripts/frame_stamps.py --config $fc --ranks ${fk:-1} --rank ${fr:-0} --mode ${fm:-3} ;;
     drvab)  # the driver's 20-frame command, ROUNDS alternating rounds over base + build/variants/*.so
       IFS=, read dc dr <<< "$arg"
       for ((i = 1; i <= ${dr:-4}; i++)); do

@@ -1795,6 +1795,11 @@ __device__ unsigned long long g_stamps2[kMaxStampWaves][2];
 // exact_pass_kernel, per workgroup: {start, end, XCC_ID << 32 | HW_ID, pixels | dense << 16}
 __device__ unsigned long long g_stamps4[kMaxStampWaves][4];
 
+// frame_kernel, per wave: {start, after the certified phase, after the completion counters, end,
+// cnt | in_place << 8 | set_flag << 9 | heavy_pass << 10, batches claimed, entry-wait spins,
+// polls | exact pixels rendered << 16}
+__device__ unsigned long long g_stamps5[kMaxStampWaves][8];
+
 __device__ __forceinline__ uint32_t hw_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -2387,6 +2392,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   if (blockIdx.x == 0 && threadIdx.x < kQCtrs)  // the other set, for the next launch on the stream
     *qctr(a, a.q_set ^ 1u, threadIdx.x) = 0u;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+#ifdef VRT_STAMPS
+  const uint32_t sw = blockIdx.x * kWgWaves + uint32_t(wave);
+  unsigned long long st5[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+#endif
   const uint32_t first_cap = kOrdClasses * a.ord_q;
   uint32_t tile = ordered_tile(a, blockIdx.x);
   if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
@@ -2415,6 +2424,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   const uint32_t l3 = lane_id();
   const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
   const bool appended = cnt != 0u && !in_place;
+#ifdef VRT_STAMPS
+  st5[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (appended) {  // append: one reservation, mbcnt ranks, one granule per pixel
     const uint32_t first = uint32_t(__builtin_ctzll(m));
     uint32_t base = 0;
@@ -2464,6 +2476,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   // end of a batch it rendered — so the counters see a few thousand polls per frame, not one per wave
   const bool set_flag = (uint32_t(__builtin_amdgcn_readfirstlane(int(ncls))) >> 16) != 0u;
   ncls &= 0xFFFFu;
+#ifdef VRT_STAMPS
+  st5[2] = __builtin_amdgcn_s_memrealtime();
+  st5[4] = cnt | (in_place ? 0x100u : 0u) | (set_flag ? 0x200u : 0u) | (blockIdx.x < first_cap ? 0x400u : 0u);
+#endif
   const bool no_heavy_pass = ncls == 0u;
   bool own = in_place;
   bool poll = appended || set_flag || in_place;
@@ -2478,6 +2494,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
     } else {
       if (!poll) break;
       const uint2 b = queue_claim(a, no_heavy_pass);
+#ifdef VRT_STAMPS
+      st5[7] += 1u;
+      st5[5] += b.y != 0u ? 1u : 0u;
+#endif
       if (b.y == 0u) break;
       act = l3 < b.y && b.x + l3 < a.q_cap;  // (the capacity bounds every reservation)
       if (act) {
@@ -2491,6 +2511,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
             break;
           }
           __builtin_amdgcn_s_sleep(1);
+#ifdef VRT_STAMPS
+          st5[6] += 1u;
+#endif
         }
         e = uint32_t(v);
         act = e != ~0u;
@@ -2518,8 +2541,22 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
         store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
       }
     }
+#ifdef VRT_STAMPS
+    st5[7] += uint64_t(__builtin_popcountll(__ballot(act))) << 16;
+#endif
     poll = true;  // after rendering a batch
   }
+#ifdef VRT_STAMPS
+  {
+    st5[3] = __builtin_amdgcn_s_memrealtime();
+    // spins: the wave's largest lane count
+    uint32_t sp = uint32_t(st5[6]);
+    for (int off = 32; off > 0; off >>= 1) sp = max(sp, uint32_t(__shfl_xor(int(sp), off, 64)));
+    st5[6] = sp;
+    if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
+      for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = st5[q];
+  }
+#endif
 }
 
 // Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
@@ -2934,6 +2971,11 @@ int vrt_debug_stamps2(uint64_t* out, uint64_t count) {
 int vrt_debug_stamps4(uint64_t* out, uint64_t count) {
   if (!out || count > 4ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps4), count * 8) == hipSuccess ? VRT_OK
+                                                                                     : VRT_ERR_DEVICE;
+}
+int vrt_debug_stamps5(uint64_t* out, uint64_t count) {
+  if (!out || count > 8ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps5), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
 int vrt_debug_stamps3(uint64_t* out, uint64_t count) {

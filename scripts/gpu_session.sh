@@ -59,6 +59,16 @@ for st in "$@"; do
     xstamps)  # exact-pass wave timeline (build/diag/libvrt_stamps.so: make variant NAME=stamps DEFS=-DVRT_STAMPS)
       IFS=, read xc xk xv xr <<< "$arg"
       VRT_LIB=$ROOT/build/diag/libvrt_stamps$xv.so run xstamps${xv}_${xc}_k${xk:-1}_r${xr:-0} 120 python -u scripts/exact_stamps.py --config $xc --ranks ${xk:-1} --rank ${xr:-0} ;;
+    varmodes)  # every library (base + build/variants/*.so) x exact-pass modes: varmodes:CFG,STEPS,M1/M2
+      IFS=, read vc vs vm <<< "$arg"
+      for lib in $(libs); do
+        ln=$(basename $lib .so)
+        if [ $lib = base ]; then unset VRT_LIB; else export VRT_LIB=$ROOT/$lib; fi
+        for m in ${vm//\// }; do
+          TAILN=0 run vm_${ln}_${vc}_s${vs}_m$m 150 python bench.py --config $vc --steps ${vs:-20} --warmup 5 --cpu-seconds 0 --no-verify --exact-pass $m
+          echo "varmodes $ln $vc steps $vs ep$m $(grep -o '"ms_per_step": [0-9.]*' $OUT/vm_${ln}_${vc}_s${vs}_m$m.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/vm_${ln}_${vc}_s${vs}_m$m.log | head -1)"
+        done
+      done; unset VRT_LIB ;;
     fstamps)  # fused-frame wave timeline (build/variants/libvrt_stamps.so): fstamps:CFG[,K[,RANK[,MODE]]]
       IFS=, read fc fk fr fm <<< "$arg"
       VRT_LIB=$ROOT/build/variants/libvrt_stamps.so run fstamps_${fc}_k${fk:-1}_r${fr:-0}_m${fm:-3} 120 python -u scripts/frame_stamps.py --config $fc --ranks ${fk:-1} --rank ${fr:-0} --mode ${fm:-3} ;;

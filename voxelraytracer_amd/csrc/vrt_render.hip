@@ -2334,6 +2334,12 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
 #define VRT_QUEUE_BATCH 64
 #endif
 constexpr uint32_t kQueueBatch = VRT_QUEUE_BATCH;
+#if defined(VRT_FQ_DIAG) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_FQ_DIAG is a diagnostic knob of make variant builds"
+#endif
+#ifndef VRT_FQ_DIAG  // diagnostic: 1 no exact work (wrong images), 2 every exact pixel in place, 3 as 2 without the counters
+#define VRT_FQ_DIAG 0
+#endif
 static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
 constexpr uint32_t kQTail = 0, kQHead = 1, kQFlags = 2, kQTop = 3, kQHTop = 4, kQHCls = 5, kQShard = 5 + kOrdClasses;
 constexpr uint32_t kQFlagHeavy = 1u, kQFlagAll = 2u;
@@ -2420,10 +2426,10 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   }
   const unsigned long long m = __ballot(deferred);
   const uint32_t cnt = uint32_t(__builtin_popcountll(m));
-  const bool in_place = cnt >= kDeferDense;
+  const bool in_place = VRT_FQ_DIAG == 1 ? false : (VRT_FQ_DIAG >= 2 ? cnt != 0u : cnt >= kDeferDense);
   const uint32_t l3 = lane_id();
   const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
-  const bool appended = cnt != 0u && !in_place;
+  const bool appended = VRT_FQ_DIAG == 0 && cnt != 0u && !in_place;
 #ifdef VRT_STAMPS
   st5[1] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2449,7 +2455,8 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
     ncls = uint32_t(__builtin_popcountll(__ballot(nr != 0u)));
     // this workgroup's class (first-pass slots only): broadcast lane (blockIdx % 8)'s count
     nr = uint32_t(__builtin_amdgcn_readlane(int(nr), int(blockIdx.x % kOrdClasses)));
-    if (l3 == 0) {
+    if (l3 == 0 && VRT_FQ_DIAG == 3) order_record(a, tile, cnt != 0u);
+    if (l3 == 0 && VRT_FQ_DIAG != 3) {
       // past the certified phase (the reservation above performed first): completion shards by
       // tile, the shard's last wave counts the shard; the last shard's last wave sets flag 2. The
       // heavy-first pass likewise by class, flag 1.
@@ -2482,7 +2489,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
 #endif
   const bool no_heavy_pass = ncls == 0u;
   bool own = in_place;
-  bool poll = appended || set_flag || in_place;
+  bool poll = VRT_FQ_DIAG == 0 && (appended || set_flag || in_place);
   bool prio = false;
   for (;;) {
     bool act = false;
@@ -2544,7 +2551,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
 #ifdef VRT_STAMPS
     st5[7] += uint64_t(__builtin_popcountll(__ballot(act))) << 16;
 #endif
-    poll = true;  // after rendering a batch
+    poll = VRT_FQ_DIAG == 0;  // after rendering a batch
   }
 #ifdef VRT_STAMPS
   {

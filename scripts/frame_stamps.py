@@ -4,8 +4,8 @@
 
 Each wave records s_memrealtime (100 MHz) at its start, after its certified phase, after the
 completion counters and at its end, plus its deferred-pixel count, whether it rendered them in
-place, set a completion flag or belongs to the heavy-first pass, the batches it claimed, its
-longest entry wait (spins of 1 s_sleep) and the exact pixels it rendered. One band is rendered
+place, drains its class's partial batch or belongs to the heavy-first pass, and the full queue
+batches it owns. One band is rendered
 alone a few times in the fused mode; the last launch's stamps are summarised.
 Usage: VRT_LIB=... python scripts/frame_stamps.py --config C3 [--ranks 8 --rank R] [--mode 3]"""
 import argparse
@@ -70,28 +70,26 @@ def main():
     start, cert, done, end = us(0), us(1), us(2), us(3)
     info = s[:, 4].astype(np.int64)
     cnt, inplace, setf, heavy = info & 0xFF, (info >> 8) & 1, (info >> 9) & 1, (info >> 10) & 1
-    claims, spins = s[:, 5].astype(np.int64), s[:, 6].astype(np.int64)
-    polls, xpx = (s[:, 7] & np.uint64(0xFFFF)).astype(np.int64), (s[:, 7] >> np.uint64(16)).astype(np.int64)
-    exact = (inplace == 1) | (claims > 0)
+    claims = s[:, 5].astype(np.int64)
+    exact = (inplace == 1) | (claims > 0) | (setf == 1)
     out = {"config": args.config, "band": [row0, rows, step, block], "mode": args.mode,
            "waves": int(len(busy)), "span_us": round(float(end.max()), 2),
            "last_certified_phase_end_us": round(float(cert.max()), 2),
            "cert_phase_us": q(cert - start), "counter_phase_us": q(done - cert),
            "heavy_pass": {"waves": int(heavy.sum()),
                           "cert_end_us": round(float(cert[heavy == 1].max()), 2) if heavy.any() else None},
-           "flags_set_at_us": sorted(round(float(x), 2) for x in done[setf == 1]),
+           "class_drains_at_us": sorted(round(float(x), 2) for x in done[setf == 1]),
            "appending_waves": int(((cnt > 0) & (inplace == 0)).sum()), "appended": int(cnt[inplace == 0].sum()),
            "in_place_waves": int(inplace.sum()), "in_place_pixels": int(cnt[inplace == 1].sum()),
-           "polls": int(polls.sum()), "claims": int(claims.sum()), "exact_pixels": int(xpx.sum()),
-           "max_entry_spins": int(spins.max()), "waves_with_spins": int((spins > 0).sum()),
+           "owned_batches": int(claims.sum()),
            "exact_waves": {"n": int(exact.sum()), "exact_phase_us": q(end[exact] - done[exact]),
                            "start_of_exact_us": q(done[exact]), "end_us": q(end[exact])},
            "other_waves_end_us": q(end[~exact])}
     order = np.argsort(-end)[:10]
     out["latest"] = [{"end_us": round(float(end[i]), 2), "start_us": round(float(start[i]), 2),
                       "cert_end_us": round(float(cert[i]), 2), "exact_from_us": round(float(done[i]), 2),
-                      "cnt": int(cnt[i]), "in_place": bool(inplace[i]), "claims": int(claims[i]),
-                      "polls": int(polls[i]), "exact_px": int(xpx[i]), "spins": int(spins[i])} for i in order]
+                      "cnt": int(cnt[i]), "in_place": bool(inplace[i]), "batches": int(claims[i]),
+                      "class_drain": bool(setf[i])} for i in order]
     print(json.dumps(out, indent=1))
 
 

@@ -1,86 +1,115 @@
-// CPU stress model of frame_kernel's queue protocol (vrt_render.hip, "fused frame"): threads play
-// waves that append 0..31 exact pixels (or >= 32: in place, no append), publish done / hdone, and
-// then claim batches (full batches at any time, partial ones once the heavy pass or every wave is
-// done: the flags their last waves set) exactly as queue_claim does, reading flags, head, tail in
-// that order; only waves that appended, set a flag or rendered a batch poll (as frame_kernel). Checks that every
-// queued pixel is rendered exactly once and no claim reaches past the reservations. Test
-// infrastructure only (tests/test_queue_protocol.py); the order of the head and tail reads is the
-// one a reversed version gets wrong (claims past the tail, waits for entries never written).
+// CPU stress model of the fused frame's queue protocol (vrt_render.hip, frame_kernel + drain_kernel).
+// Threads play the waves of one launch: heavy-pass waves of class r append to segment A_r, the
+// others to B_s; a wave appends 1..31 exact pixels (or renders >= 32 in place: no append). Batches
+// are fixed index ranges [B k, B (k + 1)) of a segment, owned by the wave whose reservation covers
+// the batch's last index; the heavy-pass wave that completes class r (a per-class counter) owns the
+// partial last batch of A_r; after every thread has joined, the "drain kernel" owns the partial last
+// batches of the B segments. Checks: every queued pixel rendered exactly once, no batch read past
+// the reservations, every entry wait satisfied. Test infrastructure only (tests/test_queue_protocol.py).
 #include <atomic>
-#include <cstdio>
 #include <cstdint>
+#include <cstdio>
 #include <random>
 #include <thread>
 #include <vector>
-std::atomic<uint32_t> tail{0}, head{0}, done_{0}, hdone{0}, flags{0};
-std::vector<std::atomic<uint64_t>> ent;
+
+constexpr uint32_t kClasses = 8, B = 64, kEpoch = 7;
+struct Seg {
+  std::atomic<uint32_t> tail{0};
+  std::vector<std::atomic<uint64_t>> ent;
+};
+Seg segA[kClasses], segB[kClasses];
+std::atomic<uint32_t> hcls[kClasses];
 std::vector<std::atomic<int>> seen;
-uint32_t total, heavy_total, cap; const uint32_t B = 64, epoch = 7;
 std::atomic<long> bad{0};
-void wave(int id, uint32_t cnt, bool heavy, bool inplace) {
+uint32_t cls_waves[kClasses];
+
+uint32_t entry(Seg& s, uint32_t i) {
+  if (i >= s.ent.size()) { bad++; return ~0u; }
+  uint64_t v;
+  long spins = 0;
+  while (((v = s.ent[i].load()) >> 32) != kEpoch) {
+    if (++spins > 100000000) { bad++; return ~0u; }
+    std::this_thread::yield();
+  }
+  return uint32_t(v);
+}
+void render(uint32_t id) { if (id != ~0u) seen[id].fetch_add(1); }
+
+void wave(int id, uint32_t cnt, bool heavy, uint32_t cls) {
   std::mt19937 rng(id);
-  const bool appended = cnt && !inplace;
-  if (appended) {
-    uint32_t base = tail.fetch_add(cnt);
+  Seg& s = heavy ? segA[cls] : segB[cls];
+  uint32_t kb0 = 0, kb1 = 0;
+  if (cnt && cnt < 32) {
+    const uint32_t base = s.tail.fetch_add(cnt);
     for (uint32_t r = 0; r < cnt; ++r) {
       if (rng() % 4 == 0) std::this_thread::yield();
-      if (base + r < cap) ent[base + r].store((uint64_t(epoch) << 32) | (id * 64 + r));
+      if (base + r < s.ent.size()) s.ent[base + r].store((uint64_t(kEpoch) << 32) | (id * 64 + r));
     }
+    kb0 = base / B;            // frame_kernel: (base + B) / B - 1
+    kb1 = (base + cnt) / B;
+  } else if (cnt >= 32) {
+    for (uint32_t r = 0; r < cnt; ++r) render(id * 64 + r);   // in place
   }
-  // completion: the last wave sets flag 2, the heavy pass's last wave flag 1 (kernel: sharded
-  // counters whose last adder counts the shard; one counter here)
-  uint32_t fl = 0;
-  if (done_.fetch_add(1) + 1 == total) fl |= 2;
-  if (heavy && hdone.fetch_add(1) + 1 == heavy_total) fl |= 1;
-  if (fl) flags.fetch_or(fl);
-  // poll only when something this wave did can have made a batch claimable
-  bool poll = appended || fl || inplace;
-  for (;;) {
-    if (!poll) break;
-    uint32_t h = 0, want = 0;
-    for (int tries = 0; tries < (1 << 20); ++tries) {
-      uint32_t f = flags.load();
-      h = head.load();
-      if (rng() % 8 == 0) std::this_thread::yield();
-      uint32_t t = tail.load();
-      uint32_t avail = t > h ? t - h : 0;
-      uint32_t w = avail >= B ? B : 0;
-      if (avail && !w && (heavy_total == 0 || f)) w = avail;
-      if (!w) break;
-      uint32_t e = h;
-      if (head.compare_exchange_strong(e, h + w)) { want = w; break; }
-    }
-    if (!want) break;
-    for (uint32_t l = 0; l < want; ++l) {
-      if (h + l >= cap) { bad++; continue; }
-      uint64_t v; long spins = 0;
-      while (((v = ent[h + l].load()) >> 32) != epoch) { if (++spins > 100000000) { bad++; break; } std::this_thread::yield(); }
-      seen[uint32_t(v)].fetch_add(1);
-    }
-    poll = true;
+  uint32_t lo = 0, hi = 0;
+  if (heavy && hcls[cls].fetch_add(1) + 1 == cls_waves[cls]) {
+    const uint32_t t = segA[cls].tail.load();
+    lo = t / B * B;
+    hi = t;
   }
+  for (uint32_t k = kb0; k < kb1; ++k)
+    for (uint32_t l = 0; l < B; ++l) render(entry(s, k * B + l));
+  for (uint32_t i = lo; i < hi; ++i) render(entry(segA[cls], i));
 }
+
 int main() {
   for (int trial = 0; trial < 200; ++trial) {
     std::mt19937 rng(trial);
-    int waves = 200 + rng() % 200; total = waves; cap = waves * 31;
-    ent = std::vector<std::atomic<uint64_t>>(cap); seen = std::vector<std::atomic<int>>(waves * 64);
-    for (auto& e : ent) e.store(0);
-    tail = head = done_ = hdone = flags = 0;
-    std::vector<uint32_t> cnt(waves); std::vector<bool> hv(waves);
-    uint32_t nheavy = 0; long expected = 0;
-    for (int i = 0; i < waves; ++i) {
-      uint32_t r = rng() % 10; cnt[i] = r < 6 ? 0 : (r < 9 ? rng() % 31 + 1 : 32 + rng() % 33);
-      hv[i] = i < waves / 5; nheavy += hv[i];
-      if (cnt[i] && cnt[i] < 32) expected += cnt[i];
+    const int waves = 200 + rng() % 300;
+    const bool heavy_pass = trial % 3 != 0;
+    seen = std::vector<std::atomic<int>>(size_t(waves) * 64);
+    std::vector<uint32_t> cnt(waves), cls(waves);
+    std::vector<bool> hv(waves);
+    for (uint32_t r = 0; r < kClasses; ++r) {
+      cls_waves[r] = 0;
+      hcls[r] = 0;
     }
-    heavy_total = (trial % 3 == 0) ? 0 : nheavy;
+    for (int i = 0; i < waves; ++i) {
+      const uint32_t x = rng() % 10;
+      cnt[i] = x < 5 ? 0 : (x < 9 ? rng() % 31 + 1 : 32 + rng() % 33);
+      hv[i] = heavy_pass && i < waves / 4;
+      cls[i] = i % kClasses;
+      if (hv[i]) cls_waves[cls[i]]++;
+    }
+    for (uint32_t r = 0; r < kClasses; ++r) {
+      segA[r].tail = 0;
+      segB[r].tail = 0;
+      segA[r].ent = std::vector<std::atomic<uint64_t>>(size_t(waves) * 31);
+      segB[r].ent = std::vector<std::atomic<uint64_t>>(size_t(waves) * 31);
+      for (auto& e : segA[r].ent) e.store(0);
+      for (auto& e : segB[r].ent) e.store(0);
+    }
     std::vector<std::thread> th;
-    for (int i = 0; i < waves; ++i) th.emplace_back(wave, i, cnt[i], hv[i], cnt[i] >= 32);
+    for (int i = 0; i < waves; ++i) th.emplace_back(wave, i, cnt[i], bool(hv[i]), cls[i]);
     for (auto& t : th) t.join();
-    long got = 0, dup = 0;
-    for (int i = 0; i < waves; ++i) for (uint32_t r = 0; r < 64; ++r) { int s = seen[i * 64 + r]; got += s; if (s > 1) dup++; if (cnt[i] && cnt[i] < 32 && r < cnt[i] && s != 1) { printf("trial %d wave %d entry %u seen %d\n", trial, i, r, s); return 1; } }
-    if (got != expected || dup || bad) { printf("trial %d: got %ld expected %ld dup %ld bad %ld\n", trial, got, expected, dup, long(bad)); return 1; }
+    // drain kernel: the partial last batches of the B segments
+    for (uint32_t r = 0; r < kClasses; ++r) {
+      const uint32_t t = segB[r].tail.load();
+      for (uint32_t i = t / B * B; i < t; ++i) render(entry(segB[r], i));
+    }
+    for (int i = 0; i < waves; ++i)
+      for (uint32_t r = 0; r < 64; ++r) {
+        const int want = r < cnt[i] ? 1 : 0;
+        if (seen[size_t(i) * 64 + r] != want) {
+          printf("trial %d wave %d pixel %u rendered %d times\n", trial, i, r, int(seen[size_t(i) * 64 + r]));
+          return 1;
+        }
+      }
+    if (bad) {
+      printf("trial %d: %ld bad reads\n", trial, long(bad));
+      return 1;
+    }
   }
   printf("ok\n");
+  return 0;
 }

@@ -1,6 +1,7 @@
-"""CPU: the fused frame's queue protocol (frame_kernel / queue_claim in vrt_render.hip) under a
+"""CPU: the fused frame's queue protocol (frame_kernel / drain_kernel in vrt_render.hip) under a
 threaded stress model (tests/queue_model.cpp): every queued pixel claimed and rendered exactly
-once, across 200 random schedules, with and without a heavy-first pass."""
+once (owned full batches, class drains, the drain kernel), across 200 random schedules, with and
+without a heavy-first pass."""
 import os
 import subprocess
 

@@ -459,7 +459,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_grid = 0;
   a.batches_out = nullptr;
   a.queue = nullptr;
-  a.q_set = a.q_epoch = a.q_cap = 0;
+  a.q_set = a.q_epoch = a.q_cap_a = a.q_cap_b = 0;
   return a;
 }
 
@@ -600,9 +600,16 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     return slot;
   }
   slot->last_defer = false;
+  const uint32_t ord_q = fused && !ctx->tile_order
+                             ? 0u
+                             : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
   if (fused) {
-    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place)
-    const uint32_t need = a.tiles * uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
+    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place); segment
+    // A_r holds the waves of at most ord_q heavy-pass tiles, B_s of at most ceil(tiles / 8) tiles
+    const uint32_t per_tile = uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
+    const uint32_t cap_a = ord_q * per_tile;
+    const uint32_t cap_b = (a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses * per_tile;
+    const uint32_t need = vrt::kOrdClasses * (cap_a + cap_b);
     if (slot->queue_cap < need) {
       // earlier launches with the slot run on st (its stream) and may still read the old queue
       if (slot->queue && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->queue) != hipSuccess)) {
@@ -633,7 +640,8 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     a.queue = slot->queue;
     a.q_set = uint32_t(slot->q_launches & 1u);
     a.q_epoch = slot->q_epoch;
-    a.q_cap = need;
+    a.q_cap_a = cap_a;
+    a.q_cap_b = cap_b;
     slot->q_launches++;
     slot->last_queue = true;
   } else {
@@ -645,9 +653,7 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
   a.ctr_r = uint32_t(slot->epoch % 3u);
   a.ctr_w = (a.ctr_r + 1u) % 3u;
   a.ctr_z = (a.ctr_r + 2u) % 3u;
-  a.ord_q = fused && !ctx->tile_order
-                ? 0u
-                : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+  a.ord_q = ord_q;
   slot->epoch++;
   return slot;
 }

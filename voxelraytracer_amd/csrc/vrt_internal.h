@@ -61,15 +61,16 @@ struct KArgs {
   // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
   uint32_t exact_grid;
   uint32_t* batches_out;
-  // fused frame (frame_kernel, vrt_set_exact_pass 1 / 3 on colour-only bands of >= 2 rounds): one
-  // launch renders the certified pixels, runs dense exact chunks in place and queues the sparse
-  // ones, which waves that finished their own tiles claim in batches (see frame_kernel). queue: the
-  // slot's counters (two sets of kQCtrs, one 256-byte line each: see kQCtrs) then q_cap 8-byte entries
-  // {epoch << 32 | pixel id}; q_set: this launch's counter set (the kernel zeroes the other one for
-  // the next launch on the stream); q_epoch: the tag of this launch's entries (never 0; entries of
-  // earlier launches keep older tags, so the entries are never cleared)
+  // fused frame (frame_kernel + drain_kernel, vrt_set_exact_pass 1 / 3 on colour-only bands): the
+  // certified pixels, dense exact chunks in place, the sparse exact pixels queued in segments and
+  // rendered in batches by the waves that complete a batch (see frame_kernel). queue: the slot's
+  // counters (two sets of kQCtrs, one 256-byte line each) then the entries, 8 bytes each
+  // {epoch << 32 | pixel id}: 8 heavy-pass segments of q_cap_a entries, then 8 segments of q_cap_b;
+  // q_set: this launch's counter set (the kernel zeroes the other one for the next launch on the
+  // stream); q_epoch: the tag of this launch's entries (never 0; entries of earlier launches keep
+  // older tags, so the entries are never cleared)
   uint32_t* queue;
-  uint32_t q_set, q_epoch, q_cap;
+  uint32_t q_set, q_epoch, q_cap_a, q_cap_b;
 };
 #if defined(VRT_EXACT_GRID_ADAPT) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_EXACT_GRID_ADAPT is an A/B knob of make variant builds"
@@ -100,13 +101,13 @@ constexpr uint32_t kOrdCtrStride = 64;      // words between list counters (one 
 constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buffer header: 3 counter sets
 constexpr uint32_t kDeferHdr = 4 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 kinds x 2 sets
 constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave keeps its own exact-pass batch
-// fused-frame queue (KArgs::queue), per counter set one 256-byte line each: tail (reserved
-// entries), head (claimed entries), flags (1: the heavy-first pass is past its certified phase,
-// 2: every wave is), top / htop (completed shards / heavy classes), then kOrdClasses heavy-class
-// counters and kQShards completion shards (waves past their certified phase, by tile % kQShards):
-// one address per ~250 waves instead of one for all (same-address atomics serialise at ~88 per us)
-constexpr uint32_t kQShards = 64;
-constexpr uint32_t kQCtrs = 5 + kOrdClasses + kQShards;
+// fused-frame queue (KArgs::queue), per counter set one 256-byte line each: the tails (reserved
+// entries) of the 8 heavy-pass segments (A, by tile-order class) and of the 8 other segments (B, by
+// workgroup % 8), then the 8 heavy classes' completion counters. Every counter sees ~1/16 of the
+// appends or ~1/8 of the heavy waves: same-address atomics serialise (~88 per us), and a hot line
+// also stalls the texel loads that hash to its channel (r05: one shared tail, head and flags word
+// polled by every wave made C3 frames 0.6-1 ms)
+constexpr uint32_t kQCtrs = 3 * kOrdClasses;
 constexpr uint32_t kQueueHdr = 2 * kQCtrs * kOrdCtrStride;  // words before the entries (8-byte aligned)
 static_assert(kQCtrs <= 128, "one zeroing thread per counter of the other set");
 #if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)

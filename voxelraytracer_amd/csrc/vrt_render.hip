@@ -1795,9 +1795,8 @@ __device__ unsigned long long g_stamps2[kMaxStampWaves][2];
 // exact_pass_kernel, per workgroup: {start, end, XCC_ID << 32 | HW_ID, pixels | dense << 16}
 __device__ unsigned long long g_stamps4[kMaxStampWaves][4];
 
-// frame_kernel, per wave: {start, after the certified phase, after the completion counters, end,
-// cnt | in_place << 8 | set_flag << 9 | heavy_pass << 10, batches claimed, entry-wait spins,
-// polls | exact pixels rendered << 16}
+// frame_kernel, per wave: {start, after the certified phase, after the queue bookkeeping, end,
+// cnt | in_place << 8 | class drain << 9 | heavy pass << 10, full batches owned, 0, 0}
 __device__ unsigned long long g_stamps5[kMaxStampWaves][8];
 
 __device__ __forceinline__ uint32_t hw_id() {
@@ -2304,45 +2303,51 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
 
 // ------------------------------------------------------------------------ fused frame --
 //
-// frame_kernel: one launch per frame for stats-free colour-only bands of >= 2 dispatch rounds (the
-// vrt_set_exact_pass default there). The two-launch scheme (render_kernel<DEFER>, then
+// frame_kernel (+ drain_kernel): the frame for stats-free colour-only bands of >= 2 dispatch rounds
+// (the vrt_set_exact_pass default there). The two-launch scheme (render_kernel<DEFER>, then
 // exact_pass_kernel on the same stream) starts the exact work only after the last certified wave:
 // a frame's latency is the certified pass plus the exact pass's longest waves (C3: ~45 + ~75 us,
 // profiles/r04_exact/). Here the exact work starts while the certified work of the same frame runs:
 //  - tiles in heavy-first order (ordered_tile: the tiles that needed exact work in an earlier frame
-//    are dispatched first), so the exact work is known early;
+//    are dispatched first, as 8 classes of the heavy-first pass), so the exact work is known early;
 //  - a wave with >= kDeferDense pixels the certified walks cannot settle (a glass region: a
-//    coherent 8x8 tile of exact work) renders them in place at once, after publishing its
-//    progress;
-//  - a wave with fewer appends them to the launch's queue (ballot, one reservation atomic, mbcnt
-//    ranks: the north_star's __ballot compaction), and every wave, once its own tile is done,
-//    claims queued pixels in batches of kQueueBatch and renders them with the exact path: full
-//    batches at any time; a partial batch once the heavy-first pass has finished its certified
-//    phase (the queue then only grows by pixels of tiles that needed no exact work last frame) or
-//    every wave of the launch has (the last one drains the rest).
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the counters are device-scope atomics;
-// an entry is ONE 8-byte {epoch, pixel} granule written by one agent-scope (sc1, write-through)
-// store, read by agent-scope loads that wait for this launch's tag (bounded; entries of earlier
-// launches carry older tags), so no fence is needed and entries are never cleared. No wave ever
-// waits for another wave except for a reserved entry, which its producer stores right after the
-// reservation: the launch cannot deadlock at any residency. Every pixel is rendered exactly once by
-// the same exact path and epilogue as the other instances, so images are identical.
+//    coherent 8x8 tile of exact work) renders them in place at once;
+//  - a wave with fewer appends them to a queue segment (ballot, one reservation atomic, mbcnt
+//    ranks: the north_star's __ballot compaction of live rays): heavy-pass waves of class r to
+//    segment A_r, the others to B_(workgroup % 8). Batches are fixed index ranges [kQueueBatch k,
+//    kQueueBatch (k + 1)) of a segment, and the wave whose reservation covers a batch's last index
+//    renders that batch once its own tile is done: every full batch has exactly one owner, known
+//    from the reservation alone — no polling, no claim counter;
+//  - the partial last batch of A_r is rendered by the heavy-pass wave that completes class r (a
+//    per-class counter): early, since the heavy-first pass runs first; the partial last batches of
+//    the B segments (pixels of tiles that needed no exact work last frame: none with a still
+//    camera) by drain_kernel, a one-wave-per-segment launch after the frame on the same stream.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the counters are device-scope atomics,
+// one 256-byte line each, each hit by ~1/16 of the appending or ~1/8 of the heavy waves (r05: a
+// single shared tail / head / flags word polled by every wave made C3 frames 0.6-1 ms: same-address
+// atomics serialise, and a hot line stalls the texel loads of its channel). An entry is ONE 8-byte
+// {epoch, pixel} granule written by one agent-scope (sc1, write-through) store and read by
+// agent-scope loads that wait for this launch's tag (bounded; entries of earlier launches carry
+// older tags, so entries are never cleared). A wave waits only for entries reserved before its own
+// reservation, which their producers store right after reserving: no deadlock at any residency.
+// Every pixel is rendered exactly once by the same exact path and epilogue as the other
+// instances, so images are identical (tests/queue_model.cpp models the protocol on the CPU).
 #if defined(VRT_QUEUE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_QUEUE_BATCH is an A/B knob of make variant builds"
 #endif
-#ifndef VRT_QUEUE_BATCH  // pixels per claimed batch of queued exact work (<= 64)
+#ifndef VRT_QUEUE_BATCH  // pixels per batch of queued exact work (<= 64)
 #define VRT_QUEUE_BATCH 64
 #endif
 constexpr uint32_t kQueueBatch = VRT_QUEUE_BATCH;
+static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
 #if defined(VRT_FQ_DIAG) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_FQ_DIAG is a diagnostic knob of make variant builds"
 #endif
 #ifndef VRT_FQ_DIAG  // diagnostic: 1 no exact work (wrong images), 2 every exact pixel in place, 3 as 2 without the counters
 #define VRT_FQ_DIAG 0
 #endif
-static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
-constexpr uint32_t kQTail = 0, kQHead = 1, kQFlags = 2, kQTop = 3, kQHTop = 4, kQHCls = 5, kQShard = 5 + kOrdClasses;
-constexpr uint32_t kQFlagHeavy = 1u, kQFlagAll = 2u;
+static_assert(kDeferDense - 1u <= 64u, "an append crosses at most a few batch ends");
+constexpr uint32_t kQTailA = 0, kQTailB = kOrdClasses, kQHCls = 2 * kOrdClasses;
 constexpr uint32_t kQueueSpinMax = 1u << 22;  // bound of an entry wait (a bug, never a normal case)
 
 __device__ __forceinline__ uint32_t* qctr(const KArgs& a, uint32_t set, uint32_t c) {
@@ -2357,40 +2362,43 @@ __device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v) {
 // waits for the wave's outstanding vector-memory operations (an atomic's return included), so
 // that a later atomic or load is performed after an earlier one
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// first entry of segment seg (0-7: A, 8-15: B)
+__device__ __forceinline__ unsigned long long* q_seg(const KArgs& a, uint32_t seg) {
+  unsigned long long* e = reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr);
+  return seg < kOrdClasses ? e + size_t(seg) * a.q_cap_a
+                           : e + size_t(kOrdClasses) * a.q_cap_a + size_t(seg - kOrdClasses) * a.q_cap_b;
+}
 
-// The batch this wave claims next, as (first entry, count); count 0: nothing to claim now (the
-// wave stops polling). Lane 0 decides, the wave follows (uniform). Full batches any time; a partial
-// batch once the heavy-first pass (flag 1; always when it is empty) or every wave (flag 2) is past
-// its certified phase.
-__device__ __forceinline__ uint2 queue_claim(const KArgs& a, bool no_heavy_pass) {
-  uint32_t h = 0, want = 0;
-  if (lane_id() == 0) {
-    // progress, not a spin: a failed claim means another wave advanced head, which only grows
-    // up to the final tail (the bound only guards against a bug)
-    for (uint32_t tries = 0; tries < (1u << 20); ++tries) {
-      // read in this order, each after the previous one returned: flags, then head, then tail.
-      // Flag 2 implies the final tail; and head <= tail at every instant with tail monotone, so a
-      // tail read after the head read is >= it (read the other way round, other waves' appends and
-      // claims in between could put head past the tail read: tests/queue_model.cpp)
-      const uint32_t fl = q_load(qctr(a, a.q_set, kQFlags));
-      vm_drain();
-      h = q_load(qctr(a, a.q_set, kQHead));
-      vm_drain();
-      const uint32_t t = q_load(qctr(a, a.q_set, kQTail));
-      const uint32_t avail = t > h ? t - h : 0u;
-      uint32_t w = avail >= kQueueBatch ? kQueueBatch : 0u;
-      if (avail != 0u && w == 0u && (no_heavy_pass || fl != 0u)) w = avail;
-      if (w == 0u) break;
-      uint32_t expect = h;
-      if (__hip_atomic_compare_exchange_strong(qctr(a, a.q_set, kQHead), &expect, h + w, __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        want = w;
-        break;
-      }
-    }
+// The exact path for one pixel id (band row << 16 | x) and its epilogue
+__device__ __forceinline__ void exact_id(const KArgs& a, const uint16_t* __restrict__ vox, float4* __restrict__ out,
+                                         float4* ax, uint32_t e) {
+  Ctx c;
+  init_ctx(c, a, vox);
+  c.ax = ax;
+  const int px = int(e & 0xFFFFu), li = int(e >> 16);
+  if (px < a.width && li < a.rows) {  // (always: ids come from this launch's pixels)
+    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+    Counters k;
+#pragma unroll
+    for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
+    uint32_t steps = 0, flags = 0;
+    int32_t hit_vidx = -1;
+    float hit_len = 0.0f;
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
+    store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
   }
-  return make_uint2(uint32_t(__builtin_amdgcn_readfirstlane(int(h))),
-                    uint32_t(__builtin_amdgcn_readfirstlane(int(want))));
+}
+
+// entry i of segment seg, waiting for this launch's tag (~0u: never written, a bug)
+__device__ __forceinline__ uint32_t q_entry(const KArgs& a, uint32_t seg, uint32_t i) {
+  const unsigned long long* ent = q_seg(a, seg) + i;
+  for (uint32_t spins = 0;; ++spins) {  // the producer stores it right after its reservation
+    const unsigned long long v = __hip_atomic_load(ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (uint32_t(v >> 32) == a.q_epoch) return uint32_t(v);
+    if (spins >= kQueueSpinMax) return ~0u;  // never reached by a correct launch
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs a, const uint16_t* __restrict__ vox,
@@ -2404,10 +2412,20 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
 #endif
   const uint32_t first_cap = kOrdClasses * a.ord_q;
   uint32_t tile = ordered_tile(a, blockIdx.x);
-  if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
+  if (tile == ~0u) {
+#ifdef VRT_STAMPS
+    if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
+      for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = 0;
+#endif
+    return;  // whole workgroup: its tile is rendered by another slot
+  }
   tile = __builtin_amdgcn_readfirstlane(tile);
+  const bool heavy = blockIdx.x < first_cap;
+  const uint32_t cls = blockIdx.x % kOrdClasses;
+  const uint32_t seg = heavy ? cls : kOrdClasses + cls;
   const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   __shared__ float4 ax_tab[kWgThreads * 3];
+  float4* const ax = &ax_tab[threadIdx.x * kAxLane];
   bool deferred = false;
   {
     const int px = pixel_x(tx, wave, lane_id());
@@ -2415,7 +2433,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
     if (px < a.width && li < a.rows) {
       Ctx c;
       init_ctx(c, a, vox);
-      c.ax = &ax_tab[threadIdx.x * kAxLane];
+      c.ax = ax;
       const Ray ray = primary_ray(a, c, px, frame_row(a, li));
       f3 color = mk(0.0f, 0.0f, 0.0f);
       deferred = !cert_pixel<false>(c, ray, color);
@@ -2429,141 +2447,95 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   const bool in_place = VRT_FQ_DIAG == 1 ? false : (VRT_FQ_DIAG >= 2 ? cnt != 0u : cnt >= kDeferDense);
   const uint32_t l3 = lane_id();
   const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
-  const bool appended = VRT_FQ_DIAG == 0 && cnt != 0u && !in_place;
 #ifdef VRT_STAMPS
   st5[1] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (appended) {  // append: one reservation, mbcnt ranks, one granule per pixel
+  // batches this wave owns: [kb0, kb1) of its segment (the batches whose last index it reserved)
+  uint32_t kb0 = 0, kb1 = 0;
+  if (VRT_FQ_DIAG == 0 && cnt != 0u && !in_place) {  // append: one reservation, mbcnt ranks, one granule per pixel
     const uint32_t first = uint32_t(__builtin_ctzll(m));
     uint32_t base = 0;
-    if (l3 == first) base = q_add(qctr(a, a.q_set, kQTail), cnt);
+    if (l3 == first) base = q_add(qctr(a, a.q_set, seg < kOrdClasses ? kQTailA + seg : kQTailB + cls), cnt);
     base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
+    const uint32_t cap = heavy ? a.q_cap_a : a.q_cap_b;
     if (deferred) {
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
       const uint32_t i = base + rank;
-      if (i < a.q_cap)
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr) + i,
-                           (static_cast<unsigned long long>(a.q_epoch) << 32) | my_id, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (i < cap)
+        __hip_atomic_store(q_seg(a, seg) + i, (static_cast<unsigned long long>(a.q_epoch) << 32) | my_id,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // batch k ends at index kQueueBatch (k + 1) - 1; this reservation covers [base, base + cnt)
+    kb0 = (base + kQueueBatch) / kQueueBatch - 1u;
+    kb1 = (base + cnt) / kQueueBatch;
   }
-  // the heavy-first pass's classes: tiles of class r in it (lane r), and how many classes have any
-  uint32_t ncls = 0;
-  {
-    uint32_t nr = 0;
-    if (l3 < kOrdClasses) nr = min(*ord_ctr(a, a.ctr_r, l3), a.ord_q);
-    ncls = uint32_t(__builtin_popcountll(__ballot(nr != 0u)));
-    // this workgroup's class (first-pass slots only): broadcast lane (blockIdx % 8)'s count
-    nr = uint32_t(__builtin_amdgcn_readlane(int(nr), int(blockIdx.x % kOrdClasses)));
-    if (l3 == 0 && VRT_FQ_DIAG == 3) order_record(a, tile, cnt != 0u);
-    if (l3 == 0 && VRT_FQ_DIAG != 3) {
-      // past the certified phase (the reservation above performed first): completion shards by
-      // tile, the shard's last wave counts the shard; the last shard's last wave sets flag 2. The
-      // heavy-first pass likewise by class, flag 1.
-      vm_drain();
-      const uint32_t shard = tile % kQShards;
-      const uint32_t shard_waves = (a.tiles / kQShards + (shard < a.tiles % kQShards ? 1u : 0u)) * uint32_t(kWgWaves);
-      uint32_t flags = 0;
-      if (q_add(qctr(a, a.q_set, kQShard + shard), 1u) + 1u == shard_waves &&
-          q_add(qctr(a, a.q_set, kQTop), 1u) + 1u == min(a.tiles, kQShards))
-        flags |= kQFlagAll;
-      if (blockIdx.x < first_cap) {
-        const uint32_t r = blockIdx.x % kOrdClasses;
-        if (q_add(qctr(a, a.q_set, kQHCls + r), 1u) + 1u == nr * uint32_t(kWgWaves) &&
-            q_add(qctr(a, a.q_set, kQHTop), 1u) + 1u == ncls)
-          flags |= kQFlagHeavy;
+  // the heavy-pass wave that completes its class drains the class segment's partial last batch
+  uint32_t drain_lo = 0, drain_hi = 0;
+  if (heavy && VRT_FQ_DIAG != 3) {
+    uint32_t nr = 0;  // heavy-pass tiles of this class
+    if (l3 == 0) {
+      nr = min(*ord_ctr(a, a.ctr_r, cls), a.ord_q);
+      vm_drain();  // this wave's reservation is performed before it counts as done
+      if (q_add(qctr(a, a.q_set, kQHCls + cls), 1u) + 1u == nr * uint32_t(kWgWaves)) {
+        vm_drain();
+        const uint32_t t = q_load(qctr(a, a.q_set, kQTailA + cls));  // final: every class wave has reserved
+        drain_lo = t / kQueueBatch * kQueueBatch;
+        drain_hi = t;
       }
-      if (flags) __hip_atomic_fetch_or(qctr(a, a.q_set, kQFlags), flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
-      ncls |= flags << 16;  // (lane 0 only: whether this wave set a flag)
     }
+    drain_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_lo)));
+    drain_hi = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_hi)));
   }
-  // the exact phase: this wave's own pixels in place, then claimed batches. A wave polls the queue
-  // only when something it did can have made a batch claimable — its appends, a flag it set, the
-  // end of a batch it rendered — so the counters see a few thousand polls per frame, not one per wave
-  const bool set_flag = (uint32_t(__builtin_amdgcn_readfirstlane(int(ncls))) >> 16) != 0u;
-  ncls &= 0xFFFFu;
+  if (l3 == 0) order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
 #ifdef VRT_STAMPS
   st5[2] = __builtin_amdgcn_s_memrealtime();
-  st5[4] = cnt | (in_place ? 0x100u : 0u) | (set_flag ? 0x200u : 0u) | (blockIdx.x < first_cap ? 0x400u : 0u);
+  st5[4] = cnt | (in_place ? 0x100u : 0u) | (drain_hi > drain_lo ? 0x200u : 0u) | (heavy ? 0x400u : 0u);
+  st5[5] = kb1 - kb0;
 #endif
-  const bool no_heavy_pass = ncls == 0u;
-  bool own = in_place;
-  bool poll = VRT_FQ_DIAG == 0 && (appended || set_flag || in_place);
-  bool prio = false;
-  for (;;) {
-    bool act = false;
-    uint32_t e = 0;
-    if (own) {
-      own = false;
+  // the exact phase: own pixels in place (item 0), owned full batches (1..nb), the class drain
+  // (nb + 1); one call site of the exact path
+  const uint32_t nb = kb1 - kb0;
+  const bool drain = drain_hi > drain_lo;
+  const uint32_t n_items = 1u + nb + (drain ? 1u : 0u);
+  if (in_place || nb != 0u || drain) {
+    if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);  // few long waves first
+  }
+  for (uint32_t it = in_place ? 0u : 1u; it < n_items; ++it) {
+    bool act;
+    uint32_t e = my_id;
+    if (it == 0u) {
       act = deferred;
-      e = my_id;
+    } else if (it <= nb) {
+      const uint32_t i = (kb0 + it - 1u) * kQueueBatch + l3;
+      act = l3 < kQueueBatch && i < (heavy ? a.q_cap_a : a.q_cap_b);
+      if (act) e = q_entry(a, seg, i);
     } else {
-      if (!poll) break;
-      const uint2 b = queue_claim(a, no_heavy_pass);
-#ifdef VRT_STAMPS
-      st5[7] += 1u;
-      st5[5] += b.y != 0u ? 1u : 0u;
-#endif
-      if (b.y == 0u) break;
-      act = l3 < b.y && b.x + l3 < a.q_cap;  // (the capacity bounds every reservation)
-      if (act) {
-        const unsigned long long* ent = reinterpret_cast<const unsigned long long*>(a.queue + kQueueHdr) + (b.x + l3);
-        unsigned long long v = 0;
-        for (uint32_t spins = 0;; ++spins) {  // the producer stores it right after its reservation
-          v = __hip_atomic_load(ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (uint32_t(v >> 32) == a.q_epoch) break;
-          if (spins >= kQueueSpinMax) {
-            v = ~0ull;  // never reached by a correct launch: the pixel stays unrendered
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-#ifdef VRT_STAMPS
-          st5[6] += 1u;
-#endif
-        }
-        e = uint32_t(v);
-        act = e != ~0u;
-      }
+      const uint32_t i = drain_lo + l3;
+      act = i < drain_hi && i < a.q_cap_a;
+      if (act) e = q_entry(a, cls, i);
     }
-    if (!prio && VRT_EXACT_PRIO > 0) {  // exact work: few long waves, their chains issue first
-      __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
-      prio = true;
-    }
-    if (act) {
-      Ctx c;
-      init_ctx(c, a, vox);
-      c.ax = &ax_tab[threadIdx.x * kAxLane];
-      const int px = int(e & 0xFFFFu), li = int(e >> 16);
-      if (px < a.width && li < a.rows) {  // (always: ids come from this launch's pixels)
-        const Ray ray = primary_ray(a, c, px, frame_row(a, li));
-        Counters k;
-#pragma unroll
-        for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
-        uint32_t steps = 0, flags = 0;
-        int32_t hit_vidx = -1;
-        float hit_len = 0.0f;
-        f3 color = mk(0.0f, 0.0f, 0.0f);
-        (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
-        store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
-      }
-    }
-#ifdef VRT_STAMPS
-    st5[7] += uint64_t(__builtin_popcountll(__ballot(act))) << 16;
-#endif
-    poll = VRT_FQ_DIAG == 0;  // after rendering a batch
+    if (act && e != ~0u) exact_id(a, vox, out, ax, e);
   }
 #ifdef VRT_STAMPS
-  {
-    st5[3] = __builtin_amdgcn_s_memrealtime();
-    // spins: the wave's largest lane count
-    uint32_t sp = uint32_t(st5[6]);
-    for (int off = 32; off > 0; off >>= 1) sp = max(sp, uint32_t(__shfl_xor(int(sp), off, 64)));
-    st5[6] = sp;
-    if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
-      for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = st5[q];
-  }
+  st5[3] = __builtin_amdgcn_s_memrealtime();
+  if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
+    for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = st5[q];
 #endif
+}
+
+// The partial last batches of the fused frame's B segments (pixels of tiles outside the
+// heavy-first pass), after frame_kernel on the same stream: one wave per segment; it exits at once
+// when the segment's entries all fell into full batches (none: a still camera).
+__global__ void __launch_bounds__(64) drain_kernel(KArgs a, const uint16_t* __restrict__ vox, float4* __restrict__ out) {
+  const uint32_t s = blockIdx.x;  // B segment
+  const uint32_t t = q_load(qctr(a, a.q_set, kQTailB + s));
+  const uint32_t lo = t / kQueueBatch * kQueueBatch;
+  const uint32_t i = lo + threadIdx.x;
+  if (t == lo || i >= t || i >= a.q_cap_b) return;
+  if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
+  __shared__ float4 ax_tab[64 * 3];
+  const uint32_t e = q_entry(a, kOrdClasses + s, i);
+  if (e != ~0u) exact_id(a, vox, out, &ax_tab[threadIdx.x * kAxLane], e);
 }
 
 // Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
@@ -2827,11 +2799,15 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // ~5 %), exact walks only (0)
   // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
   // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
-  if (a.queue && a.order && !stats && a.cert == 2 && !a.textured) {  // the fused frame (one launch)
-    if (ev_begin || ev_end)
-      hipExtLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, ev_begin, ev_end, 0, a, vox, out);
+  if (a.queue && a.order && !stats && a.cert == 2 && !a.textured) {  // the fused frame
+    if (ev_begin)
+      hipExtLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out);
     else
       hipLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, a, vox, out);
+    if (ev_end)
+      hipExtLaunchKernelGGL(drain_kernel, dim3(kOrdClasses), dim3(64), 0, s, nullptr, ev_end, 0, a, vox, out);
+    else
+      hipLaunchKernelGGL(drain_kernel, dim3(kOrdClasses), dim3(64), 0, s, a, vox, out);
     return;
   }
   if (a.defer && !stats && a.cert == 2) {

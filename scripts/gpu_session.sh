@@ -69,6 +69,15 @@ for st in "$@"; do
           echo "varmodes $ln $vc steps $vs ep$m $(grep -o '"ms_per_step": [0-9.]*' $OUT/vm_${ln}_${vc}_s${vs}_m$m.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/vm_${ln}_${vc}_s${vs}_m$m.log | head -1)"
         done
       done; unset VRT_LIB ;;
+    drvx)  # driver-shaped runs with extra bench flags, ROUNDS alternating: drvx:CFG,ROUNDS,"FLAGS1|FLAGS2|..."
+      IFS=, read xc xr xf <<< "$arg"
+      IFS='|' read -ra xfl <<< "$xf"
+      for ((i = 1; i <= ${xr:-2}; i++)); do
+        for j in "${!xfl[@]}"; do
+          TAILN=0 run drvx_${xc}_${j}_$i 150 python bench.py --config $xc --steps 20 --warmup 5 --cpu-seconds 0 --no-verify --frame-events ${xfl[$j]}
+          echo "drvx $xc [${xfl[$j]}] $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_events_ms": \[[^]]*\]' $OUT/drvx_${xc}_${j}_$i.log | head -1)"
+        done
+      done ;;
     fstamps)  # fused-frame wave timeline (build/diag/libvrt_stamps.so): fstamps:CFG[,K[,RANK[,MODE]]]
       IFS=, read fc fk fr fm <<< "$arg"
       VRT_LIB=$ROOT/build/diag/libvrt_stamps.so run fstamps_${fc}_k${fk:-1}_r${fr:-0}_m${fm:-3} 120 python -u scripts/frame_stamps.py --config $fc --ranks ${fk:-1} --rank ${fr:-0} --mode ${fm:-3} ;;

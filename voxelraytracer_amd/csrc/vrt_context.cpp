@@ -600,9 +600,15 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     return slot;
   }
   slot->last_defer = false;
+#if defined(VRT_FQ_DIAG) && VRT_FQ_DIAG >= 4  // diagnostic builds: no heavy-first pass
+  const uint32_t ord_q = fused
+                             ? 0u
+                             : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+#else
   const uint32_t ord_q = fused && !ctx->tile_order
                              ? 0u
                              : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+#endif
   if (fused) {
     // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place); segment
     // A_r holds the waves of at most ord_q heavy-pass tiles, B_s of at most ceil(tiles / 8) tiles

@@ -2343,7 +2343,9 @@ static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pix
 #if defined(VRT_FQ_DIAG) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_FQ_DIAG is a diagnostic knob of make variant builds"
 #endif
-#ifndef VRT_FQ_DIAG  // diagnostic: 1 no exact work (wrong images), 2 every exact pixel in place, 3 as 2 without the counters
+// diagnostic: 1 no exact work (wrong images), 2 every exact pixel in place, 3 as 2 without the
+// counters, 4 as 1 without the tile-order bookkeeping, 5 as 4 without the exact path in the code
+#ifndef VRT_FQ_DIAG
 #define VRT_FQ_DIAG 0
 #endif
 static_assert(kDeferDense - 1u <= 64u, "an append crosses at most a few batch ends");
@@ -2444,7 +2446,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   }
   const unsigned long long m = __ballot(deferred);
   const uint32_t cnt = uint32_t(__builtin_popcountll(m));
-  const bool in_place = VRT_FQ_DIAG == 1 ? false : (VRT_FQ_DIAG >= 2 ? cnt != 0u : cnt >= kDeferDense);
+  const bool in_place = (VRT_FQ_DIAG == 1 || VRT_FQ_DIAG >= 4) ? false : (VRT_FQ_DIAG >= 2 ? cnt != 0u : cnt >= kDeferDense);
   const uint32_t l3 = lane_id();
   const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
 #ifdef VRT_STAMPS
@@ -2471,7 +2473,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   }
   // the heavy-pass wave that completes its class drains the class segment's partial last batch
   uint32_t drain_lo = 0, drain_hi = 0;
-  if (heavy && VRT_FQ_DIAG != 3) {
+  if (heavy && VRT_FQ_DIAG != 3 && VRT_FQ_DIAG < 4) {
     uint32_t nr = 0;  // heavy-pass tiles of this class
     if (l3 == 0) {
       nr = min(*ord_ctr(a, a.ctr_r, cls), a.ord_q);
@@ -2486,7 +2488,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
     drain_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_lo)));
     drain_hi = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_hi)));
   }
-  if (l3 == 0) order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
+  if (l3 == 0 && VRT_FQ_DIAG < 4) order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
 #ifdef VRT_STAMPS
   st5[2] = __builtin_amdgcn_s_memrealtime();
   st5[4] = cnt | (in_place ? 0x100u : 0u) | (drain_hi > drain_lo ? 0x200u : 0u) | (heavy ? 0x400u : 0u);
@@ -2514,7 +2516,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
       act = i < drain_hi && i < a.q_cap_a;
       if (act) e = q_entry(a, cls, i);
     }
-    if (act && e != ~0u) exact_id(a, vox, out, ax, e);
+    if (VRT_FQ_DIAG < 5 && act && e != ~0u) exact_id(a, vox, out, ax, e);
   }
 #ifdef VRT_STAMPS
   st5[3] = __builtin_amdgcn_s_memrealtime();

@@ -47,8 +47,17 @@ constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 
 // ceil(tiles / 8) tiles' pixels each. Allocated per tile-order slot at its first deferred launch,
 // sized for that band (a 1080p band: 8.3 MB; until r03 every slot was sized for 65 536 tiles up
 // front, 537 MB per device).
-size_t defer_words(uint32_t tiles) {
-  return vrt::kDeferHdr + size_t(vrt::kOrdClasses) * ((tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * vrt::kWgThreads;
+// tiles of the largest segment: workgroup % 8 classes, or (VRT_DEFER_SEG 1 builds) column blocks
+uint32_t defer_seg_tiles(uint32_t tiles, uint32_t tiles_x) {
+#if defined(VRT_DEFER_SEG) && VRT_DEFER_SEG == 1
+  return (tiles_x + vrt::kOrdClasses - 1u) / vrt::kOrdClasses * (tiles / tiles_x);
+#else
+  (void)tiles_x;
+  return (tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses;
+#endif
+}
+size_t defer_words(uint32_t tiles, uint32_t tiles_x) {
+  return vrt::kDeferHdr + size_t(vrt::kOrdClasses) * defer_seg_tiles(tiles, tiles_x) * vrt::kWgThreads;
 }
 // first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
 // 8160 tiles are heavy)
@@ -549,7 +558,7 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
   if (!slot) return nullptr;
   if (defer) {
     slot->last_queue = false;  // both counter sets zeroed whenever the slot's previous launch was not one
-    const size_t need = defer_words(a.tiles);
+    const size_t need = defer_words(a.tiles, a.tiles_x);
     if (slot->defer_cap < need) {  // first deferred launch of this band on the slot (or a larger band)
       // earlier launches with the slot run on st (its stream) and may still read the old list
       if (slot->defer && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->defer) != hipSuccess)) return slot;
@@ -569,7 +578,7 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     }
     a.defer = d;
     a.defer_e = uint32_t(slot->defer_epoch & 1u);
-    a.defer_seg = uint32_t((a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses) * uint32_t(vrt::kWgThreads);
+    a.defer_seg = defer_seg_tiles(a.tiles, a.tiles_x) * uint32_t(vrt::kWgThreads);
     // bands of under 4 rounds: the exact pass's latency follows a short certified pass
     a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
     if (VRT_EXACT_GRID_ADAPT && !a.exact_fat) {

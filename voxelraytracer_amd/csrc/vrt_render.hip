@@ -2039,6 +2039,12 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 #ifndef VRT_EXACT_WAVES
 #define VRT_EXACT_WAVES VRT_MIN_WAVES
 #endif
+#if defined(VRT_DEFER_SEG) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DEFER_SEG is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_DEFER_SEG
+#define VRT_DEFER_SEG 0
+#endif
 template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false>
 __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
@@ -2126,7 +2132,10 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
     const unsigned long long m = __ballot(deferred);
     if (m != 0ull) {
-      const uint32_t seg = blockIdx.x % kOrdClasses, first = uint32_t(__builtin_ctzll(m));
+      // segment: the XCD class of the workgroup (0), or the tile's column block of the band (1:
+      // consecutive list entries then come from nearby tiles, so a sparse batch's rays are alike)
+      const uint32_t seg = VRT_DEFER_SEG == 1 ? tx * kOrdClasses / a.tiles_x : blockIdx.x % kOrdClasses;
+      const uint32_t first = uint32_t(__builtin_ctzll(m));
       const uint32_t cnt = uint32_t(__builtin_popcountll(m));
       // a wave with many deferred pixels (a glass region) keeps them as a chunk of its own, each
       // at its lane (a coherent 8x8 tile of exact work); the others append compactly

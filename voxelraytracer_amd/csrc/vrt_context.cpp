@@ -59,17 +59,9 @@ uint32_t defer_seg_tiles(uint32_t tiles, uint32_t tiles_x) {
 size_t defer_words(uint32_t tiles, uint32_t tiles_x) {
   return vrt::kDeferHdr + size_t(vrt::kOrdClasses) * defer_seg_tiles(tiles, tiles_x) * vrt::kWgThreads;
 }
-// first-pass workgroups of a tile-order launch: tiles / VRT_ORD_DIV (C3: ~1600 of a part launch's
-// 8160 tiles are heavy)
 #if (defined(VRT_DEV_NOQUERY) || defined(VRT_DEV_NOCONSUME) || defined(VRT_DEV_NOCSWAIT)) && \
     !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_DEV_* are diagnostic knobs of make variant builds"
-#endif
-#if defined(VRT_ORD_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_ORD_DIV is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_ORD_DIV
-#define VRT_ORD_DIV 4
 #endif
 // Filtered frames rotate through kRing buffers: frame f reads ring[(f-1) % kRing] (the temporal
 // history) and writes ring[f % kRing]. A device-output frame (vrt_render_frame_device) is handed
@@ -468,7 +460,7 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_grid = 0;
   a.batches_out = nullptr;
   a.queue = nullptr;
-  a.q_set = a.q_epoch = a.q_cap_a = a.q_cap_b = 0;
+  a.q_set = a.q_epoch = a.q_cap_b = 0;
   return a;
 }
 
@@ -612,50 +604,54 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
 #if defined(VRT_FQ_DIAG) && VRT_FQ_DIAG >= 4  // diagnostic builds: no heavy-first pass
   const uint32_t ord_q = fused
                              ? 0u
-                             : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+                             : vrt::ord_q_for(a.tiles);
 #else
   const uint32_t ord_q = fused && !ctx->tile_order
                              ? 0u
-                             : (a.tiles + vrt::kOrdClasses * VRT_ORD_DIV - 1u) / (vrt::kOrdClasses * VRT_ORD_DIV);
+                             : vrt::ord_q_for(a.tiles);
 #endif
+  bool heavy_pass = true;
   if (fused) {
-    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place); segment
-    // A_r holds the waves of at most ord_q heavy-pass tiles, B_s of at most ceil(tiles / 8) tiles
-    const uint32_t per_tile = uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
-    const uint32_t cap_a = ord_q * per_tile;
-    const uint32_t cap_b = (a.tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses * per_tile;
-    const uint32_t need = vrt::kOrdClasses * (cap_a + cap_b);
-    if (slot->queue_cap < need) {
+    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place); every
+    // segment holds the pixels of at most one column block's tiles
+    const uint32_t cap_b = vrt::q_block_tiles(a.tiles_x, a.tiles) * uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
+    const uint32_t need = 2u * vrt::kOrdClasses * cap_b;  // entries
+    const size_t words = size_t(vrt::kQueueHdr) + vrt::q_tag_words(a.tiles) + 2u * size_t(need);
+    if (slot->queue_cap < words) {
       // earlier launches with the slot run on st (its stream) and may still read the old queue
       if (slot->queue && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->queue) != hipSuccess)) {
+        slot->queue = nullptr;
+        slot->queue_cap = 0;
         slot->last_queue = false;
         return slot;
       }
       slot->queue = nullptr;
       slot->queue_cap = 0;
-      const size_t bytes = (size_t(vrt::kQueueHdr) + 2u * size_t(need)) * sizeof(uint32_t);
-      if (hipMalloc(&slot->queue, bytes) != hipSuccess) {
+      if (hipMalloc(&slot->queue, words * sizeof(uint32_t)) != hipSuccess) {
         slot->queue = nullptr;
         slot->last_queue = false;
         return slot;  // no queue: the in-lane path (order only) below
       }
-      // entries start with tag 0, which no launch uses
-      if (hipMemsetAsync(slot->queue, 0, bytes, st) != hipSuccess) {
+      // entries and tile tags start with tag 0, which no launch uses
+      if (hipMemsetAsync(slot->queue, 0, words * sizeof(uint32_t), st) != hipSuccess) {
         slot->last_queue = false;
         return slot;
       }
-      slot->queue_cap = need;
+      slot->queue_cap = uint32_t(words);
       slot->last_queue = false;
     }
-    if (!slot->last_queue) {  // both counter sets zeroed whenever the slot's last launch was not fused
+    if (!slot->last_queue) {
+      // the slot's last launch was not a fused one: zero the counters and the heavy-tile counts,
+      // and run this launch without a heavy-first pass (the tile order's ranks and lists of other
+      // launches carry no column-block counts); it records them for the next launch
       if (hipMemsetAsync(slot->queue, 0, vrt::kQueueHdr * sizeof(uint32_t), st) != hipSuccess) return slot;
       slot->q_launches = 0;
+      heavy_pass = false;
     }
     if (++slot->q_epoch == 0u) slot->q_epoch = 1u;  // (a wrap would take 2^32 frames)
     a.queue = slot->queue;
     a.q_set = uint32_t(slot->q_launches & 1u);
     a.q_epoch = slot->q_epoch;
-    a.q_cap_a = cap_a;
     a.q_cap_b = cap_b;
     slot->q_launches++;
     slot->last_queue = true;
@@ -668,7 +664,7 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
   a.ctr_r = uint32_t(slot->epoch % 3u);
   a.ctr_w = (a.ctr_r + 1u) % 3u;
   a.ctr_z = (a.ctr_r + 2u) % 3u;
-  a.ord_q = ord_q;
+  a.ord_q = heavy_pass ? ord_q : 0u;
   slot->epoch++;
   return slot;
 }

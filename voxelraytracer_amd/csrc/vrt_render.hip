@@ -2358,12 +2358,18 @@ static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pix
 #define VRT_FQ_DIAG 0
 #endif
 static_assert(kDeferDense - 1u <= 64u, "an append crosses at most a few batch ends");
-constexpr uint32_t kQTailA = 0, kQTailB = kOrdClasses, kQHCls = 2 * kOrdClasses;
+constexpr uint32_t kQTailA = 0, kQTailB = kOrdClasses, kQHSeg = 2 * kOrdClasses;
 constexpr uint32_t kQueueSpinMax = 1u << 22;  // bound of an entry wait (a bug, never a normal case)
 
 __device__ __forceinline__ uint32_t* qctr(const KArgs& a, uint32_t set, uint32_t c) {
   return a.queue + (set * kQCtrs + c) * kOrdCtrStride;
 }
+// heavy-pass tiles of column block s, in the tile order's rotating counter set `set`
+__device__ __forceinline__ uint32_t* q_hseg(const KArgs& a, uint32_t set, uint32_t s) {
+  return a.queue + kQHSegHdr + (set * kOrdClasses + s) * kOrdCtrStride;
+}
+// tile t's tag: the epoch of the last launch that recorded it as heavy
+__device__ __forceinline__ uint32_t* q_tag(const KArgs& a, uint32_t t) { return a.queue + kQueueHdr + t; }
 __device__ __forceinline__ uint32_t q_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2373,12 +2379,14 @@ __device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v) {
 // waits for the wave's outstanding vector-memory operations (an atomic's return included), so
 // that a later atomic or load is performed after an earlier one
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// first entry of segment seg (0-7: A, 8-15: B)
+// first entry of segment seg (0-7: A, 8-15: B; segment s % 8 = column block s % 8 of the band)
 __device__ __forceinline__ unsigned long long* q_seg(const KArgs& a, uint32_t seg) {
-  unsigned long long* e = reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr);
-  return seg < kOrdClasses ? e + size_t(seg) * a.q_cap_a
-                           : e + size_t(kOrdClasses) * a.q_cap_a + size_t(seg - kOrdClasses) * a.q_cap_b;
+  return reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr + q_tag_words(a.tiles)) + size_t(seg) * a.q_cap_b;
 }
+// the band's column block of tile column tx: consecutive queue entries come from nearby tiles, so
+// a batch's rays are alike (sparse exact waves 57 -> 49 us median at C3 against the 8 XCD classes'
+// every-8th-tile order, profiles/r05_s8)
+__device__ __forceinline__ uint32_t col_block(const KArgs& a, uint32_t tx) { return tx * kOrdClasses / a.tiles_x; }
 
 // The exact path for one pixel id (band row << 16 | x) and its epilogue
 __device__ __forceinline__ void exact_id(const KArgs& a, const uint16_t* __restrict__ vox, float4* __restrict__ out,
@@ -2412,17 +2420,64 @@ __device__ __forceinline__ uint32_t q_entry(const KArgs& a, uint32_t seg, uint32
   }
 }
 
+// The fused frame's tile order (the heavy-first scheme of ordered_tile with its lists, ranks and
+// counter rotation, but bookkept only by the waves that had exact work: a per-wave returning atomic
+// at the end of every wave cost C3 ~25 % per frame, profiles/r05_s8 fq1 vs fq4). Workgroup L < 8 ord_q
+// renders entry n - 1 - L / 8 of class L % 8's list (n = its length, at most ord_q); L = 8 ord_q + t
+// renders tile t unless its rank is in [1, ord_q], and clears the rank it read (that rank set is the
+// one the next launch writes, which records only heavy tiles). With ord_q == 0 (the first fused
+// launch of a slot, or the tile order off) every tile is in the second pass, and the rendering
+// workgroup also clears the rank this launch writes (it may hold another kind of launch's ranks).
+__device__ __forceinline__ uint32_t fq_tile(const KArgs& a, uint32_t L, bool& heavy) {
+  const uint32_t cap = kOrdClasses * a.ord_q;
+  heavy = L < cap;
+  if (L < cap) {
+    const uint32_t r = L % kOrdClasses, j = L / kOrdClasses;
+    const uint32_t n = min(*ord_ctr(a, a.ctr_r, r), a.ord_q);
+    return j < n ? ord_list(a, a.ord_r)[(n - 1u - j) * kOrdClasses + r] : ~0u;
+  }
+  const uint32_t t = L - cap;
+  uint32_t* rank = ord_rank(a, a.ord_r) + t;
+  const uint32_t rk = *rank;
+  __syncthreads();  // both waves read it before it is cleared
+  if (threadIdx.x == 0) {
+    *rank = 0u;
+    if (a.ord_q == 0u) ord_rank(a, a.ord_w)[t] = 0u;
+  }
+  return rk - 1u < a.ord_q ? ~0u : t;  // rank 0 wraps to ~0u: not in the first pass
+}
+
+// A wave that had exact work files its tile for the next launch's heavy-first pass: the first such
+// wave of the tile (the tile's tag is this launch's epoch after it) appends the tile to its class's
+// list, sets its rank, and counts it in its column block when it will be in the next first pass.
+__device__ __forceinline__ void fq_record(const KArgs& a, uint32_t tile, uint32_t tx) {
+  if (__hip_atomic_exchange(q_tag(a, tile), a.q_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.q_epoch)
+    return;
+  const uint32_t r = tile % kOrdClasses;
+  const uint32_t k = q_add(ord_ctr(a, a.ctr_w, r), 1u);  // <= tiles / 8: one per tile of class r
+  ord_list(a, a.ord_w)[k * kOrdClasses + r] = tile;
+  ord_rank(a, a.ord_w)[tile] = k + 1u;
+  if (k < ord_q_for(a.tiles)) q_add(q_hseg(a, a.ctr_w, col_block(a, tx)), 1u);
+}
+
 __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                            float4* __restrict__ out) {
-  if (blockIdx.x == 0 && threadIdx.x < kQCtrs)  // the other set, for the next launch on the stream
-    *qctr(a, a.q_set ^ 1u, threadIdx.x) = 0u;
+  if (blockIdx.x == 0) {
+    // for later launches on the stream: the other counter set (the next launch), and the
+    // rotating sets the launch after the next appends to
+    if (threadIdx.x < kQCtrs) *qctr(a, a.q_set ^ 1u, threadIdx.x) = 0u;
+    if (threadIdx.x < kOrdClasses) {
+      *q_hseg(a, a.ctr_z, threadIdx.x) = 0u;
+      *ord_ctr(a, a.ctr_z, threadIdx.x) = 0u;
+    }
+  }
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
 #ifdef VRT_STAMPS
   const uint32_t sw = blockIdx.x * kWgWaves + uint32_t(wave);
   unsigned long long st5[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
 #endif
-  const uint32_t first_cap = kOrdClasses * a.ord_q;
-  uint32_t tile = ordered_tile(a, blockIdx.x);
+  bool heavy;
+  uint32_t tile = fq_tile(a, blockIdx.x, heavy);
   if (tile == ~0u) {
 #ifdef VRT_STAMPS
     if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
@@ -2431,10 +2486,9 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
     return;  // whole workgroup: its tile is rendered by another slot
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
-  const bool heavy = blockIdx.x < first_cap;
-  const uint32_t cls = blockIdx.x % kOrdClasses;
-  const uint32_t seg = heavy ? cls : kOrdClasses + cls;
   const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  const uint32_t cb = col_block(a, tx);
+  const uint32_t seg = heavy ? cb : kOrdClasses + cb;
   __shared__ float4 ax_tab[kWgThreads * 3];
   float4* const ax = &ax_tab[threadIdx.x * kAxLane];
   bool deferred = false;
@@ -2466,44 +2520,42 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
   if (VRT_FQ_DIAG == 0 && cnt != 0u && !in_place) {  // append: one reservation, mbcnt ranks, one granule per pixel
     const uint32_t first = uint32_t(__builtin_ctzll(m));
     uint32_t base = 0;
-    if (l3 == first) base = q_add(qctr(a, a.q_set, seg < kOrdClasses ? kQTailA + seg : kQTailB + cls), cnt);
+    if (l3 == first) base = q_add(qctr(a, a.q_set, heavy ? kQTailA + cb : kQTailB + cb), cnt);
     base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
-    const uint32_t cap = heavy ? a.q_cap_a : a.q_cap_b;
     if (deferred) {
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
       const uint32_t i = base + rank;
-      if (i < cap)
+      if (i < a.q_cap_b)
         __hip_atomic_store(q_seg(a, seg) + i, (static_cast<unsigned long long>(a.q_epoch) << 32) | my_id,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // batch k ends at index kQueueBatch (k + 1) - 1; this reservation covers [base, base + cnt)
-    kb0 = (base + kQueueBatch) / kQueueBatch - 1u;
+    kb0 = base / kQueueBatch;
     kb1 = (base + cnt) / kQueueBatch;
   }
-  // the heavy-pass wave that completes its class drains the class segment's partial last batch
+  // the heavy-pass wave that completes its column block drains that A segment's partial last batch
   uint32_t drain_lo = 0, drain_hi = 0;
-  if (heavy && VRT_FQ_DIAG != 3 && VRT_FQ_DIAG < 4) {
-    uint32_t nr = 0;  // heavy-pass tiles of this class
-    if (l3 == 0) {
-      nr = min(*ord_ctr(a, a.ctr_r, cls), a.ord_q);
+  if (l3 == 0) {
+    if (cnt != 0u && VRT_FQ_DIAG < 4) fq_record(a, tile, tx);  // heavy tile for the next launch's order
+    if (heavy && VRT_FQ_DIAG != 3) {
+      const uint32_t nseg = *q_hseg(a, a.ctr_r, cb);  // heavy-pass tiles of this column block
       vm_drain();  // this wave's reservation is performed before it counts as done
-      if (q_add(qctr(a, a.q_set, kQHCls + cls), 1u) + 1u == nr * uint32_t(kWgWaves)) {
+      if (q_add(qctr(a, a.q_set, kQHSeg + cb), 1u) + 1u == nseg * uint32_t(kWgWaves)) {
         vm_drain();
-        const uint32_t t = q_load(qctr(a, a.q_set, kQTailA + cls));  // final: every class wave has reserved
+        const uint32_t t = q_load(qctr(a, a.q_set, kQTailA + cb));  // final: every such wave has reserved
         drain_lo = t / kQueueBatch * kQueueBatch;
         drain_hi = t;
       }
     }
-    drain_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_lo)));
-    drain_hi = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_hi)));
   }
-  if (l3 == 0 && VRT_FQ_DIAG < 4) order_record(a, tile, cnt != 0u);  // heavy tile for the next launch's order
+  drain_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_lo)));
+  drain_hi = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_hi)));
 #ifdef VRT_STAMPS
   st5[2] = __builtin_amdgcn_s_memrealtime();
   st5[4] = cnt | (in_place ? 0x100u : 0u) | (drain_hi > drain_lo ? 0x200u : 0u) | (heavy ? 0x400u : 0u);
   st5[5] = kb1 - kb0;
 #endif
-  // the exact phase: own pixels in place (item 0), owned full batches (1..nb), the class drain
+  // the exact phase: own pixels in place (item 0), owned full batches (1..nb), the block drain
   // (nb + 1); one call site of the exact path
   const uint32_t nb = kb1 - kb0;
   const bool drain = drain_hi > drain_lo;
@@ -2518,12 +2570,12 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
       act = deferred;
     } else if (it <= nb) {
       const uint32_t i = (kb0 + it - 1u) * kQueueBatch + l3;
-      act = l3 < kQueueBatch && i < (heavy ? a.q_cap_a : a.q_cap_b);
+      act = l3 < kQueueBatch && i < a.q_cap_b;
       if (act) e = q_entry(a, seg, i);
     } else {
       const uint32_t i = drain_lo + l3;
-      act = i < drain_hi && i < a.q_cap_a;
-      if (act) e = q_entry(a, cls, i);
+      act = i < drain_hi && i < a.q_cap_b;
+      if (act) e = q_entry(a, cb, i);
     }
     if (VRT_FQ_DIAG < 5 && act && e != ~0u) exact_id(a, vox, out, ax, e);
   }
@@ -2538,7 +2590,7 @@ __global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs 
 // heavy-first pass), after frame_kernel on the same stream: one wave per segment; it exits at once
 // when the segment's entries all fell into full batches (none: a still camera).
 __global__ void __launch_bounds__(64) drain_kernel(KArgs a, const uint16_t* __restrict__ vox, float4* __restrict__ out) {
-  const uint32_t s = blockIdx.x;  // B segment
+  const uint32_t s = blockIdx.x;  // B segment (column block s)
   const uint32_t t = q_load(qctr(a, a.q_set, kQTailB + s));
   const uint32_t lo = t / kQueueBatch * kQueueBatch;
   const uint32_t i = lo + threadIdx.x;

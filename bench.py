@@ -108,9 +108,8 @@ def parse():
                          "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
     ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1, 2, 3],
                     help="pixels the certified walks cannot settle (vrt_set_exact_pass): 1 automatic "
-                         "(launches of >= 2 rounds of resident waves: the fused frame), 2 a second, "
-                         "compacted exact-pass kernel, 3 the fused frame at any size, 0 in their own "
-                         "lanes")
+                         "(launches of >= 2 rounds of resident waves: a second, compacted exact-pass "
+                         "kernel), 2 that kernel at any size, 3 the fused frame, 0 in their own lanes")
     ap.add_argument("--tile-order", type=int, default=1, choices=[0, 1],
                     help="heavy-first tile order of in-lane launches with glass (vrt_set_tile_order)")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],

@@ -221,14 +221,15 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
  *   0: the exact path runs in the pixel's own lane (heavy-first tile order, vrt_set_tile_order);
  *   1 (default, automatic): bands of at least two rounds of resident waves (CUs x 4 x 7 x 2 waves:
  *      14336, e.g. 1920 x 960 pixels, on MI355X) of the async band entry points and device-output
- *      frames use the FUSED frame (ABI v13) when colour-only: one launch that renders the certified
- *      pixels, runs glass regions' exact work in place at once (heavy tiles dispatched first) and
- *      queues the scattered exact pixels, which the launch's own waves render in batches as they
- *      finish their tiles; textured bands use the two-kernel deferral of mode 2; smaller bands and
- *      the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path;
- *   2: always the two-kernel deferral (ABI v9), whatever the band size: the certified pass appends
- *      the pixels to a list and a second kernel on the same stream renders them 64 to a wave;
- *   3 (ABI v13): always the fused frame for colour-only bands (tests and A/B timing).
+ *      frames use the two-kernel deferral: the certified pass appends the pixels to a list and a
+ *      second kernel on the same stream renders them in batches; smaller bands and the synchronous
+ *      whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path;
+ *   2: the two-kernel deferral whatever the band size;
+ *   3 (ABI v13): the FUSED frame for colour-only bands: one launch renders the certified pixels,
+ *      runs glass regions' exact work in place (heavy tiles dispatched first) and queues the
+ *      scattered exact pixels, which the launch's own waves render in batches as they finish their
+ *      tiles (a one-wave-per-segment drain launch follows); measured slower than mode 1 on MI355X
+ *      (DESIGN.md §6), kept for its lower single-frame latency experiments.
  * Bands over 65536 tiles, and launches on a stream being captured into a graph, use the in-lane
  * path. Images are identical in every mode. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);

@@ -298,9 +298,9 @@ class Renderer:
 
     def set_exact_pass(self, mode):
         """Exact work of certified launches (vrt_set_exact_pass): 0/False in the pixel's own lane,
-        1/True automatic (default: bands of at least two rounds of resident waves take the fused
-        frame when colour-only, the two-kernel deferral when textured), 2 always the two-kernel
-        deferral, 3 always the fused frame (colour-only). Images are identical."""
+        1/True automatic (default: bands of at least two rounds of resident waves take the
+        two-kernel deferral), 2 always the two-kernel deferral, 3 the fused frame (colour-only
+        bands). Images are identical."""
         self._check(self._lib.vrt_set_exact_pass(self._h, int(mode)), "vrt_set_exact_pass")
 
     def volume_device_ptr(self) -> int:

@@ -534,10 +534,9 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 
 OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
   const bool big = a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots;
-  // the fused frame (frame_kernel): colour-only certified bands of >= 2 rounds (exact_pass 1), or
-  // every colour-only certified band (3)
-  const bool fused = allow_defer && a.cert == 2 && !a.textured &&
-                     (ctx->exact_pass == 3 || (ctx->exact_pass == 1 && big));
+  // the fused frame (frame_kernel, exact_pass 3: every colour-only certified band). Not the
+  // automatic choice: measured slower than the two-kernel deferral (DESIGN.md §6 "Fused frame")
+  const bool fused = allow_defer && a.cert == 2 && !a.textured && ctx->exact_pass == 3;
   const bool defer = !fused && allow_defer && (ctx->exact_pass == 1 || ctx->exact_pass == 2) && a.cert == 2 &&
                      (ctx->exact_pass == 2 || big);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:

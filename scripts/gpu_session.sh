@@ -101,6 +101,15 @@ for st in "$@"; do
           echo "benchab ${ln} ${bc} $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1) $(grep -o '"kernel_ms": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1)"
         done
       done; unset VRT_LIB ;;
+    strongm)  # K-way split rehearsal of every rank over exact-pass modes: strongm:CFG,K,M1/M2
+      IFS=, read sc sk sm <<< "$arg"
+      for m in ${sm//\// }; do
+        for ((r = 0; r < sk; r++)); do
+          TAILN=0 run strongm_${sc}_k${sk}_r${r}_m$m 150 python bench.py --config $sc --rehearse-ranks $sk \
+            --rehearse-rank $r --steps 400 --warmup 100 --cpu-seconds 0 --no-verify --exact-pass $m
+          echo "strongm $sc k$sk r$r ep$m $(grep -o '"kernel_ms": [0-9.]*' $OUT/strongm_${sc}_k${sk}_r${r}_m$m.log | head -1)"
+        done
+      done ;;
     strong)  # strong-scaling rehearsal: every rank's band of the K-way split for K = 2, 4, 8
       for k in 2 4 8; do
         for ((r = 0; r < k; r++)); do

@@ -106,10 +106,10 @@ def parse():
     ap.add_argument("--parts", type=int, default=0,
                     help="interleaved row parts per frame, each on its own HIP stream (tiles.py); "
                          "0: 1 with several lanes, else 2 (one launch's tail overlaps the other's)")
-    ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1, 2, 3],
-                    help="pixels the certified walks cannot settle (vrt_set_exact_pass): 1 automatic "
-                         "(launches of >= 2 rounds of resident waves: a second, compacted exact-pass "
-                         "kernel), 2 that kernel at any size, 3 the fused frame, 0 in their own lanes")
+    ap.add_argument("--exact-pass", type=int, default=1, choices=[0, 1, 2],
+                    help="pixels the certified walks cannot settle rendered by a second, compacted "
+                         "exact pass (vrt_set_exact_pass): 1 automatic (launches of >= 2 rounds of "
+                         "resident waves), 2 always, 0 never (in their own lanes)")
     ap.add_argument("--tile-order", type=int, default=1, choices=[0, 1],
                     help="heavy-first tile order of in-lane launches with glass (vrt_set_tile_order)")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],

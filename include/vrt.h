@@ -215,23 +215,19 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
  * (ABI v9: the old stream is never touched; its owner may have destroyed it). */
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 
-/* ABI v9: deferred exact pass for stats-free launches with certified pixels (vrt_certified() == 1).
- * The certified walks settle most pixels; the others (glass hits, near-edge walks, textured hits
- * near a texel edge) need the exact path. Modes:
- *   0: the exact path runs in the pixel's own lane (heavy-first tile order, vrt_set_tile_order);
- *   1 (default, automatic): bands of at least two rounds of resident waves (CUs x 4 x 7 x 2 waves:
- *      14336, e.g. 1920 x 960 pixels, on MI355X) of the async band entry points and device-output
- *      frames use the two-kernel deferral: the certified pass appends the pixels to a list and a
- *      second kernel on the same stream renders them in batches; smaller bands and the synchronous
- *      whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path;
- *   2: the two-kernel deferral whatever the band size;
- *   3 (ABI v13): the FUSED frame for colour-only bands: one launch renders the certified pixels,
- *      runs glass regions' exact work in place (heavy tiles dispatched first) and queues the
- *      scattered exact pixels, which the launch's own waves render in batches as they finish their
- *      tiles (a one-wave-per-segment drain launch follows); measured slower than mode 1 on MI355X
- *      (DESIGN.md §6), kept for its lower single-frame latency experiments.
- * Bands over 65536 tiles, and launches on a stream being captured into a graph, use the in-lane
- * path. Images are identical in every mode. */
+/* ABI v9: deferred exact pass for stats-free launches with certified pixels (vrt_certified() == 1):
+ * on = 1 (default, automatic) or 2 (always, whatever the band size: tests and A/B timing): the
+ * certified pass renders the pixels its certified walks settle and appends the others (glass hits,
+ * near-edge walks, textured hits near a texel edge) to a list, in 8 segments by column block of the
+ * band (ABI v13; spatially coherent batches); a second kernel on the same stream renders them with
+ * the exact path: a wave's own >= 32 pixels as one chunk, the rest 32 to a wave (16 in short bands).
+ * It pays when other work overlaps the exact pass and the launch is large: the async band entry
+ * points and the device-output frames (frames in flight) use it for bands of at least two rounds of
+ * resident waves (CUs x 4 x 7 x 2 waves: 14336, e.g. 1920 x 960 pixels, on MI355X); smaller bands
+ * and the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path. off =
+ * 0: the exact path runs in the pixel's own lane, with the heavy-first tile order
+ * (vrt_set_tile_order). Bands over 65536 tiles, and launches on a stream being captured into a
+ * graph, use the in-lane path. Images are identical either way. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3

@@ -78,9 +78,6 @@ for st in "$@"; do
           echo "drvx $xc [${xfl[$j]}] $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_events_ms": \[[^]]*\]' $OUT/drvx_${xc}_${j}_$i.log | head -1)"
         done
       done ;;
-    fstamps)  # fused-frame wave timeline (build/diag/libvrt_stamps.so): fstamps:CFG[,K[,RANK[,MODE]]]
-      IFS=, read fc fk fr fm <<< "$arg"
-      VRT_LIB=$ROOT/build/diag/libvrt_stamps.so run fstamps_${fc}_k${fk:-1}_r${fr:-0}_m${fm:-3} 120 python -u scripts/frame_stamps.py --config $fc --ranks ${fk:-1} --rank ${fr:-0} --mode ${fm:-3} ;;
     drvab)  # the driver's 20-frame command, ROUNDS alternating rounds over base + build/variants/*.so
       IFS=, read dc dr <<< "$arg"
       for ((i = 1; i <= ${dr:-4}; i++)); do

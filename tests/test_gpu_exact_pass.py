@@ -8,9 +8,7 @@ checked frame by frame in test_gpu_bench_path.py). Images must be bit-identical
 to the in-lane fallback and to the exact STATS instance, frame after frame, on scenes where many
 pixels defer (glass cube: most pixels; random sparse volumes with every byte; near-edge cameras)
 and with the temporal filter reading its history (alpha 0.5), including bands (row steps),
-pitched output and band heights that leave partial tiles. The fused frame (mode 3, ABI v13: one
-launch; dense exact work in place, the rest claimed from a queue by the launch's own waves) must
-match the same references."""
+pitched output and band heights that leave partial tiles."""
 import numpy as np
 import pytest
 import torch
@@ -62,12 +60,10 @@ def test_exact_pass_is_bit_identical(built, case):
         cam = vrt.make_camera(w, h)
         a = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 2, **kw)   # deferred, any size
         b = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 0, **kw)
-        f = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 3, **kw)   # fused frame, any size
         ref = frames(r, cam, 3, R, T, 0.5, row0, rows, step, w, 2, counters=True, **kw)
     for k in range(3):
         assert np.array_equal(a[k], ref[k]), f"exact pass, frame {k}"
         assert np.array_equal(b[k], ref[k]), f"in-lane, frame {k}"
-        assert np.array_equal(f[k], ref[k]), f"fused frame, frame {k}"
 
 
 def test_exact_pass_lattice_cameras(built):
@@ -80,16 +76,13 @@ def test_exact_pass_lattice_cameras(built):
                          ((-2.5, 0.5, 1.5), (-35.26439, 45.0, 0.0))]:
             cam = vrt.make_camera(w, h, pos=pos, rot=rot)
             a = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, 2)
-            f = frames(r, cam, 2, 4, 4, 1.0, 0, h, 1, w, 3)
             ref = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, 2, counters=True)
             assert np.array_equal(a[0], ref[0]), pos
-            assert np.array_equal(f[0], ref[0]) and np.array_equal(f[1], ref[0]), pos
 
 
 def test_exact_pass_toggled_between_frames(built):
     """The exact pass switched on and off between frames on one stream: the deferred-pixel list's
-    and the fused frame's queue counter sets are reset whenever the slot's previous launch was not
-    one of their kind."""
+    counter sets are reset whenever the slot's previous launch was not a deferred one."""
     n, w, h = 128, 320, 180
     with vrt.Renderer(0) as r:
         r.upload_volume(vrt.build_scene("refraction", n), n)
@@ -98,7 +91,7 @@ def test_exact_pass_toggled_between_frames(built):
         ref = torch.zeros_like(hist)
         cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
         s = torch.cuda.current_stream().cuda_stream
-        for t, on in enumerate([2, 0, 2, 2, 0, 0, 2, 1, 2, 3, 3, 2, 3, 0, 3, 3, 3, 1]):
+        for t, on in enumerate([2, 0, 2, 2, 0, 0, 2, 1, 2]):
             p = vrt.default_params(4, 4, time=float(t + 1), ray_noise=0.01 * (t % 2))
             r.set_exact_pass(on)
             r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, hist.data_ptr(), hist.data_ptr(), stream=s)

@@ -297,10 +297,8 @@ class Renderer:
         self._check(self._lib.vrt_set_tile_order(self._h, 1 if on else 0), "vrt_set_tile_order")
 
     def set_exact_pass(self, mode):
-        """Exact work of certified launches (vrt_set_exact_pass): 0/False in the pixel's own lane,
-        1/True automatic (default: bands of at least two rounds of resident waves take the
-        two-kernel deferral), 2 always the two-kernel deferral, 3 the fused frame (colour-only
-        bands). Images are identical."""
+        """Deferred exact pass for certified launches: 0/False off, 1/True automatic (default:
+        bands of at least two rounds of resident waves), 2 always. Images are identical."""
         self._check(self._lib.vrt_set_exact_pass(self._h, int(mode)), "vrt_set_exact_pass")
 
     def volume_device_ptr(self) -> int:

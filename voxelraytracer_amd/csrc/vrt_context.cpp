@@ -47,14 +47,9 @@ constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 
 // ceil(tiles / 8) tiles' pixels each. Allocated per tile-order slot at its first deferred launch,
 // sized for that band (a 1080p band: 8.3 MB; until r03 every slot was sized for 65 536 tiles up
 // front, 537 MB per device).
-// tiles of the largest segment: workgroup % 8 classes, or (VRT_DEFER_SEG 1 builds) column blocks
+// tiles of the largest segment: a column block of the band (tile columns tx * 8 / tiles_x)
 uint32_t defer_seg_tiles(uint32_t tiles, uint32_t tiles_x) {
-#if defined(VRT_DEFER_SEG) && VRT_DEFER_SEG == 1
   return (tiles_x + vrt::kOrdClasses - 1u) / vrt::kOrdClasses * (tiles / tiles_x);
-#else
-  (void)tiles_x;
-  return (tiles + vrt::kOrdClasses - 1u) / vrt::kOrdClasses;
-#endif
 }
 size_t defer_words(uint32_t tiles, uint32_t tiles_x) {
   return vrt::kDeferHdr + size_t(vrt::kOrdClasses) * defer_seg_tiles(tiles, tiles_x) * vrt::kWgThreads;
@@ -89,14 +84,6 @@ struct OrderSlot {
   // evicting the slot waits for it instead of the whole device
   hipEvent_t ev_last = nullptr;
   bool ev_last_valid = false;
-  // the fused frame's queue (KArgs::queue; lazily allocated, entries zeroed once), its entry
-  // capacity, the last entry tag used, launches since its counters were zeroed, and whether the
-  // slot's last launch was a fused one
-  uint32_t* queue = nullptr;
-  uint32_t queue_cap = 0;
-  uint32_t q_epoch = 0;
-  uint64_t q_launches = 0;
-  bool last_queue = false;
 };
 
 struct Shard {
@@ -153,7 +140,7 @@ struct vrt_ctx {
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
   bool tile_order = true;               // vrt_set_tile_order
-  int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 two-kernel, 3 fused
+  int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 always
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
   // timestamps (2 per launch, created up front), and how many are in use since the last read
   std::vector<hipEvent_t> lt_ev;
@@ -304,7 +291,6 @@ void shard_free(Shard& s) {
                              (void*)s.d_atlas, (void*)s.d_order_pool};
   for (OrderSlot& o : s.order) {
     bufs.push_back(o.defer);
-    bufs.push_back(o.queue);
     if (o.h_batches) (void)hipHostFree(o.h_batches);
     if (o.ev_last) (void)hipEventDestroy(o.ev_last);
   }
@@ -459,8 +445,6 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_fat = 0;
   a.exact_grid = 0;
   a.batches_out = nullptr;
-  a.queue = nullptr;
-  a.q_set = a.q_epoch = a.q_cap_b = 0;
   return a;
 }
 
@@ -505,7 +489,6 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
     slot->stream = st;
     slot->epoch = 0;
     slot->last_defer = false;
-    slot->last_queue = false;
     slot->used = true;
   }
   slot->tick = ++s.order_tick;
@@ -533,22 +516,16 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 }
 
 OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
-  const bool big = a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots;
-  // the fused frame (frame_kernel, exact_pass 3: every colour-only certified band). Not the
-  // automatic choice: measured slower than the two-kernel deferral (DESIGN.md §6 "Fused frame")
-  const bool fused = allow_defer && a.cert == 2 && !a.textured && ctx->exact_pass == 3;
-  const bool defer = !fused && allow_defer && (ctx->exact_pass == 1 || ctx->exact_pass == 2) && a.cert == 2 &&
-                     (ctx->exact_pass == 2 || big);
+  const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 &&
+                     (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
-  // every tile is heavy, keep dispatch order: C1 +3.4 %); the fused frame always keeps the order's
-  // bookkeeping (its first pass is empty with the tile order off)
-  const bool order = fused || (!defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass);
+  // every tile is heavy, keep dispatch order: C1 +3.4 %)
+  const bool order = !defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass;
   if (!defer && !order) return nullptr;
   OrderSlot* slot = acquire_slot(s, a, st);
   if (!slot) return nullptr;
-  if (defer) {
-    slot->last_queue = false;  // both counter sets zeroed whenever the slot's previous launch was not one
+  if (defer) {  // both counter sets zeroed whenever the slot's previous launch was not one
     const size_t need = defer_words(a.tiles, a.tiles_x);
     if (slot->defer_cap < need) {  // first deferred launch of this band on the slot (or a larger band)
       // earlier launches with the slot run on st (its stream) and may still read the old list
@@ -600,70 +577,13 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     return slot;
   }
   slot->last_defer = false;
-#if defined(VRT_FQ_DIAG) && VRT_FQ_DIAG >= 4  // diagnostic builds: no heavy-first pass
-  const uint32_t ord_q = fused
-                             ? 0u
-                             : vrt::ord_q_for(a.tiles);
-#else
-  const uint32_t ord_q = fused && !ctx->tile_order
-                             ? 0u
-                             : vrt::ord_q_for(a.tiles);
-#endif
-  bool heavy_pass = true;
-  if (fused) {
-    // queue capacity: a wave queues at most kDeferDense - 1 pixels (more render in place); every
-    // segment holds the pixels of at most one column block's tiles
-    const uint32_t cap_b = vrt::q_block_tiles(a.tiles_x, a.tiles) * uint32_t(vrt::kWgWaves) * (vrt::kDeferDense - 1u);
-    const uint32_t need = 2u * vrt::kOrdClasses * cap_b;  // entries
-    const size_t words = size_t(vrt::kQueueHdr) + vrt::q_tag_words(a.tiles) + 2u * size_t(need);
-    if (slot->queue_cap < words) {
-      // earlier launches with the slot run on st (its stream) and may still read the old queue
-      if (slot->queue && (hipStreamSynchronize(st) != hipSuccess || hipFree(slot->queue) != hipSuccess)) {
-        slot->queue = nullptr;
-        slot->queue_cap = 0;
-        slot->last_queue = false;
-        return slot;
-      }
-      slot->queue = nullptr;
-      slot->queue_cap = 0;
-      if (hipMalloc(&slot->queue, words * sizeof(uint32_t)) != hipSuccess) {
-        slot->queue = nullptr;
-        slot->last_queue = false;
-        return slot;  // no queue: the in-lane path (order only) below
-      }
-      // entries and tile tags start with tag 0, which no launch uses
-      if (hipMemsetAsync(slot->queue, 0, words * sizeof(uint32_t), st) != hipSuccess) {
-        slot->last_queue = false;
-        return slot;
-      }
-      slot->queue_cap = uint32_t(words);
-      slot->last_queue = false;
-    }
-    if (!slot->last_queue) {
-      // the slot's last launch was not a fused one: zero the counters and the heavy-tile counts,
-      // and run this launch without a heavy-first pass (the tile order's ranks and lists of other
-      // launches carry no column-block counts); it records them for the next launch
-      if (hipMemsetAsync(slot->queue, 0, vrt::kQueueHdr * sizeof(uint32_t), st) != hipSuccess) return slot;
-      slot->q_launches = 0;
-      heavy_pass = false;
-    }
-    if (++slot->q_epoch == 0u) slot->q_epoch = 1u;  // (a wrap would take 2^32 frames)
-    a.queue = slot->queue;
-    a.q_set = uint32_t(slot->q_launches & 1u);
-    a.q_epoch = slot->q_epoch;
-    a.q_cap_b = cap_b;
-    slot->q_launches++;
-    slot->last_queue = true;
-  } else {
-    slot->last_queue = false;
-  }
   a.order = slot->d;
   a.ord_r = uint32_t(slot->epoch & 1u);
   a.ord_w = a.ord_r ^ 1u;
   a.ctr_r = uint32_t(slot->epoch % 3u);
   a.ctr_w = (a.ctr_r + 1u) % 3u;
   a.ctr_z = (a.ctr_r + 2u) % 3u;
-  a.ord_q = heavy_pass ? ord_q : 0u;
+  a.ord_q = vrt::ord_q_for(a.tiles);
   slot->epoch++;
   return slot;
 }
@@ -1396,7 +1316,7 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
 
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
-  if (on < 0 || on > 3) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0, 1, 2 or 3");
+  if (on < 0 || on > 2) return fail(ctx, VRT_ERR_INVALID, "exact pass must be 0, 1 or 2");
   ctx->exact_pass = on;
   ctx->err.clear();
   return VRT_OK;

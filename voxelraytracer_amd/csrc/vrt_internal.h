@@ -61,17 +61,6 @@ struct KArgs {
   // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
   uint32_t exact_grid;
   uint32_t* batches_out;
-  // fused frame (frame_kernel + drain_kernel, vrt_set_exact_pass 1 / 3 on colour-only bands): the
-  // certified pixels, dense exact chunks in place, the sparse exact pixels queued in segments and
-  // rendered in batches by the waves that complete a batch (see frame_kernel). queue: the slot's
-  // buffer (q_* helpers below): two per-launch counter sets, three rotating sets of heavy-tile counts
-  // per column block, a tag word per tile, then the entries, 8 bytes each {epoch << 32 | pixel id}:
-  // 8 heavy-pass segments (A) then 8 other segments (B) of q_cap_b entries each, one per column
-  // block of the band; q_set: this launch's counter set (the kernel zeroes the other one for the
-  // next launch on the stream); q_epoch: the tag of this launch (entries and tile tags; never 0, so
-  // nothing is cleared between launches)
-  uint32_t* queue;
-  uint32_t q_set, q_epoch, q_cap_b;
 };
 #if defined(VRT_EXACT_GRID_ADAPT) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_EXACT_GRID_ADAPT is an A/B knob of make variant builds"
@@ -113,23 +102,6 @@ __host__ __device__ inline uint32_t ord_q_for(uint32_t tiles) {
 }
 constexpr uint32_t kDeferHdr = 4 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 kinds x 2 sets
 constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave keeps its own exact-pass batch
-// fused-frame queue (KArgs::queue), per counter set one 256-byte line each: the tails (reserved
-// entries) of the 8 heavy-pass segments (A) and of the 8 other segments (B), then the 8 column
-// blocks' heavy-pass completion counters. Every counter sees ~1/16 of the appending or ~1/8 of the
-// heavy waves: same-address atomics serialise (~88 per us), and a hot line also stalls the texel
-// loads that hash to its channel (r05: one shared tail, head and flags word polled by every wave
-// made C3 frames 0.6-1 ms)
-constexpr uint32_t kQCtrs = 3 * kOrdClasses;
-// then 3 rotating sets (the tile order's ctr_r / ctr_w / ctr_z) of 8 heavy-tile counts per column
-// block, one line each, then one tag word per tile (rounded to an even count), then the entries
-constexpr uint32_t kQHSegHdr = 2 * kQCtrs * kOrdCtrStride;
-constexpr uint32_t kQueueHdr = kQHSegHdr + 3 * kOrdClasses * kOrdCtrStride;
-__host__ __device__ inline uint32_t q_tag_words(uint32_t tiles) { return (tiles + 1u) & ~1u; }
-// tiles of the largest column block (band column blocks: tile column tx * 8 / tiles_x)
-__host__ __device__ inline uint32_t q_block_tiles(uint32_t tiles_x, uint32_t tiles) {
-  return (tiles_x + kOrdClasses - 1u) / kOrdClasses * (tiles / tiles_x);
-}
-static_assert(kQCtrs <= 128, "one zeroing thread per counter of the other set");
 #if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_DEFER_GRID_DIV is an A/B knob of make variant builds"
 #endif

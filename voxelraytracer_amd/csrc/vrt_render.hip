@@ -1795,10 +1795,6 @@ __device__ unsigned long long g_stamps2[kMaxStampWaves][2];
 // exact_pass_kernel, per workgroup: {start, end, XCC_ID << 32 | HW_ID, pixels | dense << 16}
 __device__ unsigned long long g_stamps4[kMaxStampWaves][4];
 
-// frame_kernel, per wave: {start, after the certified phase, after the queue bookkeeping, end,
-// cnt | in_place << 8 | class drain << 9 | heavy pass << 10, full batches owned, 0, 0}
-__device__ unsigned long long g_stamps5[kMaxStampWaves][8];
-
 __device__ __forceinline__ uint32_t hw_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -2039,12 +2035,6 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__
 #ifndef VRT_EXACT_WAVES
 #define VRT_EXACT_WAVES VRT_MIN_WAVES
 #endif
-#if defined(VRT_DEFER_SEG) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_DEFER_SEG is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_DEFER_SEG
-#define VRT_DEFER_SEG 0
-#endif
 template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false>
 __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
@@ -2132,9 +2122,11 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
     const unsigned long long m = __ballot(deferred);
     if (m != 0ull) {
-      // segment: the XCD class of the workgroup (0), or the tile's column block of the band (1:
-      // consecutive list entries then come from nearby tiles, so a sparse batch's rays are alike)
-      const uint32_t seg = VRT_DEFER_SEG == 1 ? tx * kOrdClasses / a.tiles_x : blockIdx.x % kOrdClasses;
+      // segment: the tile's column block of the band (tile column tx * 8 / tiles_x), so that
+      // consecutive list entries come from nearby tiles and a sparse batch's rays are alike: C3
+      // sparse exact waves 57 -> 49 us median against the 8 XCD classes' every-8th-tile order
+      // (profiles/r05_s8 xstamps)
+      const uint32_t seg = tx * kOrdClasses / a.tiles_x;
       const uint32_t first = uint32_t(__builtin_ctzll(m));
       const uint32_t cnt = uint32_t(__builtin_popcountll(m));
       // a wave with many deferred pixels (a glass region) keeps them as a chunk of its own, each
@@ -2190,8 +2182,14 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
      defined(VRT_FORCE_FAT)) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_SPARSE_BATCH / VRT_EXACT_PRIO / VRT_FORCE_FAT are A/B knobs of make variant builds"
 #endif
-#ifndef VRT_SPARSE_BATCH  // pixels per sparse batch of the exact pass (<= 64)
-#define VRT_SPARSE_BATCH 64
+// pixels per sparse batch of the exact pass (<= 64): a sparse wave lasts as long as its slowest
+// walk and its steps execute the union of its lanes' sampled steps, so smaller batches shorten the
+// exact pass's span, which the frame's latency and a short run's drain wait for, at more waves: 32
+// with the column-block segments: the driver's 20-frame C3 command 0.0500 -> 0.0464 ms, latency
+// 0.123 -> 0.106 ms, 500 frames +0.8 % (C4 +-0, C2 +1 %); 16: 0.0485 / 0.103 / +2.6 %; 8: 0.0479 /
+// 0.102 / +6 % (profiles/r05_s10)
+#ifndef VRT_SPARSE_BATCH
+#define VRT_SPARSE_BATCH 32
 #endif
 #ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
 #define VRT_SPARSE_BATCH_FAT 16
@@ -2308,297 +2306,6 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     }
   }
 #endif
-}
-
-// ------------------------------------------------------------------------ fused frame --
-//
-// frame_kernel (+ drain_kernel): the frame for stats-free colour-only bands of >= 2 dispatch rounds
-// (the vrt_set_exact_pass default there). The two-launch scheme (render_kernel<DEFER>, then
-// exact_pass_kernel on the same stream) starts the exact work only after the last certified wave:
-// a frame's latency is the certified pass plus the exact pass's longest waves (C3: ~45 + ~75 us,
-// profiles/r04_exact/). Here the exact work starts while the certified work of the same frame runs:
-//  - tiles in heavy-first order (ordered_tile: the tiles that needed exact work in an earlier frame
-//    are dispatched first, as 8 classes of the heavy-first pass), so the exact work is known early;
-//  - a wave with >= kDeferDense pixels the certified walks cannot settle (a glass region: a
-//    coherent 8x8 tile of exact work) renders them in place at once;
-//  - a wave with fewer appends them to a queue segment (ballot, one reservation atomic, mbcnt
-//    ranks: the north_star's __ballot compaction of live rays): heavy-pass waves of class r to
-//    segment A_r, the others to B_(workgroup % 8). Batches are fixed index ranges [kQueueBatch k,
-//    kQueueBatch (k + 1)) of a segment, and the wave whose reservation covers a batch's last index
-//    renders that batch once its own tile is done: every full batch has exactly one owner, known
-//    from the reservation alone — no polling, no claim counter;
-//  - the partial last batch of A_r is rendered by the heavy-pass wave that completes class r (a
-//    per-class counter): early, since the heavy-first pass runs first; the partial last batches of
-//    the B segments (pixels of tiles that needed no exact work last frame: none with a still
-//    camera) by drain_kernel, a one-wave-per-segment launch after the frame on the same stream.
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the counters are device-scope atomics,
-// one 256-byte line each, each hit by ~1/16 of the appending or ~1/8 of the heavy waves (r05: a
-// single shared tail / head / flags word polled by every wave made C3 frames 0.6-1 ms: same-address
-// atomics serialise, and a hot line stalls the texel loads of its channel). An entry is ONE 8-byte
-// {epoch, pixel} granule written by one agent-scope (sc1, write-through) store and read by
-// agent-scope loads that wait for this launch's tag (bounded; entries of earlier launches carry
-// older tags, so entries are never cleared). A wave waits only for entries reserved before its own
-// reservation, which their producers store right after reserving: no deadlock at any residency.
-// Every pixel is rendered exactly once by the same exact path and epilogue as the other
-// instances, so images are identical (tests/queue_model.cpp models the protocol on the CPU).
-#if defined(VRT_QUEUE_BATCH) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_QUEUE_BATCH is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_QUEUE_BATCH  // pixels per batch of queued exact work (<= 64)
-#define VRT_QUEUE_BATCH 64
-#endif
-constexpr uint32_t kQueueBatch = VRT_QUEUE_BATCH;
-static_assert(kQueueBatch >= 1 && kQueueBatch <= 64, "a batch is at most one pixel per lane");
-#if defined(VRT_FQ_DIAG) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_FQ_DIAG is a diagnostic knob of make variant builds"
-#endif
-// diagnostic: 1 no exact work (wrong images), 2 every exact pixel in place, 3 as 2 without the
-// counters, 4 as 1 without the tile-order bookkeeping, 5 as 4 without the exact path in the code
-#ifndef VRT_FQ_DIAG
-#define VRT_FQ_DIAG 0
-#endif
-static_assert(kDeferDense - 1u <= 64u, "an append crosses at most a few batch ends");
-constexpr uint32_t kQTailA = 0, kQTailB = kOrdClasses, kQHSeg = 2 * kOrdClasses;
-constexpr uint32_t kQueueSpinMax = 1u << 22;  // bound of an entry wait (a bug, never a normal case)
-
-__device__ __forceinline__ uint32_t* qctr(const KArgs& a, uint32_t set, uint32_t c) {
-  return a.queue + (set * kQCtrs + c) * kOrdCtrStride;
-}
-// heavy-pass tiles of column block s, in the tile order's rotating counter set `set`
-__device__ __forceinline__ uint32_t* q_hseg(const KArgs& a, uint32_t set, uint32_t s) {
-  return a.queue + kQHSegHdr + (set * kOrdClasses + s) * kOrdCtrStride;
-}
-// tile t's tag: the epoch of the last launch that recorded it as heavy
-__device__ __forceinline__ uint32_t* q_tag(const KArgs& a, uint32_t t) { return a.queue + kQueueHdr + t; }
-__device__ __forceinline__ uint32_t q_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t q_add(uint32_t* p, uint32_t v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// waits for the wave's outstanding vector-memory operations (an atomic's return included), so
-// that a later atomic or load is performed after an earlier one
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// first entry of segment seg (0-7: A, 8-15: B; segment s % 8 = column block s % 8 of the band)
-__device__ __forceinline__ unsigned long long* q_seg(const KArgs& a, uint32_t seg) {
-  return reinterpret_cast<unsigned long long*>(a.queue + kQueueHdr + q_tag_words(a.tiles)) + size_t(seg) * a.q_cap_b;
-}
-// the band's column block of tile column tx: consecutive queue entries come from nearby tiles, so
-// a batch's rays are alike (sparse exact waves 57 -> 49 us median at C3 against the 8 XCD classes'
-// every-8th-tile order, profiles/r05_s8)
-__device__ __forceinline__ uint32_t col_block(const KArgs& a, uint32_t tx) { return tx * kOrdClasses / a.tiles_x; }
-
-// The exact path for one pixel id (band row << 16 | x) and its epilogue
-__device__ __forceinline__ void exact_id(const KArgs& a, const uint16_t* __restrict__ vox, float4* __restrict__ out,
-                                         float4* ax, uint32_t e) {
-  Ctx c;
-  init_ctx(c, a, vox);
-  c.ax = ax;
-  const int px = int(e & 0xFFFFu), li = int(e >> 16);
-  if (px < a.width && li < a.rows) {  // (always: ids come from this launch's pixels)
-    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
-    Counters k;
-#pragma unroll
-    for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
-    uint32_t steps = 0, flags = 0;
-    int32_t hit_vidx = -1;
-    float hit_len = 0.0f;
-    f3 color = mk(0.0f, 0.0f, 0.0f);
-    (void)exact_pixel<false, false, true, true>(a, c, ray, color, k, steps, flags, hit_vidx, hit_len);
-    store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
-  }
-}
-
-// entry i of segment seg, waiting for this launch's tag (~0u: never written, a bug)
-__device__ __forceinline__ uint32_t q_entry(const KArgs& a, uint32_t seg, uint32_t i) {
-  const unsigned long long* ent = q_seg(a, seg) + i;
-  for (uint32_t spins = 0;; ++spins) {  // the producer stores it right after its reservation
-    const unsigned long long v = __hip_atomic_load(ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (uint32_t(v >> 32) == a.q_epoch) return uint32_t(v);
-    if (spins >= kQueueSpinMax) return ~0u;  // never reached by a correct launch
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// The fused frame's tile order (the heavy-first scheme of ordered_tile with its lists, ranks and
-// counter rotation, but bookkept only by the waves that had exact work: a per-wave returning atomic
-// at the end of every wave cost C3 ~25 % per frame, profiles/r05_s8 fq1 vs fq4). Workgroup L < 8 ord_q
-// renders entry n - 1 - L / 8 of class L % 8's list (n = its length, at most ord_q); L = 8 ord_q + t
-// renders tile t unless its rank is in [1, ord_q], and clears the rank it read (that rank set is the
-// one the next launch writes, which records only heavy tiles). With ord_q == 0 (the first fused
-// launch of a slot, or the tile order off) every tile is in the second pass, and the rendering
-// workgroup also clears the rank this launch writes (it may hold another kind of launch's ranks).
-__device__ __forceinline__ uint32_t fq_tile(const KArgs& a, uint32_t L, bool& heavy) {
-  const uint32_t cap = kOrdClasses * a.ord_q;
-  heavy = L < cap;
-  if (L < cap) {
-    const uint32_t r = L % kOrdClasses, j = L / kOrdClasses;
-    const uint32_t n = min(*ord_ctr(a, a.ctr_r, r), a.ord_q);
-    return j < n ? ord_list(a, a.ord_r)[(n - 1u - j) * kOrdClasses + r] : ~0u;
-  }
-  const uint32_t t = L - cap;
-  uint32_t* rank = ord_rank(a, a.ord_r) + t;
-  const uint32_t rk = *rank;
-  __syncthreads();  // both waves read it before it is cleared
-  if (threadIdx.x == 0) {
-    *rank = 0u;
-    if (a.ord_q == 0u) ord_rank(a, a.ord_w)[t] = 0u;
-  }
-  return rk - 1u < a.ord_q ? ~0u : t;  // rank 0 wraps to ~0u: not in the first pass
-}
-
-// A wave that had exact work files its tile for the next launch's heavy-first pass: the first such
-// wave of the tile (the tile's tag is this launch's epoch after it) appends the tile to its class's
-// list, sets its rank, and counts it in its column block when it will be in the next first pass.
-__device__ __forceinline__ void fq_record(const KArgs& a, uint32_t tile, uint32_t tx) {
-  if (__hip_atomic_exchange(q_tag(a, tile), a.q_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.q_epoch)
-    return;
-  const uint32_t r = tile % kOrdClasses;
-  const uint32_t k = q_add(ord_ctr(a, a.ctr_w, r), 1u);  // <= tiles / 8: one per tile of class r
-  ord_list(a, a.ord_w)[k * kOrdClasses + r] = tile;
-  ord_rank(a, a.ord_w)[tile] = k + 1u;
-  if (k < ord_q_for(a.tiles)) q_add(q_hseg(a, a.ctr_w, col_block(a, tx)), 1u);
-}
-
-__global__ void __launch_bounds__(kWgThreads, VRT_MIN_WAVES) frame_kernel(KArgs a, const uint16_t* __restrict__ vox,
-                                                                           float4* __restrict__ out) {
-  if (blockIdx.x == 0) {
-    // for later launches on the stream: the other counter set (the next launch), and the
-    // rotating sets the launch after the next appends to
-    if (threadIdx.x < kQCtrs) *qctr(a, a.q_set ^ 1u, threadIdx.x) = 0u;
-    if (threadIdx.x < kOrdClasses) {
-      *q_hseg(a, a.ctr_z, threadIdx.x) = 0u;
-      *ord_ctr(a, a.ctr_z, threadIdx.x) = 0u;
-    }
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
-#ifdef VRT_STAMPS
-  const uint32_t sw = blockIdx.x * kWgWaves + uint32_t(wave);
-  unsigned long long st5[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
-#endif
-  bool heavy;
-  uint32_t tile = fq_tile(a, blockIdx.x, heavy);
-  if (tile == ~0u) {
-#ifdef VRT_STAMPS
-    if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
-      for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = 0;
-#endif
-    return;  // whole workgroup: its tile is rendered by another slot
-  }
-  tile = __builtin_amdgcn_readfirstlane(tile);
-  const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  const uint32_t cb = col_block(a, tx);
-  const uint32_t seg = heavy ? cb : kOrdClasses + cb;
-  __shared__ float4 ax_tab[kWgThreads * 3];
-  float4* const ax = &ax_tab[threadIdx.x * kAxLane];
-  bool deferred = false;
-  {
-    const int px = pixel_x(tx, wave, lane_id());
-    const int li = pixel_row(ty, wave, lane_id());
-    if (px < a.width && li < a.rows) {
-      Ctx c;
-      init_ctx(c, a, vox);
-      c.ax = ax;
-      const Ray ray = primary_ray(a, c, px, frame_row(a, li));
-      f3 color = mk(0.0f, 0.0f, 0.0f);
-      deferred = !cert_pixel<false>(c, ray, color);
-      const uint32_t l2 = lane_id();
-      if (!deferred)
-        store_pixel(a, out, size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2)), color);
-    }
-  }
-  const unsigned long long m = __ballot(deferred);
-  const uint32_t cnt = uint32_t(__builtin_popcountll(m));
-  const bool in_place = (VRT_FQ_DIAG == 1 || VRT_FQ_DIAG >= 4) ? false : (VRT_FQ_DIAG >= 2 ? cnt != 0u : cnt >= kDeferDense);
-  const uint32_t l3 = lane_id();
-  const uint32_t my_id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
-#ifdef VRT_STAMPS
-  st5[1] = __builtin_amdgcn_s_memrealtime();
-#endif
-  // batches this wave owns: [kb0, kb1) of its segment (the batches whose last index it reserved)
-  uint32_t kb0 = 0, kb1 = 0;
-  if (VRT_FQ_DIAG == 0 && cnt != 0u && !in_place) {  // append: one reservation, mbcnt ranks, one granule per pixel
-    const uint32_t first = uint32_t(__builtin_ctzll(m));
-    uint32_t base = 0;
-    if (l3 == first) base = q_add(qctr(a, a.q_set, heavy ? kQTailA + cb : kQTailB + cb), cnt);
-    base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
-    if (deferred) {
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-      const uint32_t i = base + rank;
-      if (i < a.q_cap_b)
-        __hip_atomic_store(q_seg(a, seg) + i, (static_cast<unsigned long long>(a.q_epoch) << 32) | my_id,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // batch k ends at index kQueueBatch (k + 1) - 1; this reservation covers [base, base + cnt)
-    kb0 = base / kQueueBatch;
-    kb1 = (base + cnt) / kQueueBatch;
-  }
-  // the heavy-pass wave that completes its column block drains that A segment's partial last batch
-  uint32_t drain_lo = 0, drain_hi = 0;
-  if (l3 == 0) {
-    if (cnt != 0u && VRT_FQ_DIAG < 4) fq_record(a, tile, tx);  // heavy tile for the next launch's order
-    if (heavy && VRT_FQ_DIAG != 3) {
-      const uint32_t nseg = *q_hseg(a, a.ctr_r, cb);  // heavy-pass tiles of this column block
-      vm_drain();  // this wave's reservation is performed before it counts as done
-      if (q_add(qctr(a, a.q_set, kQHSeg + cb), 1u) + 1u == nseg * uint32_t(kWgWaves)) {
-        vm_drain();
-        const uint32_t t = q_load(qctr(a, a.q_set, kQTailA + cb));  // final: every such wave has reserved
-        drain_lo = t / kQueueBatch * kQueueBatch;
-        drain_hi = t;
-      }
-    }
-  }
-  drain_lo = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_lo)));
-  drain_hi = uint32_t(__builtin_amdgcn_readfirstlane(int(drain_hi)));
-#ifdef VRT_STAMPS
-  st5[2] = __builtin_amdgcn_s_memrealtime();
-  st5[4] = cnt | (in_place ? 0x100u : 0u) | (drain_hi > drain_lo ? 0x200u : 0u) | (heavy ? 0x400u : 0u);
-  st5[5] = kb1 - kb0;
-#endif
-  // the exact phase: own pixels in place (item 0), owned full batches (1..nb), the block drain
-  // (nb + 1); one call site of the exact path
-  const uint32_t nb = kb1 - kb0;
-  const bool drain = drain_hi > drain_lo;
-  const uint32_t n_items = 1u + nb + (drain ? 1u : 0u);
-  if (in_place || nb != 0u || drain) {
-    if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);  // few long waves first
-  }
-  for (uint32_t it = in_place ? 0u : 1u; it < n_items; ++it) {
-    bool act;
-    uint32_t e = my_id;
-    if (it == 0u) {
-      act = deferred;
-    } else if (it <= nb) {
-      const uint32_t i = (kb0 + it - 1u) * kQueueBatch + l3;
-      act = l3 < kQueueBatch && i < a.q_cap_b;
-      if (act) e = q_entry(a, seg, i);
-    } else {
-      const uint32_t i = drain_lo + l3;
-      act = i < drain_hi && i < a.q_cap_b;
-      if (act) e = q_entry(a, cb, i);
-    }
-    if (VRT_FQ_DIAG < 5 && act && e != ~0u) exact_id(a, vox, out, ax, e);
-  }
-#ifdef VRT_STAMPS
-  st5[3] = __builtin_amdgcn_s_memrealtime();
-  if (lane_id() == 0 && sw < uint32_t(kMaxStampWaves))
-    for (int q = 0; q < 8; ++q) g_stamps5[sw][q] = st5[q];
-#endif
-}
-
-// The partial last batches of the fused frame's B segments (pixels of tiles outside the
-// heavy-first pass), after frame_kernel on the same stream: one wave per segment; it exits at once
-// when the segment's entries all fell into full batches (none: a still camera).
-__global__ void __launch_bounds__(64) drain_kernel(KArgs a, const uint16_t* __restrict__ vox, float4* __restrict__ out) {
-  const uint32_t s = blockIdx.x;  // B segment (column block s)
-  const uint32_t t = q_load(qctr(a, a.q_set, kQTailB + s));
-  const uint32_t lo = t / kQueueBatch * kQueueBatch;
-  const uint32_t i = lo + threadIdx.x;
-  if (t == lo || i >= t || i >= a.q_cap_b) return;
-  if constexpr (VRT_EXACT_PRIO > 0) __builtin_amdgcn_s_setprio(VRT_EXACT_PRIO);
-  __shared__ float4 ax_tab[64 * 3];
-  const uint32_t e = q_entry(a, kOrdClasses + s, i);
-  if (e != ~0u) exact_id(a, vox, out, &ax_tab[threadIdx.x * kAxLane], e);
 }
 
 // Glass and non-empty voxel counts of the canonical volume (vrt_set_certified's automatic mode):
@@ -2862,17 +2569,6 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   // ~5 %), exact walks only (0)
   // textured frames: the hit colour needs the exact hit point, so every pixel takes the exact
   // walk; its shadow rays are certified walks where they settle (CERT 1, texture-independent)
-  if (a.queue && a.order && !stats && a.cert == 2 && !a.textured) {  // the fused frame
-    if (ev_begin)
-      hipExtLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out);
-    else
-      hipLaunchKernelGGL(frame_kernel, grid, dim3(kWgThreads), 0, s, a, vox, out);
-    if (ev_end)
-      hipExtLaunchKernelGGL(drain_kernel, dim3(kOrdClasses), dim3(64), 0, s, nullptr, ev_end, 0, a, vox, out);
-    else
-      hipLaunchKernelGGL(drain_kernel, dim3(kOrdClasses), dim3(64), 0, s, a, vox, out);
-    return;
-  }
   if (a.defer && !stats && a.cert == 2) {
     // certified pass, then the exact pass over the pixels it deferred (no tile order: the
     // certified pass has no long waves)
@@ -3017,11 +2713,6 @@ int vrt_debug_stamps2(uint64_t* out, uint64_t count) {
 int vrt_debug_stamps4(uint64_t* out, uint64_t count) {
   if (!out || count > 4ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps4), count * 8) == hipSuccess ? VRT_OK
-                                                                                     : VRT_ERR_DEVICE;
-}
-int vrt_debug_stamps5(uint64_t* out, uint64_t count) {
-  if (!out || count > 8ull * vrt::kMaxStampWaves) return VRT_ERR_INVALID;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_stamps5), count * 8) == hipSuccess ? VRT_OK
                                                                                      : VRT_ERR_DEVICE;
 }
 int vrt_debug_stamps3(uint64_t* out, uint64_t count) {

@@ -107,6 +107,16 @@ for st in "$@"; do
           echo "strongm $sc k$sk r$r ep$m $(grep -o '"kernel_ms": [0-9.]*' $OUT/strongm_${sc}_k${sk}_r${r}_m$m.log | head -1)"
         done
       done ;;
+    rep)  # one rank's band of a K-way split in N separate processes per flag set: rep:CFG,K,R,N,"FLAGS1|FLAGS2"
+      IFS=, read rc rk rr rn rf <<< "$arg"
+      IFS='|' read -ra rfl <<< "$rf"
+      for ((i = 1; i <= ${rn:-3}; i++)); do
+        for j in "${!rfl[@]}"; do
+          TAILN=0 run rep_${rc}_k${rk}_r${rr}_${j}_$i 150 python bench.py --config $rc --rehearse-ranks $rk --rehearse-rank $rr \
+            --steps 400 --warmup 100 --cpu-seconds 0 --no-verify ${rfl[$j]}
+          echo "rep $rc k$rk r$rr [${rfl[$j]}] $i $(grep -o '"kernel_ms": [0-9.]*' $OUT/rep_${rc}_k${rk}_r${rr}_${j}_$i.log | head -1) $(grep -o '"launches_in_flight": [0-9.]*' $OUT/rep_${rc}_k${rk}_r${rr}_${j}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/rep_${rc}_k${rk}_r${rr}_${j}_$i.log | head -1)"
+        done
+      done ;;
     strong)  # strong-scaling rehearsal: every rank's band of the K-way split for K = 2, 4, 8
       for k in 2 4 8; do
         for ((r = 0; r < k; r++)); do

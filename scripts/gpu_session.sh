@@ -3,7 +3,7 @@
 # first step that ends in a fault, abort or timeout):
 #   bash scripts/gpu_session.sh TAG step [step ...]
 # steps: tests | smoke | pyt:FILES(,) | modes:CFG,STEPS,ROUNDS,M1/M2 | bench[:CFG] | drv[:CFG] (the driver's 20-after-5 command) | ab[:CFGS] | benchvar[:CFGS] | write[:CFG] | fetch[:CFG] |
-#        sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT[,RANK]]] | trace[:CFG] | strong[:CFG] | drvab[:CFG[,ROUNDS]] | py:<script args...> (quoted)
+#        bandsx:CFG,K,"F1|F2" | sq[:CFG] | waits[:CFG] | xstamps:CFG[,K[,VARIANT[,RANK]]] | trace[:CFG] | strong[:CFG] | drvab[:CFG[,ROUNDS]] | py:<script args...> (quoted)
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -106,6 +106,20 @@ for st in "$@"; do
             --rehearse-rank $r --steps 400 --warmup 100 --cpu-seconds 0 --no-verify --exact-pass $m
           echo "strongm $sc k$sk r$r ep$m $(grep -o '"kernel_ms": [0-9.]*' $OUT/strongm_${sc}_k${sk}_r${r}_m$m.log | head -1)"
         done
+      done ;;
+    bandsx)  # every rank's band of a K-way split per flag set, slowest last: bandsx:CFG,K,"FLAGS1|FLAGS2"
+      IFS=, read bc bk bf <<< "$arg"
+      IFS='|' read -ra bfl <<< "$bf"
+      for j in "${!bfl[@]}"; do
+        worst=0
+        for ((r = 0; r < bk; r++)); do
+          TAILN=0 run bandsx_${bc}_k${bk}_${j}_r$r 150 python bench.py --config $bc --rehearse-ranks $bk --rehearse-rank $r \
+            --steps 400 --warmup 100 --cpu-seconds 0 --no-verify ${bfl[$j]}
+          km=$(grep -o '"kernel_ms": [0-9.]*' $OUT/bandsx_${bc}_k${bk}_${j}_r$r.log | head -1 | grep -o '[0-9.]*$')
+          echo "bandsx $bc k$bk [${bfl[$j]}] r$r kernel_ms $km $(grep -o '"launches_in_flight": [0-9.]*' $OUT/bandsx_${bc}_k${bk}_${j}_r$r.log | head -1)"
+          worst=$(python3 -c "print(max($worst, ${km:-0}))")
+        done
+        echo "bandsx $bc k$bk [${bfl[$j]}] slowest $worst"
       done ;;
     rep)  # one rank's band of a K-way split in N separate processes per flag set: rep:CFG,K,R,N,"FLAGS1|FLAGS2"
       IFS=, read rc rk rr rn rf <<< "$arg"

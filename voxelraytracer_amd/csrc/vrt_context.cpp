@@ -94,8 +94,6 @@ struct Shard {
   uint8_t* d_tmp = nullptr;
   uint16_t* d_vox_pad = nullptr;
   int32_t n = 0, octants = 0;
-  uint8_t* d_bricks = nullptr;  // A/B experiment (VRT_EXACT_LDS builds): brick distance table
-  int32_t brick_nb = 0, brick_sh = 0;
   bool cert_auto = true;   // automatic certified-pixel choice for the resident volume
   bool has_glass = true;   // the resident volume has glass (bounce stacks; tile order)
   unsigned long long* d_vstats = nullptr;  // glass and non-empty voxel counts
@@ -288,7 +286,7 @@ PartRows part_rows(int32_t height, int32_t k, int32_t parts, int32_t j, int32_t 
 
 void shard_free(Shard& s) {
   (void)hipSetDevice(s.device);
-  std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats, (void*)s.d_bricks,
+  std::vector<void*> bufs = {(void*)s.d_vox, (void*)s.d_tmp, (void*)s.d_vox_pad, (void*)s.d_vstats,
                              (void*)s.d_cnt, (void*)s.d_cnt_rep, (void*)s.d_out, (void*)s.d_hit,
                              (void*)s.d_atlas, (void*)s.d_order_pool};
   for (OrderSlot& o : s.order) {
@@ -447,9 +445,6 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_fat = 0;
   a.exact_grid = 0;
   a.batches_out = nullptr;
-  a.bricks = s.d_bricks;
-  a.brick_sh = s.brick_sh;
-  a.brick_nb = s.brick_nb;
   return a;
 }
 
@@ -654,17 +649,6 @@ int volume_finish_all(vrt_ctx* ctx) {
     VRT_HIP(ctx, hipSetDevice(s.device));
     const uint64_t vol = uint64_t(s.n) * s.n * s.n;
     vrt::launch_volume_passes(s.d_vox, s.d_tmp, s.d_vox_pad, uint32_t(s.n), s.octants, main_stream(s));
-#if defined(VRT_EXACT_LDS) && VRT_EXACT_LDS
-    if (s.octants == 8) {  // A/B experiment: the brick distance table (d_tmp is free after the passes)
-      s.brick_nb = std::min(s.n, 32);
-      s.brick_sh = 0;
-      while ((s.brick_nb << s.brick_sh) < s.n) ++s.brick_sh;
-      if (s.d_bricks) (void)hipFree(s.d_bricks);
-      VRT_HIP(ctx, hipMalloc(&s.d_bricks, size_t(32768)));
-      VRT_HIP(ctx, hipMemsetAsync(s.d_bricks, 0, size_t(32768), main_stream(s)));
-      vrt::launch_bricks(s.d_vox, uint32_t(s.n), uint32_t(s.brick_nb), s.d_tmp, s.d_bricks, main_stream(s));
-    }
-#endif
     // certified walks cannot settle glass pixels (their secondary rays start at the exact hit
     // point) and a glass pixel pays the certified primary walk before the exact path: the
     // automatic mode turns them off when glass makes up more than 1/8 of the non-empty voxels

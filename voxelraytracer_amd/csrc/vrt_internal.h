@@ -61,9 +61,6 @@ struct KArgs {
   // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
   uint32_t exact_grid;
   uint32_t* batches_out;
-  // A/B experiment (VRT_EXACT_LDS builds): brick distance table (brick_nb^3 bytes, nullptr: none)
-  const uint8_t* bricks;
-  int32_t brick_sh, brick_nb;
 };
 #if defined(VRT_EXACT_GRID_ADAPT) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_EXACT_GRID_ADAPT is an A/B knob of make variant builds"
@@ -140,8 +137,6 @@ void launch_volume_passes(const uint8_t* vox, uint8_t* tmp, uint16_t* packed, ui
                           int octants, hipStream_t s);
 // glass and non-empty voxel counts into out[0..1] (accumulating)
 void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* out, hipStream_t s);
-// A/B experiment (VRT_EXACT_LDS builds): Chebyshev distance of nb^3 bricks (tmp: 2 nb^3 bytes)
-void launch_bricks(const uint8_t* vox, uint32_t n, uint32_t nb, uint8_t* tmp, uint8_t* out, hipStream_t s);
 void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise, hipStream_t s);
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,
                       float* out, hipStream_t s);

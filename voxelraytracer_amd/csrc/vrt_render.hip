@@ -29,13 +29,6 @@
 #error "VRT_STAMPS / VRT_CERT_DIAG are diagnostic builds: use make variant"
 #endif
 
-#if defined(VRT_EXACT_LDS) && !defined(VRT_DIAGNOSTIC_BUILD)
-#error "VRT_EXACT_LDS is an A/B knob of make variant builds"
-#endif
-#ifndef VRT_EXACT_LDS  // A/B: the exact pass's walks check an LDS brick-distance table before a texel load
-#define VRT_EXACT_LDS 0
-#endif
-
 namespace vrt {
 
 // ------------------------------------------------------------------ GLSL vector semantics --
@@ -197,20 +190,9 @@ struct Ctx {
   const uint32_t* atlas;  // textured instances only (TEX)
   uint32_t atlas_mask;   // atlas_size - 1 (power of two)
   float atlas_fs, atlas_fts;  // (float)u_AtlasSize, (float)u_AtlasTextureSize
-#if VRT_EXACT_LDS
-  // A/B experiment (VRT_EXACT_LDS builds): the exact pass's LDS copy of the brick distance table
-  // (byte address, 0: none), log2 of the brick edge, bricks per axis
-  uint32_t btab;
-  uint32_t bsh, bnb;
-#endif
 };
 
 // a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024).
-#if VRT_EXACT_LDS
-__device__ __forceinline__ uint32_t lds_u8(uint32_t addr) {
-  return *(__attribute__((address_space(3))) const uint8_t*)(size_t)addr;
-}
-#endif
 // b is wave-uniform (the padded pitch) and goes in as the instruction's one SGPR operand.
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
@@ -628,20 +610,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         const bool inb = (qx == smp.x) & (qy == smp.y) & (qz == smp.z);
         const uint32_t vi = cvt_flr(qx), vj = cvt_flr(qy), vk = cvt_flr(qz);
         const uint32_t pidx = mad24(mad24(vk, c.p, vj), c.p, vi);
-#if VRT_EXACT_LDS
-        // A/B experiment: a sample in a brick the LDS table marks empty (distance bD >= 1) is an
-        // empty in-volume voxel: no texel load; its window is the empty box of bricks around it
-        uint32_t bD = 0;
-        if (c.btab != 0u) {
-          const bool tin = inb & ((vi | vj | vk) < uint32_t(c.n));  // (plane N: the texel path)
-          const uint32_t bidx = mad24(mad24(vk >> c.bsh, c.bnb, vj >> c.bsh), c.bnb, vi >> c.bsh);
-          bD = tin ? lds_u8(c.btab + bidx) : 0u;
-        }
-        uint32_t packed = 0u;
-        if (bD == 0u) packed = load_u16_at(c.vox, pidx, obase);
-#else
         const uint32_t packed = load_u16_at(c.vox, pidx, obase);
-#endif
         const uint32_t v_raw = packed & kVoxMask;
         const uint32_t dist = packed >> kDistShift;
         const uint32_t v_ev = inb ? v_raw : kOutside;
@@ -649,21 +618,10 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
         // as v*rcp + (fd*|rcp| + boff): only has to be conservative (error <~ 4e-4 |rcp| for
         // N <= 1024, against the 1/256 * |rcp| face margin), so it may contract
         const float fd = float(dist) - kSkipMargin;
-        float lx = __builtin_fmaf(float(vi), rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
-        float ly = __builtin_fmaf(float(vj), rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
-        float lz = __builtin_fmaf(float(vk), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
-        bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
-#if VRT_EXACT_LDS
-        if (bD >= 2u) {  // brick box [(b - bD + 1) B, (b + bD) B) per axis, faces pulled in by the margin
-          const float S = float(1u << c.bsh), fdb = float(bD) * S - kSkipMargin;
-          const float bx = float((vi >> c.bsh) << c.bsh), by = float((vj >> c.bsh) << c.bsh),
-                      bz = float((vk >> c.bsh) << c.bsh);
-          lx = ((dir.x > 0.0f ? bx + fdb : (bx + S) - fdb) - pos.x) * rcp.x;
-          ly = ((dir.y > 0.0f ? by + fdb : (by + S) - fdb) - pos.y) * rcp.y;
-          lz = ((dir.z > 0.0f ? bz + fdb : (bz + S) - fdb) - pos.z) * rcp.z;
-          open = skip_ok;
-        }
-#endif
+        const float lx = __builtin_fmaf(float(vi), rcp.x, __builtin_fmaf(fd, __builtin_fabsf(rcp.x), boff.x));
+        const float ly = __builtin_fmaf(float(vj), rcp.y, __builtin_fmaf(fd, __builtin_fabsf(rcp.y), boff.y));
+        const float lz = __builtin_fmaf(float(vk), rcp.z, __builtin_fmaf(fd, __builtin_fabsf(rcp.z), boff.z));
+        const bool open = skip_ok & inb & (v_raw == 0u) & (dist >= 2u);
         s_lim = open ? __builtin_fminf(__builtin_fminf(lx, ly), __builtin_fminf(lz, s_len)) : -1.0f;
         // stop the inner loop on: outside sample, a byte that is an event, the length. Only a
         // sampled step can stop it: a skipped one reads an empty in-volume texel and has
@@ -1881,11 +1839,6 @@ __device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t*
   c.atlas_mask = uint32_t(a.atlas_size) - 1u;
   c.atlas_fs = float(a.atlas_size);
   c.atlas_fts = float(a.atlas_tex_size);
-#if VRT_EXACT_LDS
-  c.btab = 0u;
-  c.bsh = uint32_t(a.brick_sh);
-  c.bnb = uint32_t(a.brick_nb);
-#endif
 }
 
 // The primary ray of pixel (px, frame row py): vertex stage (voxel.glsl:467-472) evaluated at the
@@ -2310,15 +2263,6 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
   init_ctx(c, a, vox);
   __shared__ float4 ax_tab[64 * 3];
   c.ax = &ax_tab[lane * kAxLane];
-#if VRT_EXACT_LDS
-  __shared__ uint4 btab4[32768 / 16];
-  if (a.bricks) {
-    const uint32_t words = (uint32_t(a.brick_nb) * uint32_t(a.brick_nb) * uint32_t(a.brick_nb) + 15u) / 16u;
-    for (uint32_t i = lane; i < words; i += 64u) btab4[i] = reinterpret_cast<const uint4*>(a.bricks)[i];
-    __syncthreads();
-    c.btab = uint32_t(reinterpret_cast<size_t>((__attribute__((address_space(3))) uint4*)btab4));
-  }
-#endif
   for (uint32_t b = blockIdx.x; b < batches; b += gridDim.x) {
     // batch b: dense chunk b (in segment order), else sparse entries [64 (b - total_d), + 64)
     const bool dense = b < total_d;
@@ -2512,21 +2456,6 @@ __global__ void __launch_bounds__(64) reduce_counters_kernel(unsigned long long*
   dst[q] += s;
 }
 
-#if VRT_EXACT_LDS
-// A/B experiment: brick occupancy (nb^3 bricks of edge B = n / nb): 1 if any voxel is non-empty
-__global__ void __launch_bounds__(256) brick_occ_kernel(const uint8_t* __restrict__ vox, uint32_t n, uint32_t nb,
-                                                        uint8_t* __restrict__ occ) {
-  const uint32_t b = blockIdx.x * 256u + threadIdx.x;
-  if (b >= nb * nb * nb) return;
-  const uint32_t B = n / nb, bx = b % nb, by = (b / nb) % nb, bz = b / (nb * nb);
-  uint32_t any = 0;
-  for (uint32_t z = 0; z < B; ++z)
-    for (uint32_t y = 0; y < B; ++y)
-      for (uint32_t x = 0; x < B; ++x)
-        any |= vox[(bx * B + x) + uint64_t(n) * ((by * B + y) + uint64_t(n) * (bz * B + z))];
-  occ[b] = any ? 1u : 0u;
-}
-#endif
 
 // Chebyshev distance field, one separable pass per axis (x, then y, then z), capped at
 // kDistCap: out(v) = min(kDistCap, distance to the boundary pseudo-voxels -1 and N on this axis,
@@ -2711,16 +2640,6 @@ void launch_volume_passes(const uint8_t* vox, uint8_t* tmp, uint16_t* packed, ui
     hipLaunchKernelGGL(pack_volume_kernel, dim3(b2), dim3(256), 0, s, vox, da, packed, n);
   }
 }
-
-#if VRT_EXACT_LDS
-void launch_bricks(const uint8_t* vox, uint32_t n, uint32_t nb, uint8_t* tmp, uint8_t* out, hipStream_t s) {
-  const uint32_t cnt = nb * nb * nb;
-  hipLaunchKernelGGL(brick_occ_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, vox, n, nb, tmp);
-  hipLaunchKernelGGL(dist_pass_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, tmp, tmp + cnt, nb, 0, 1);
-  hipLaunchKernelGGL(dist_pass_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, tmp + cnt, tmp, nb, 1, 0);
-  hipLaunchKernelGGL(dist_pass_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, tmp, out, nb, 2, 0);
-}
-#endif
 
 void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* out, hipStream_t s) {
   const unsigned b = unsigned(std::min<uint64_t>((total + 255) / 256, 16384));

@@ -110,8 +110,10 @@ def parse():
                     help="pixels the certified walks cannot settle rendered by a second, compacted "
                          "exact pass (vrt_set_exact_pass): 1 automatic (launches of >= 2 rounds of "
                          "resident waves), 2 always, 0 never (in their own lanes)")
-    ap.add_argument("--tile-order", type=int, default=1, choices=[0, 1],
-                    help="heavy-first tile order of in-lane launches with glass (vrt_set_tile_order)")
+    ap.add_argument("--tile-order", type=int, default=1, choices=[0, 1, 2],
+                    help="heavy-first tile order of in-lane launches with glass (vrt_set_tile_order): "
+                         "1 automatic (launches of at least one dispatch round of waves), 2 every "
+                         "launch, 0 off")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
                     help="certified pixels (vrt_set_certified): 0 automatic, 1 always, -1 never")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -329,7 +331,7 @@ def main():
     ren = vrt.Renderer(local)
     ren.set_exact_pass(args.exact_pass)
     ren.set_certified(args.certified)
-    ren.set_tile_order(bool(args.tile_order))
+    ren.set_tile_order(args.tile_order)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
     kparams = params   # the kernel's params: textured frames use the atlas uploaded once
     if atlas is not None:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 13
+#define VRT_ABI_VERSION 14
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -202,7 +202,9 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
 
 /* ABI v7: heavy-first tile order for stats-free colour-only launches with certified pixels
  * (vrt_certified() == 1) of volumes with glass (DESIGN.md §6 "Tile order"): on = 1 (default),
- * off = 0. Each launch records which of its 16x8 tiles had a pixel on the exact path (glass
+ * off = 0. ABI v14: 1 is automatic, launches of at least one dispatch round of resident waves
+ * (CUs x 4 x 7: 7168 waves, e.g. 1920 x 240 pixels, on MI355X; smaller launches have every tile
+ * resident at once, so the order would only cost its bookkeeping), 2 = every launch. Each launch records which of its 16x8 tiles had a pixel on the exact path (glass
  * bounce stacks, near-edge walks; until ABI v8 only bounce stacks); the next launch of the same
  * band (width, rows, row0, row_step) on the same stream dispatches those tiles first, each on the
  * same XCD as before, the last to finish first, so the frame's longest waves start first.

@@ -3,7 +3,7 @@
 # utilisation, VMEM latency, LDS waits/conflicts. Usage: bash scripts/pmc_deep.sh OUTDIR CFG...
 set -e
 out=$1; shift
-cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-.}"; ROOT=$(pwd); export TMPDIR=/tmp; mkdir -p "$ROOT/$out"
 for cfg in "$@"; do
   i=0
   for grp in "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \

@@ -31,11 +31,27 @@ def free_port():
 @pytest.mark.parametrize("scaling,gather", [("weak", False), ("strong", False), ("weak", True),
                                             ("strong", True)])
 def test_bench_two_ranks_json(built, scaling, gather):
+    two_ranks(scaling, gather, ["--backend", "gloo", "--same-device"])
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()   # counts devices without initialising HIP in this process
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="RCCL needs one GPU per rank (the driver's multi-GPU node)")
+@pytest.mark.parametrize("gather", [True, False])
+def test_bench_two_ranks_rccl(built, gather):
+    """The driver's N > 1 command itself on two GPUs: nccl backend (RCCL over xGMI), the library's
+    per-lane communicators and ncclGather of RGB8 bands, rank 0's assembly checked bit for bit."""
+    two_ranks("strong", gather, [])
+
+
+def two_ranks(scaling, gather, backend_args):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
-           "--backend", "gloo", "--same-device", "--scaling", scaling, "--cpu-seconds", "0",
-           "--watchdog-s", "100"]
+           "--scaling", scaling, "--cpu-seconds", "0", "--watchdog-s", "100"] + backend_args
     cmd += [] if gather else ["--no-gather"]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     # own process group: a hung run is killed with its torchrun workers, after SIGUSR1 has made
@@ -77,6 +93,7 @@ def test_bench_two_ranks_json(built, scaling, gather):
         assert sum(out["verify"]["gathers_per_lane"]) > 0
         ro = out["gather"]["render_only"]
         assert ro["ms_per_step"] > 0 and ro["kernel_ms_max_over_ranks"] > 0
-        assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * 4
+        bpp = 3 if (out["gather"]["wire"] or "").startswith("RGB8") else 4   # RCCL: RGB8 wire
+        assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * bpp
     else:   # one gather of the last frame after the timed region
         assert out["collect"]["rows"] == rows and out["collect"]["bytes"] == rows * 1920 * 4

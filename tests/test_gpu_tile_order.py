@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 def renderer(built):
     r = vrt.Renderer(0)
     yield r
-    r.set_tile_order(True)
+    r.set_tile_order(1)
     r.close()
 
 
@@ -51,19 +51,19 @@ def test_tile_order_frames_identical(renderer, scene, n, w, h, R, T):
     cam = vrt.make_camera(w, h)
     p = vrt.default_params(R, T)
     exact, _, _ = renderer.render(cam, p)   # stats instance: exact walks, dispatch order
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
     for k, img in enumerate(frames(renderer, cam, p, h, w, 5)):
         assert same(img, exact), f"frame {k}"
     renderer.set_tile_order(False)
     assert same(frames(renderer, cam, p, h, w, 1)[0], exact)
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
 
 
 def test_tile_order_bands_streams_and_geometry(renderer):
     n = 128
     renderer.upload_volume(vrt.build_scene("refraction", n), n)
     p = vrt.default_params(4, 4)
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
     s2 = [torch.cuda.Stream(), torch.cuda.Stream()]
     for w, h in ((400, 240), (416, 240), (400, 240), (200, 120)):
         cam = vrt.make_camera(w, h)
@@ -84,7 +84,7 @@ def test_tile_order_temporal_in_place(renderer):
     cam = vrt.make_camera(w, h)
     p = vrt.default_params(4, 4)
     runs = []
-    for on in (False, True):
+    for on in (0, 2):
         renderer.set_tile_order(on)
         hist = torch.zeros((h, w), dtype=torch.int32, device="cuda")
         seq = []
@@ -100,8 +100,9 @@ def test_tile_order_temporal_in_place(renderer):
 
 
 def test_tile_order_switch(renderer):
-    assert renderer._lib.vrt_set_tile_order(renderer._h, 2) == vrt.abi.VRT_ERR_INVALID
-    renderer.set_tile_order(True)
+    assert renderer._lib.vrt_set_tile_order(renderer._h, 3) == vrt.abi.VRT_ERR_INVALID
+    assert renderer._lib.vrt_set_tile_order(renderer._h, -1) == vrt.abi.VRT_ERR_INVALID
+    renderer.set_tile_order(2)
 
 
 def test_tile_order_slot_recycling(renderer):
@@ -111,7 +112,7 @@ def test_tile_order_slot_recycling(renderer):
     n, w, h = 128, 256, 160
     renderer.upload_volume(vrt.build_scene("refraction", n), n)
     p = vrt.default_params(4, 4)
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
     cam = vrt.make_camera(w, h)
     exact, _, _ = renderer.render(cam, p)
     streams = [torch.cuda.Stream() for _ in range(3)]
@@ -129,7 +130,7 @@ def test_tile_order_graph_capture(renderer):
     n, w, h = 128, 240, 136
     renderer.upload_volume(vrt.build_scene("refraction", n), n)
     p = vrt.default_params(4, 4)
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
     cam = vrt.make_camera(w, h)
     exact, _, _ = renderer.render(cam, p)
     img = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
@@ -155,7 +156,7 @@ def test_tile_order_band_beyond_the_pool(renderer):
     n, w, h = 128, 7680, 4320
     renderer.upload_volume(vrt.build_scene("refraction", n), n)
     p = vrt.default_params(4, 4)
-    renderer.set_tile_order(True)
+    renderer.set_tile_order(2)
     cam = vrt.make_camera(w, h)
     exact, _, _ = renderer.render(cam, p, want_hits=False)
     img = frames(renderer, cam, p, h, w, 2)

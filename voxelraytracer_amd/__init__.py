@@ -292,9 +292,10 @@ class Renderer:
         """Whether the next stats-free colour-only frame uses certified walks."""
         return self._lib.vrt_certified(self._h) == 1
 
-    def set_tile_order(self, on: bool):
-        """Heavy-first tile order for stats-free launches (default on; images are identical)."""
-        self._check(self._lib.vrt_set_tile_order(self._h, 1 if on else 0), "vrt_set_tile_order")
+    def set_tile_order(self, on):
+        """Heavy-first tile order for stats-free launches: False/0 off, True/1 automatic (default:
+        launches of at least one dispatch round of waves), 2 every launch. Images are identical."""
+        self._check(self._lib.vrt_set_tile_order(self._h, int(on)), "vrt_set_tile_order")
 
     def set_exact_pass(self, mode):
         """Deferred exact pass for certified launches: 0/False off, 1/True automatic (default:

@@ -139,7 +139,7 @@ struct vrt_ctx {
   std::vector<ncclComm_t> comms;
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
-  bool tile_order = true;               // vrt_set_tile_order
+  int tile_order = 1;                   // vrt_set_tile_order: 0 off, 1 automatic, 2 always
   int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 always
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
   // timestamps (2 per launch, created up front), and how many are in use since the last read
@@ -521,7 +521,12 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
   // every tile is heavy, keep dispatch order: C1 +3.4 %)
-  const bool order = !defer && ctx->tile_order && !a.textured && a.cert == 2 && s.has_glass;
+  // Nor for launches below one dispatch round of waves (VRT_ORD_MIN_ROUNDS): all of their tiles are
+  // resident at once, so an order only costs its list reads and bookkeeping (C3's 8-way bands
+  // in flight: rank 7 0.0078 -> 0.0072, rank 6 0.0127 -> 0.0105 ms per frame, profiles/r05_s14)
+  const bool order = !defer && ctx->tile_order != 0 && !a.textured && a.cert == 2 && s.has_glass &&
+                     (ctx->tile_order == 2 ||
+                      a.tiles * uint32_t(vrt::kWgWaves) >= uint32_t(VRT_ORD_MIN_ROUNDS) * s.wave_slots);
   if (!defer && !order) return nullptr;
   OrderSlot* slot = acquire_slot(s, a, st);
   if (!slot) return nullptr;
@@ -1308,8 +1313,8 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches) {
 
 int vrt_set_tile_order(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
-  if (on != 0 && on != 1) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0 or 1");
-  ctx->tile_order = on != 0;
+  if (on < 0 || on > 2) return fail(ctx, VRT_ERR_INVALID, "tile order must be 0, 1 or 2");
+  ctx->tile_order = on;
   ctx->err.clear();
   return VRT_OK;
 }

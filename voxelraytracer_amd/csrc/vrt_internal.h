@@ -100,6 +100,12 @@ constexpr uint32_t kOrdHdr = 3 * kOrdClasses * kOrdCtrStride;  // tile-order buf
 __host__ __device__ inline uint32_t ord_q_for(uint32_t tiles) {
   return (tiles + kOrdClasses * VRT_ORD_DIV - 1u) / (kOrdClasses * VRT_ORD_DIV);
 }
+#if defined(VRT_ORD_MIN_ROUNDS) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_ORD_MIN_ROUNDS is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_ORD_MIN_ROUNDS  // dispatch rounds of waves from which an in-lane launch takes the tile order
+#define VRT_ORD_MIN_ROUNDS 1
+#endif
 constexpr uint32_t kDeferHdr = 4 * kOrdClasses * kOrdCtrStride;  // deferred-pass slot header: 2 kinds x 2 sets
 constexpr uint32_t kDeferDense = 32;        // deferred pixels from which a wave keeps its own exact-pass batch
 #if defined(VRT_DEFER_GRID_DIV) && !defined(VRT_DIAGNOSTIC_BUILD)

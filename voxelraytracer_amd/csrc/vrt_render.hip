@@ -1894,6 +1894,34 @@ struct StackRay {
 __device__ __forceinline__ StackRay pack_stack_ray(const Ray& r) {
   return StackRay{r.pos, r.dir, r.len, r.energy, uint32_t(r.rdepth) | (uint32_t(r.tdepth) << 16)};
 }
+#if defined(VRT_LDS_STACK) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_LDS_STACK is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_LDS_STACK  // the bounce stack's bottom entry in LDS (0: every entry in scratch)
+#define VRT_LDS_STACK 1
+#endif
+// The bounce stack's bottom entry of each lane in LDS, component-major (dword j of lane t at
+// [j * NL + t]: conflict-free ds_write_b32 / ds_read_b32), the rest in scratch. A pixel whose
+// tree holds at most one entry at a time (every C1 pixel: a reflection ray under the first
+// refraction ray) then never touches scratch for it.
+constexpr int kStackWords = 9;
+template <int NL>
+__device__ __forceinline__ void lds_stack_put(float* __restrict__ b, const StackRay& e) {
+  b[0 * NL] = e.pos.x;
+  b[1 * NL] = e.pos.y;
+  b[2 * NL] = e.pos.z;
+  b[3 * NL] = e.dir.x;
+  b[4 * NL] = e.dir.y;
+  b[5 * NL] = e.dir.z;
+  b[6 * NL] = e.len;
+  b[7 * NL] = e.energy;
+  b[8 * NL] = __uint_as_float(e.depths);
+}
+template <int NL>
+__device__ __forceinline__ StackRay lds_stack_get(const float* __restrict__ b) {
+  return StackRay{mk(b[0 * NL], b[1 * NL], b[2 * NL]), mk(b[3 * NL], b[4 * NL], b[5 * NL]), b[6 * NL],
+                  b[7 * NL], __float_as_uint(b[8 * NL])};
+}
 __device__ __forceinline__ Ray unpack_stack_ray(const StackRay& e) {
   Ray r;
   r.pos = e.pos;
@@ -1918,11 +1946,12 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 // they settle (cert_shadow_exact); CSEC: air-medium secondary rays by certified walks first
 // (cert_secondary; on glass-heavy frames their glass hits pay both walks, C1 +19 %: off there).
 // Returns whether the pixel ran a bounce stack.
-template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false>
+// NL: lanes per workgroup of the LDS stack bottom `lstk` (this lane's word 0; VRT_LDS_STACK).
+template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int NL = kWgThreads>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
-                                            int32_t& hit_vidx, float& hit_len) {
-  StackRay stack[kMaxStack - 1];  // the top entry lives in `ray`
+                                            int32_t& hit_vidx, float& hit_len, float* __restrict__ lstk) {
+  StackRay stack[kMaxStack - 1 - VRT_LDS_STACK];  // the top entry lives in `ray`, the bottom one in LDS
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
   const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
@@ -1962,7 +1991,12 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
         if ((pr && !push_r) || (pt && !push_t)) flags |= VRT_HIT_FLAG_STACK_FULL;
       }
       if (push_r && push_t) {
-        stack[sp++] = pack_stack_ray(reflection_ray(lc, ray, h));
+        const StackRay e = pack_stack_ray(reflection_ray(lc, ray, h));
+        if (VRT_LDS_STACK && sp == 0)
+          lds_stack_put<NL>(lstk, e);
+        else
+          stack[sp - VRT_LDS_STACK] = e;
+        ++sp;
         ray = refraction_ray<TEX>(lc, ray, h, k);
       } else if (push_r) {
         ray = reflection_ray(lc, ray, h);
@@ -1970,7 +2004,8 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
         ray = refraction_ray<TEX>(lc, ray, h, k);
       } else {
         if (sp == 0) break;
-        ray = unpack_stack_ray(stack[--sp]);
+        --sp;
+        ray = unpack_stack_ray(VRT_LDS_STACK && sp == 0 ? lds_stack_get<NL>(lstk) : stack[sp - VRT_LDS_STACK]);
       }
       k.c[VRT_CNT_SECONDARY_RAYS]++;
       if constexpr (CSH && CSEC) {
@@ -2104,8 +2139,9 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     } else if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
       heavy = true;
-      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps,
-                                                                                     flags, hit_vidx, hit_len);
+      __shared__ float lstk[VRT_LDS_STACK ? kStackWords * kWgThreads : 1];
+      (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
+                                                         hit_len, &lstk[threadIdx.x]);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2));
@@ -2288,8 +2324,9 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     int32_t hit_vidx = -1;
     float hit_len = 0.0f;
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX>(a, c, ray, color, k, steps, flags, hit_vidx,
-                                                                hit_len);
+    __shared__ float lstk[VRT_LDS_STACK ? kStackWords * 64 : 1];
+    (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, 64>(a, c, ray, color, k, steps, flags,
+                                                                    hit_vidx, hit_len, &lstk[lane]);
     store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
 #ifdef VRT_STAMPS
     xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);

@@ -126,6 +126,10 @@ def parse():
     ap.add_argument("--rehearse-rank", type=int, default=0,
                     help="with --rehearse-ranks K: time rank R's band instead of rank 0's (block-"
                          "cyclic bands differ by up to one block; the K-GPU frame is the slowest)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch of a rank's band (vrt_render_temporal_batch_async, "
+                         "alpha 1): 0 automatic, min(8, K) for a K-way split (each launch then has "
+                         "about a whole frame's waves), 1 off")
     ap.add_argument("--row-block", type=int, default=0,
                     help="rows per block of a rank's band (vrt_render_*_blocks_pitched_async, ABI "
                          "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 16 for a "
@@ -243,11 +247,24 @@ def pipeline_shape(args, world: int):
     split = max(world, args.rehearse_ranks if world == 1 else 1)
     rows = -(-frame_h // split)
     waves = -(-w // 8) * -(-rows // 8)
-    small = split > 1 and waves < WAVE_SLOTS
     independent = args.alpha == 1.0
+    batch = frame_batch(args, split)
+    small = split > 1 and waves * batch < WAVE_SLOTS
     lanes = args.lanes or ((8 if small else 4) if independent else 1)
     queues = args.queues or (8 if small and lanes == 8 else 4)
-    return lanes, queues
+    return lanes, queues, batch
+
+
+def frame_batch(args, split: int) -> int:
+    """Frames per launch of a rank's band. A band of a K-way split holds 1/K of the frame's waves:
+    below a few dispatch rounds its launches are bound by their longest waves and by the hardware
+    queues that overlap them, so K frames per launch (at most 8) give every launch
+    about a whole frame's waves again. Only for independent frames (RGBA8 output at alpha 1)."""
+    if args.batch:
+        return args.batch
+    if split <= 1 or args.alpha != 1.0 or args.output != "rgba8" or args.scaling != "strong":
+        return 1
+    return min(8, split)
 
 
 def share_ids(ids, count, dev):
@@ -278,7 +295,7 @@ def main():
     watchdog_s = args.watchdog_s if args.watchdog_s >= 0 else (300.0 if world > 1 else 0.0)
     if watchdog_s > 0:
         faulthandler.dump_traceback_later(watchdog_s, exit=True)
-    lanes, queues = pipeline_shape(args, world)
+    lanes, queues, batch = pipeline_shape(args, world)
     if args.queues or queues != 4:   # before HIP initialises (the GPU box exports 4)
         os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
     queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
@@ -364,6 +381,11 @@ def main():
             ren.render_rows_async(cam, kparams, row0, rows, step, out_ptr, 0, 0, sp, pitch=pitch,
                                   row_block=row_block)
 
+    def launch_batch(row0, rows, step, outs, pitch, sp, row_block=1):
+        # frame batches (FrameTiler batch > 1): the band of len(outs) frames in one launch
+        ren.render_temporal_batch_async([cam] * len(outs), kparams, row0, rows, step, outs, None, sp,
+                                        pitch=pitch, row_block=row_block)
+
     gather = world > 1 and not args.no_gather
     parts = args.parts or (1 if lanes > 1 or gather else 2)
     parts = parts if frame_h % (max(world, args.rehearse_ranks) * parts) == 0 else 1
@@ -392,7 +414,8 @@ def main():
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
                        gather=gather, lanes=lanes,
                        independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs,
-                       row_block=row_block, exchange=exchange)
+                       row_block=row_block, exchange=exchange, batch=batch,
+                       launch_batch=launch_batch if batch > 1 else None)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -474,10 +497,11 @@ def main():
         fev_ = []
         for i_ in range(steps):
             tiler.frame()
-            if events:
+            if events and tiler.pending == 0:
                 # one event on every stream of the frame just enqueued (its lane counts the warm-up
-                # frames too; no part streams: the current stream); its completion is the last of them
-                sts = (tiler.part_streams[(tiler.k - 1) % tiler.lanes] if tiler.part_streams
+                # frames too; no part streams: the current stream); its completion is the last of them.
+                # Frame batches: after each batch's launch (its last frame)
+                sts = (tiler.part_streams[((tiler.k - 1) // tiler.batch) % tiler.lanes] if tiler.part_streams
                        else [torch.cuda.current_stream(dev)])
                 evs = []
                 for st_ in sts:
@@ -485,6 +509,7 @@ def main():
                     e.record(st_)
                     evs.append(e)
                 fev_.append(evs)
+        tiler.flush()   # a partial frame batch is launched inside the timed region
         for e, st in zip(ev1, lane_st):
             e.record(st)
         torch.cuda.synchronize(dev)
@@ -518,7 +543,8 @@ def main():
     # frames in flight overlap, so a launch lasts longer than frame_gpu_ms / parts). Not in the
     # timed region: the per-launch events cost ~8 % of the frame rate (r02 s17).
     lt_frames = max(20, min(args.steps, 200))
-    ren.set_launch_timing(lt_frames * parts)
+    lt_frames -= lt_frames % batch   # whole batches: every launch holds `batch` frames
+    ren.set_launch_timing(lt_frames * parts // batch)
     for _ in range(lt_frames):
         tiler.frame()
     tiler.finish()
@@ -545,6 +571,7 @@ def main():
         ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ea.record(st_)
         tiler.frame()
+        tiler.flush()   # frame batches: the frame alone is a batch of one
         eb.record(st_)
         torch.cuda.synchronize(dev)
         lat.append(ea.elapsed_time(eb))
@@ -670,9 +697,9 @@ def main():
         # frames in flight, launches overlap (launches_in_flight on average), so the GPU's rate is
         # the per-launch rate times that: this rank's bytes per frame / GPU time per frame.
         own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
-        bytes_per_launch = float(np.mean(part_bytes))
+        bytes_per_launch = float(np.mean(part_bytes)) * batch   # a launch renders `batch` frames
         per_launch = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        in_flight = launch_ms * parts / frame_gpu_ms
+        in_flight = launch_ms * parts / (frame_gpu_ms * batch)
         achieved = own_bytes / (frame_gpu_ms * 1e-3) / 1e9
         lib_hash = lib_sha256()
         traffic = traffic_frame = hbm_frac = None
@@ -771,7 +798,11 @@ def main():
                                  f"({band_kind}) of a {rehearse}-way strong split is rendered and "
                                  "timed; rays counted over the whole frame"
                                  if rehearse else "single GPU, whole frame"))
-                               + (f", {lanes} frames in flight (lanes)" if lanes > 1 else "")
+                               + (f", {batch} frames per launch (frame batches: each launch renders the "
+                                  f"band of {batch} consecutive frames, vrt_render_temporal_batch_async)"
+                                  if batch > 1 else "")
+                               + (f", {lanes} {'batches' if batch > 1 else 'frames'} in flight (lanes)"
+                                  if lanes > 1 else "")
                                + f", {parts} interleaved row part{'s' if parts > 1 else ''} per "
                                f"frame on {lanes * parts} HIP stream{'s' if lanes * parts > 1 else ''}",
                 "rays_per_frame": rays_per_frame,
@@ -810,6 +841,7 @@ def main():
                                  "events, vrt_set_launch_timing) over a pass of the same frames "
                                  "after the timed region"),
                 "launches_per_frame": parts,
+                "frames_per_launch": batch,
                 "lanes": lanes,
                 "kernel_ms": round(frame_gpu_ms, 4),
                 "kernel_ms_is": (f"GPU time per frame of this rank ({lanes} frame(s) in flight, "

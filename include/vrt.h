@@ -338,6 +338,22 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
                                              vrt_hit* d_out_hit, uint64_t* d_counters,
                                              void* hip_stream);
 
+/* ABI v14: a FRAME BATCH: the same band of `nframes` (1..8) frames in ONE launch, at u_Alpha = 1
+ * (each frame's RGB8 store is its output; no history is read), frame f with its own camera
+ * cams[f] (same image size) and u_Time params[f].time, every other field of params[f] equal to
+ * params[0]'s, written to d_cur_rgba8[f] (and d_raw_rgba8[f] when d_raw_rgba8 is not NULL; pitch
+ * pixels per band row in all of them). Band geometry as vrt_render_temporal_blocks_pitched_async;
+ * bands of < 8192 rows. A band of a k-way split is 1/k of the frame's waves: below a few dispatch
+ * rounds a launch is bound by its longest waves and by the hardware queues that overlap launches,
+ * not by the GPU's throughput, and a batch of k frames gives it a whole frame's waves again (the
+ * deferred exact pass, the tile order and the grid sizing then see one large launch). Bytes equal
+ * nframes single-frame launches' (tests/test_gpu_batch.py). No hit records or counters. */
+int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams,
+                                    const vrt_params* params, int32_t row0, int32_t rows,
+                                    int32_t row_step, int32_t row_block, int64_t pitch,
+                                    uint32_t* const* d_cur_rgba8, uint32_t* const* d_raw_rgba8,
+                                    void* hip_stream);
+
 /* Synchronous frame loop of main.cpp:323-393 with the history and the ray-trace FBO kept in the
  * context: render, filter against the last filtered frame, copy the new filtered frame to the
  * HOST buffer out_rgba8 (W*H*4 bytes). The history starts black and restarts black when the image

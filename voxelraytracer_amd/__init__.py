@@ -386,6 +386,24 @@ class Renderer:
             "vrt_render_temporal_rows_async",
         )
 
+    def render_temporal_batch_async(self, cams, params, row0: int, rows: int, row_step: int,
+                                    d_curs, d_raws=None, stream: int = 0, pitch: int = 0,
+                                    row_block: int = 1):
+        """The same band of len(cams) frames in one launch at alpha 1 (vrt_render_temporal_batch_async,
+        ABI v14): cams / params / d_curs (/ d_raws) one per frame; params may differ only in time."""
+        nf = len(cams)
+        if isinstance(params, Params):
+            params = [params] * nf
+        ca = (Camera * nf)(*cams)
+        pa = (Params * nf)(*params)
+        cur = (C.c_void_p * nf)(*d_curs)
+        raw = (C.c_void_p * nf)(*d_raws) if d_raws else None
+        self._check(
+            self._lib.vrt_render_temporal_batch_async(self._h, nf, ca, pa, row0, rows, row_step, row_block,
+                                                      pitch or cams[0].width, cur, raw, stream or None),
+            "vrt_render_temporal_batch_async",
+        )
+
     def render_frame(self, cam: Camera, params: Params, alpha: float = 1.0, counters: bool = False):
         """main.cpp's frame loop with the history in the context (vrt_render_frame): returns the
         new filtered frame as rgba8[H,W,4] uint8 and the stats (counters only when asked: they

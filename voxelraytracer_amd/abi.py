@@ -171,6 +171,12 @@ SIGNATURES = {
          C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
          C.c_void_p, C.c_void_p],
     ),
+    "vrt_render_temporal_batch_async": (
+        C.c_int,
+        [C.c_void_p, C.c_int32, C.POINTER(Camera), C.POINTER(Params), C.c_int32, C.c_int32,
+         C.c_int32, C.c_int32, C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+         C.c_void_p],
+    ),
     "vrt_render_temporal_rows_async": (
         C.c_int,
         [C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_float, C.c_int32, C.c_int32,

@@ -70,6 +70,7 @@ static_assert(kRing % kLanes == 0, "a ring slot is always written from the same 
 
 struct OrderSlot {
   int32_t width = 0, rows = 0, row0 = 0, row_step = 0, row_blk_sh = 0;
+  int32_t nframes = 1;         // frames per launch (frame batches)
   hipStream_t stream = nullptr;
   uint32_t* d = nullptr;       // kOrderSlotWords words inside the shard's pool
   bool used = false;
@@ -445,6 +446,9 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.exact_fat = 0;
   a.exact_grid = 0;
   a.batches_out = nullptr;
+  a.nframes = 1;
+  a.frame_tiles = a.tiles;
+  std::memset(a.fb, 0, sizeof(a.fb));
   return a;
 }
 
@@ -466,7 +470,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
   OrderSlot* slot = nullptr;
   for (auto& o : s.order)
     if (o.used && o.width == a.width && o.rows == a.rows && o.row0 == a.row0 && o.row_step == a.row_step &&
-        o.row_blk_sh == a.row_blk_sh && o.stream == st)
+        o.row_blk_sh == a.row_blk_sh && o.nframes == a.nframes && o.stream == st)
       slot = &o;
   if (!slot) {
     slot = &s.order[0];
@@ -486,6 +490,7 @@ OrderSlot* acquire_slot(Shard& s, const vrt::KArgs& a, hipStream_t st) {
     slot->row0 = a.row0;
     slot->row_step = a.row_step;
     slot->row_blk_sh = a.row_blk_sh;
+    slot->nframes = a.nframes;
     slot->stream = st;
     slot->epoch = 0;
     slot->last_defer = false;
@@ -516,7 +521,8 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 }
 
 OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
-  const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 &&
+  // (the deferred list packs a pixel as frame | band row | column in 3 | 13 | 16 bits)
+  const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 && a.rows < 8192 &&
                      (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
   // the tile order only where it pays: glass in the volume (without it the order gains nothing:
   // C2 ±0, C4 +5 %, profiles/r02_s14_tileorder) and certified pixels (glass-heavy volumes, where
@@ -1461,6 +1467,59 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
   launch_timing_events(ctx, eb, ee);
   launch(ctx, s, a, nullptr, d_out_hit, reinterpret_cast<unsigned long long*>(d_counters),
          static_cast<hipStream_t>(hip_stream), eb, ee);
+  VRT_HIP(ctx, hipGetLastError());
+  return VRT_OK;
+}
+
+int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams, const vrt_params* p,
+                                    int32_t row0, int32_t rows, int32_t row_step, int32_t row_block, int64_t pitch,
+                                    uint32_t* const* d_cur_rgba8, uint32_t* const* d_raw_rgba8, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (nframes < 1 || nframes > vrt::kMaxBatch || !cams || !d_cur_rgba8)
+    return fail(ctx, VRT_ERR_INVALID, "nframes must be in [1, 8] with a camera and an output per frame");
+  int st = check_render_args(ctx, &cams[0], p);
+  if (st != VRT_OK) return st;
+  for (int f = 0; f < nframes; ++f) {
+    if (!d_cur_rgba8[f]) return fail(ctx, VRT_ERR_INVALID, "null output");
+    if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
+      return fail(ctx, VRT_ERR_INVALID, "the frames of a batch share the image size");
+  }
+  int32_t sh = 0;
+  if ((st = check_band(ctx, &cams[0], row0, rows, row_step, pitch, row_block, &sh)) != VRT_OK) return st;
+  if (nframes > 1 && rows >= 8192) return fail(ctx, VRT_ERR_UNSUPPORTED, "frame batches need bands of < 8192 rows");
+  if (rows == 0) return VRT_OK;
+  Shard& s = ctx->sh[0];
+  vrt::KArgs a = make_args(ctx, s, &cams[0], p, row0, rows, row_step);
+  a.row_blk_sh = sh;
+  a.pitch = int32_t(pitch);
+  a.alpha = 1.0f;  // frames of a batch are independent: no history is read
+  a.prev = d_cur_rgba8[0];
+  a.cur = d_cur_rgba8[0];
+  a.raw = d_raw_rgba8 ? d_raw_rgba8[0] : nullptr;
+  a.time = p[0].time;
+  for (int f = 1; f < nframes; ++f) {
+    vrt::KArgs::FrameB& b = a.fb[f - 1];
+    std::memcpy(b.inv_pv, cams[f].inv_pv, sizeof(b.inv_pv));
+    b.time = p[f].time;
+    b.cur = d_cur_rgba8[f];
+    b.raw = d_raw_rgba8 ? d_raw_rgba8[f] : nullptr;
+    // every other parameter is one per launch
+    const vrt_params& q = p[f];
+    const bool same = q.sun_dir[0] == p[0].sun_dir[0] && q.sun_dir[1] == p[0].sun_dir[1] &&
+                      q.sun_dir[2] == p[0].sun_dir[2] && q.ray_noise == p[0].ray_noise &&
+                      q.reflection_noise == p[0].reflection_noise && q.refraction_noise == p[0].refraction_noise &&
+                      q.max_ray_length == p[0].max_ray_length && q.max_reflections == p[0].max_reflections &&
+                      q.max_transparencies == p[0].max_transparencies && q.color_only == p[0].color_only &&
+                      q.atlas_rgba == p[0].atlas_rgba && q.atlas_size == p[0].atlas_size &&
+                      q.atlas_texture_size == p[0].atlas_texture_size;
+    if (!same) return fail(ctx, VRT_ERR_INVALID, "the frames of a batch may differ only in camera and time");
+  }
+  a.nframes = nframes;
+  a.frame_tiles = a.tiles;
+  a.tiles = a.frame_tiles * uint32_t(nframes);
+  hipEvent_t eb, ee;
+  launch_timing_events(ctx, eb, ee);
+  launch(ctx, s, a, nullptr, nullptr, nullptr, static_cast<hipStream_t>(hip_stream), eb, ee);
   VRT_HIP(ctx, hipGetLastError());
   return VRT_OK;
 }

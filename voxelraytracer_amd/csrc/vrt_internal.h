@@ -61,7 +61,19 @@ struct KArgs {
   // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
   uint32_t exact_grid;
   uint32_t* batches_out;
+  // frame batches (vrt_render_temporal_batch_async, alpha 1): `nframes` frames of the same band in
+  // one launch, frame f's tiles at [f * frame_tiles, (f + 1) * frame_tiles) of the grid (tiles =
+  // nframes * frame_tiles); frame 0 is inv_pv / time / cur / raw above, frame f >= 1 is fb[f - 1]
+  int32_t nframes;
+  uint32_t frame_tiles;
+  struct FrameB {
+    float inv_pv[16];
+    float time;
+    uint32_t* cur;
+    uint32_t* raw;
+  } fb[7];
 };
+constexpr int kMaxBatch = 8;  // frames per launch (1 + the fb entries)
 #if defined(VRT_EXACT_GRID_ADAPT) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_EXACT_GRID_ADAPT is an A/B knob of make variant builds"
 #endif

@@ -1821,6 +1821,20 @@ __device__ __forceinline__ uint32_t xcc_id() {
 #define VRT_MIN_WAVES 7
 #endif
 
+// The per-frame fields of frame f of a launch (frame batches, KArgs::nframes): its camera, time
+// and outputs (the history is read only at alpha != 1, where launches hold one frame)
+struct FrameView {
+  const float* pv;
+  float time;
+  uint32_t* cur;
+  uint32_t* raw;
+};
+__device__ __forceinline__ FrameView frame_view(const KArgs& a, uint32_t f) {
+  if (f == 0u) return FrameView{a.inv_pv, a.time, a.cur, a.raw};
+  const KArgs::FrameB& b = a.fb[f - 1u];
+  return FrameView{b.inv_pv, b.time, b.cur, b.raw};
+}
+
 // Per-launch constants of the walk context
 __device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t* __restrict__ vox) {
   c.vox = vox;
@@ -1860,16 +1874,17 @@ __device__ __forceinline__ f3 div3_rn(float x, float y, float z, float d) {
   return mk(x / d, y / d, z / d);
 }
 
-__device__ __forceinline__ Ray primary_ray(const KArgs& a, const Ctx& c, int px, int py) {
+__device__ __forceinline__ Ray primary_ray(const KArgs& a, const float* __restrict__ inv_pv, const Ctx& c, int px,
+                                           int py) {
   // (2 (p + 0.5)) / W with RN(1/W) from the host: the numerator is in (0, 2W), W <= 32768
   const float ndx = div_rn(2.0f * (float(px) + 0.5f), float(a.width), a.rcp_w) - 1.0f;
   const float ndy = div_rn(2.0f * (float(py) + 0.5f), float(a.height), a.rcp_h) - 1.0f;
   float n4[4], f4[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float base = a.inv_pv[0 * 4 + i] * ndx + a.inv_pv[1 * 4 + i] * ndy;
-    n4[i] = (base + a.inv_pv[2 * 4 + i] * -1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
-    f4[i] = (base + a.inv_pv[2 * 4 + i] * 1.0f) + a.inv_pv[3 * 4 + i] * 1.0f;
+    const float base = inv_pv[0 * 4 + i] * ndx + inv_pv[1 * 4 + i] * ndy;
+    n4[i] = (base + inv_pv[2 * 4 + i] * -1.0f) + inv_pv[3 * 4 + i] * 1.0f;
+    f4[i] = (base + inv_pv[2 * 4 + i] * 1.0f) + inv_pv[3 * 4 + i] * 1.0f;
   }
   const f3 vnear = div3_rn(n4[0], n4[1], n4[2], n4[3]);
   const f3 vdir = div3_rn(f4[0], f4[1], f4[2], f4[3]) - vnear;
@@ -2034,14 +2049,14 @@ __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ra
 
 // output of one pixel: float RGBA, or the fused reference post-pass (RGB8 ray-trace store,
 // temporal blend, RGB8 store)
-__device__ __forceinline__ void store_pixel(const KArgs& a, float4* __restrict__ out, size_t o,
-                                            const f3 color) {
-  if (a.cur) {
+__device__ __forceinline__ void store_pixel(const KArgs& a, const FrameView& fv, float4* __restrict__ out,
+                                            size_t o, const f3 color) {
+  if (fv.cur) {
     const uint32_t rw = pack_rgb8(color.x, color.y, color.z);
-    if (a.raw) a.raw[o] = rw;
+    if (fv.raw) fv.raw[o] = rw;
     // u_Alpha = 1 (the slider default): 1 * b/255 + 0 * old stores b back for every byte b and any
     // history (exhaustive, tests/test_temporal_oracle.py), so the history is not read
-    a.cur[o] = a.alpha == 1.0f ? rw : temporal_blend(rw, a.prev[o], a.alpha);
+    fv.cur[o] = a.alpha == 1.0f ? rw : temporal_blend(rw, a.prev[o], a.alpha);
   } else {
     out[o] = make_float4(color.x, color.y, color.z, 1.0f);
   }
@@ -2096,7 +2111,10 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     if (tile == ~0u) return;  // whole workgroup: its tile is rendered by another slot
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
-  const uint32_t ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  // frame batches: the tile's frame and its tile within the frame (wave-uniform)
+  const uint32_t fr = a.nframes > 1 ? uint32_t(__builtin_amdgcn_readfirstlane(int(tile / a.frame_tiles))) : 0u;
+  const uint32_t ltile = tile - fr * a.frame_tiles;
+  const uint32_t ty = ltile / a.tiles_x, tx = ltile - ty * a.tiles_x;
   const int px = pixel_x(tx, wave, lane_id());
   const int li = pixel_row(ty, wave, lane_id());
   const bool valid = px < a.width && li < a.rows;
@@ -2110,9 +2128,11 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   if (valid) {
     Ctx c;
     init_ctx(c, a, vox);
+    const FrameView fv = frame_view(a, fr);
+    c.time = fv.time;
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * kAxLane];
-    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+    const Ray ray = primary_ray(a, fv.pv, c, px, frame_row(a, li));
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
     uint32_t steps = 0, flags = 0;
@@ -2153,7 +2173,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
       hr.flags = flags;
       hits[o] = hr;
     }
-    if (!deferred) store_pixel(a, out, o, color);
+    if (!deferred) store_pixel(a, fv, out, o, color);
   }
   if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
     const unsigned long long m = __ballot(deferred);
@@ -2175,7 +2195,8 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
       base = uint32_t(__builtin_amdgcn_readlane(int(base), int(first)));
       uint32_t* list = a.defer + kDeferHdr + seg * a.defer_seg;
       const uint32_t l3 = lane_id();  // the pixel re-derived (not kept live across the walks)
-      const uint32_t id = (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
+      // frame (3 bits) | band row (13 bits) | column (16 bits): batches need rows < 8192
+      const uint32_t id = (fr << 29) | (uint32_t(pixel_row(ty, wave, l3)) << 16) | uint32_t(pixel_x(tx, wave, l3));
       if (dense) {  // chunks fill the segment's region from its end
         list[a.defer_seg - 64u * (base + 1u) + l3] = deferred ? id : ~0u;
       } else if (deferred) {
@@ -2315,8 +2336,12 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     const uint32_t* list = a.defer + kDeferHdr + seg * a.defer_seg;
     const uint32_t e = dense ? list[a.defer_seg - 64u * (idx + 1u) + lane] : list[idx];
     if (e == ~0u) continue;  // a lane of a dense chunk whose pixel the certified pass settled
-    const int px = int(e & 0xFFFFu), li = int(e >> 16);
-    const Ray ray = primary_ray(a, c, px, frame_row(a, li));
+    Ray ray;
+    {
+      const FrameView fv = frame_view(a, e >> 29);
+      c.time = fv.time;
+      ray = primary_ray(a, fv.pv, c, int(e & 0xFFFFu), frame_row(a, int((e >> 16) & 0x1FFFu)));
+    }
     Counters k;
 #pragma unroll
     for (int q = 0; q < VRT_CNT_COUNT; ++q) k.c[q] = 0;
@@ -2327,7 +2352,11 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     __shared__ float lstk[VRT_LDS_STACK ? kStackWords * 64 : 1];
     (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, 64>(a, c, ray, color, k, steps, flags,
                                                                     hit_vidx, hit_len, &lstk[lane]);
-    store_pixel(a, out, size_t(li) * size_t(a.pitch) + size_t(px), color);
+    // the pixel and its frame re-derived from e (only e stays live across the exact path)
+    uint32_t e2 = e;
+    asm volatile("" : "+v"(e2));  // not CSE'd with the decode above (whose results would stay live)
+    store_pixel(a, frame_view(a, e2 >> 29), out, size_t((e2 >> 16) & 0x1FFFu) * size_t(a.pitch) + size_t(e2 & 0xFFFFu),
+                color);
 #ifdef VRT_STAMPS
     xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);
 #endif

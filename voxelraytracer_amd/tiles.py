@@ -131,13 +131,13 @@ class GatherTorch:
     def __init__(self, group=None):
         self.group = group
 
-    def run(self, tiler, lane: int) -> None:
-        band = tiler.bufs[lane]
-        glist = list(tiler.gathered[lane].unbind(0)) if tiler.rank == 0 else None
+    def run(self, tiler, slot: int) -> None:
+        band = tiler.bufs[slot]
+        glist = list(tiler.gathered[slot].unbind(0)) if tiler.rank == 0 else None
         dist.gather(band, glist, dst=0, group=self.group)
         if tiler.rank == 0:
-            g = tiler.gathered[lane]
-            tiler.frames[lane].index_copy_(0, tiler.asm_index, g.view(-1, *g.shape[2:]))
+            g = tiler.gathered[slot]
+            tiler.frames[slot].index_copy_(0, tiler.asm_index, g.view(-1, *g.shape[2:]))
 
 
 class GatherLib:
@@ -164,20 +164,21 @@ class GatherLib:
         self.words = tiler.width * tiler.channels * tiler.dtype.itemsize // 4
         self.packed = self.gpacked = None
         dev = tiler.bufs[0].device
-        if self.rgb8:   # per lane: the packed band, and (rank 0) the gathered packed bands
+        if self.rgb8:   # per frame slot: the packed band, and (rank 0) the gathered packed bands
             px = tiler.rmax * tiler.width
-            self.packed = [torch.empty(px * 3, dtype=torch.uint8, device=dev) for _ in range(tiler.lanes)]
+            self.packed = [torch.empty(px * 3, dtype=torch.uint8, device=dev) for _ in range(tiler.slots)]
             if tiler.rank == 0:
                 self.gpacked = [torch.empty(tiler.world * px * 3, dtype=torch.uint8, device=dev)
-                                for _ in range(tiler.lanes)]
+                                for _ in range(tiler.slots)]
         self.args = []
-        for g in range(tiler.lanes):   # (band, pixels, packed, gathered, frame, stream)
+        for g in range(tiler.slots):   # (band, pixels, packed, gathered, frame, stream, communicator)
             self.args.append((tiler.bufs[g].data_ptr(), tiler.bufs[g].numel() // tiler.channels,
                               self.packed[g].data_ptr() if self.rgb8 else 0,
                               (self.gpacked[g] if self.rgb8 else tiler.gathered[g]).data_ptr()
                               if tiler.rank == 0 else 0,
                               tiler.frames[g].data_ptr() if tiler.rank == 0 else 0,
-                              tiler.part_streams[g][0].cuda_stream))
+                              tiler.part_streams[g // tiler.batch][0].cuda_stream,
+                              (g // tiler.batch) % self.lanes))
 
     def bytes_per_rank(self, tiler) -> int:
         """Bytes every rank sends per frame."""
@@ -186,11 +187,10 @@ class GatherLib:
         px = tiler.rmax * tiler.width
         return px * 3 if self.rgb8 else px * tiler.channels * tiler.dtype.itemsize
 
-    def run(self, tiler, lane: int) -> None:
+    def run(self, tiler, slot: int) -> None:
         if self.args is None:
             self._setup(tiler)
-        band, px, packed, gath, frame, st = self.args[lane]
-        comm = lane % self.lanes
+        band, px, packed, gath, frame, st, comm = self.args[slot]
         if self.rgb8:
             self.ren.pack_rgb8_async(band, px, packed, st)
             self.ren.gather_band_async(comm, packed, px * 3, gath, st)
@@ -229,13 +229,18 @@ class FrameTiler:
     part's HIP stream; frames whose lanes need no event ordering (one lane, or independent) then
     enqueue from precomputed arguments with no torch stream switches or tensor views (~4 us per
     launch on the host instead of ~20: a band of a k-GPU split at k = 8 renders in ~11 us).
+    batch > 1 (independent frames, one part, launch_batch given): `batch` consecutive frames of a
+    lane are rendered by ONE launch, launch_batch(row0, rows, row_step, out_ptrs, pitch, stream)
+    (vrt_render_temporal_batch_async), enqueued when the batch's last frame is requested (finish()
+    enqueues a partial batch); each frame has its own buffer (slot), exchanged after the launch. A
+    lane then holds `batch` frames in flight.
     """
 
     def __init__(self, width: int, height: int, render_band: Callable, device, group=None,
                  channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
                  lanes: int = 1, independent: bool = False, launch: Optional[Callable] = None,
                  world: Optional[int] = None, rank: Optional[int] = None, row_block: int = 1,
-                 exchange=None):
+                 exchange=None, batch: int = 1, launch_batch: Optional[Callable] = None):
         # world / rank: override the process group's (one process rehearsing rank `rank` of a
         # `world`-way split on one GPU; no exchange may then be requested)
         self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -244,6 +249,11 @@ class FrameTiler:
             raise ValueError("a rehearsed split keeps its band (gather=False)")
         if lanes < 1:
             raise ValueError("lanes >= 1")
+        if batch < 1 or (batch > 1 and (not independent or parts != 1 or launch_batch is None)):
+            raise ValueError("frame batches need independent frames, one part and launch_batch")
+        self.batch = batch
+        self.slots = lanes * batch   # frame buffers: slot = lane * batch + frame of the batch
+        self.pending = 0             # frames of the current batch requested but not yet launched
         self.group = group
         self.width, self.height, self.parts = width, height, parts
         self.row_block = row_block
@@ -270,36 +280,46 @@ class FrameTiler:
         # on that lane's own communicator in enqueue order, so every rank must enqueue the same
         # frames on every lane: exchange_log() is compared across ranks (bench.py)
         self.xlog = [[0, 0] for _ in range(lanes)]
+        self.launch_batch = launch_batch
         self.latest = None
         if self.gather:
             # every rank's band padded to the largest band's rows: equal gather sizes
             specs = [block_band_spec(r, self.world, height, row_block) for r in range(self.world)]
             self.rmax = max(sp[1] for sp in specs)
             self.bufs = [torch.zeros((self.rmax, width, channels), dtype=dtype, device=device)
-                         for _ in range(lanes)]
+                         for _ in range(self.slots)]
             self.gathered = self.frames = None
             if self.rank == 0:
                 self.gathered = [torch.empty((self.world, self.rmax, width, channels), dtype=dtype,
-                                             device=device) for _ in range(lanes)]
+                                             device=device) for _ in range(self.slots)]
                 # frame row of every gathered row; padding rows land in a scratch row `height`
                 idx = torch.full((self.world, self.rmax), height, dtype=torch.int64)
                 for r, (r0, rows, step) in enumerate(specs):
                     idx[r, :rows] = band_frame_rows(r0, rows, step, row_block)
                 self.asm_index = idx.reshape(-1).to(device)
                 self.frames = [torch.zeros((height + 1, width, channels), dtype=dtype, device=device)
-                               for _ in range(lanes)]
+                               for _ in range(self.slots)]
             self.exchange = exchange or GatherTorch(group)
         else:
             # this rank's band per lane; part s renders band rows s, s + parts, ... in place
             self.bufs = [torch.zeros((self.rows, width, channels), dtype=dtype, device=device)
-                         for _ in range(lanes)]
+                         for _ in range(self.slots)]
         self.part_streams = ([[torch.cuda.Stream(device=device) for _ in range(parts)]
                               for _ in range(lanes)]
-                             if self.cuda and (parts > 1 or lanes > 1 or self.gather) else None)
+                             if self.cuda and (parts > 1 or lanes > 1 or self.gather or batch > 1) else None)
         self.part_done = [[None] * parts for _ in range(lanes)]   # dependent lanes: frame events
         self.fresh = True   # the streams must first wait for the current stream's work
         self.plan = None   # lean launches: per lane, per part (row0, rows, step, out, prev, pitch, stream)
-        if launch is not None and self.part_streams is not None and (lanes == 1 or independent):
+        if batch > 1:
+            if self.part_streams is None:
+                raise ValueError("frame batches need CUDA streams")
+            row0, rows, step = self.specs[0]
+            self.plan = []   # per lane: (row0, rows, step, out pointers of its slots, pitch, stream)
+            for g in range(lanes):
+                outs = [self.part_rows(self.bufs[g * batch + j], 0) for j in range(batch)]
+                self.plan.append((row0, rows, step, [o.data_ptr() for o in outs], row_pitch(outs[0]),
+                                  self.part_streams[g][0].cuda_stream))
+        elif launch is not None and self.part_streams is not None and (lanes == 1 or independent):
             self.launch = launch
             self.plan = []
             for g in range(lanes):
@@ -320,16 +340,20 @@ class FrameTiler:
             return buf[:self.rows]
         return buf.view(self.rows_p, self.parts, self.width, -1)[:, s]
 
+    def slot_of(self, k: int) -> int:
+        """The buffer slot of frame k (its lane's batch position)."""
+        return ((k // self.batch) % self.lanes) * self.batch + k % self.batch
+
     def last(self) -> torch.Tensor:
         """This rank's band buffer of the last frame enqueued (its band rows)."""
-        b = self.bufs[(self.k - 1) % self.lanes]
+        b = self.bufs[self.slot_of(self.k - 1)]
         return b[:self.rows] if self.gather else b
 
     def next_stream(self):
         """The HIP stream the next frame's (first) launch is enqueued on (CUDA), or None."""
         if self.part_streams is None:
             return torch.cuda.current_stream() if self.cuda else None
-        return self.part_streams[self.k % self.lanes][0]
+        return self.part_streams[(self.k // self.batch) % self.lanes][0]
 
     def _render_parts(self, lane: int, band: torch.Tensor, prev: torch.Tensor):
         """Enqueue every part of the next frame on `lane` (and its exchange). Returns the parts'
@@ -367,9 +391,35 @@ class FrameTiler:
                 events.append(ev)
         return events
 
-    def _log_exchange(self, lane: int) -> None:
+    def _log_exchange(self, lane: int, k: Optional[int] = None) -> None:
         self.xlog[lane][0] += 1
-        self.xlog[lane][1] += self.k - 1   # the index of the frame being enqueued
+        self.xlog[lane][1] += self.k - 1 if k is None else k   # the index of the frame being enqueued
+
+    def _flush_batch(self) -> None:
+        """Launch the pending frames of the current batch (one launch) and their exchanges."""
+        n = self.pending
+        if n == 0:
+            return
+        self.pending = 0
+        k0 = self.k - n
+        lane = (k0 // self.batch) % self.lanes
+        if self.fresh:
+            cur = torch.cuda.current_stream()
+            for ln in self.part_streams:
+                for st in ln:
+                    st.wait_stream(cur)
+            self.fresh = False
+        row0, rows, step, outs, pitch, stream = self.plan[lane]
+        self.launch_batch(row0, rows, step, outs[:n], pitch, stream, **self.block_kw)
+        if self.gather and self.exchange_on:
+            for j in range(n):
+                self._log_exchange(lane, k0 + j)
+                slot = lane * self.batch + j
+                if isinstance(self.exchange, GatherLib):
+                    self.exchange.run(self, slot)
+                else:
+                    with torch.cuda.stream(self.part_streams[lane][0]):
+                        self.exchange.run(self, slot)
 
     def exchange_log(self):
         """Per lane [exchanges enqueued, sum of their frame indices] (a flat list of 2 x lanes ints):
@@ -378,6 +428,16 @@ class FrameTiler:
 
     # ---- pipeline --------------------------------------------------------------------------
     def frame(self) -> Optional[torch.Tensor]:
+        if self.batch > 1:   # frame batches: one launch per `batch` frames of a lane
+            slot = self.slot_of(self.k)
+            self.k += 1
+            self.pending += 1
+            if self.pending == self.batch:
+                self._flush_batch()
+            if not self.gather:
+                return self.bufs[slot]
+            self.latest = self.frames[slot][:self.height] if self.rank == 0 else None
+            return self.latest
         lane = self.k % self.lanes
         self.k += 1
         if self.plan is not None:   # lean launches from precomputed arguments
@@ -438,7 +498,15 @@ class FrameTiler:
         """The HIP streams the frames are enqueued on (empty without part streams)."""
         return [st for ln in (self.part_streams or ()) for st in ln]
 
+    def flush(self) -> None:
+        """Enqueue the frames of a partial batch now (frame batches; no-op otherwise): e.g. before
+        recording an event after the last frame of a timed region."""
+        if self.batch > 1:
+            self._flush_batch()
+
     def finish(self) -> Optional[torch.Tensor]:
+        if self.batch > 1:
+            self._flush_batch()   # a partial batch
         if self.cuda:
             cur = torch.cuda.current_stream()
             for ln in self.part_streams or ():

@@ -568,13 +568,18 @@ def main():
         if world > 1:
             dist.barrier()
         st_ = tiler.next_stream()
-        ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ea.record(st_)
+        lane_ = (tiler.k // tiler.batch) % tiler.lanes
+        sts_ = tiler.part_streams[lane_] if tiler.part_streams else [st_]   # every part of the frame
+        ea = [torch.cuda.Event(enable_timing=True) for _ in sts_]
+        eb = [torch.cuda.Event(enable_timing=True) for _ in sts_]
+        for e, s_ in zip(ea, sts_):
+            e.record(s_)
         tiler.frame()
         tiler.flush()   # frame batches: the frame alone is a batch of one
-        eb.record(st_)
+        for e, s_ in zip(eb, sts_):
+            e.record(s_)
         torch.cuda.synchronize(dev)
-        lat.append(ea.elapsed_time(eb))
+        lat.append(max(a.elapsed_time(b) for a in ea for b in eb))
     tiler.finish()
     lat_t = torch.tensor([float(np.median(lat))], dtype=torch.float64, device=dev)
     if world > 1:

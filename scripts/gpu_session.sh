@@ -78,6 +78,15 @@ for st in "$@"; do
           echo "drvx $xc [${xfl[$j]}] $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/drvx_${xc}_${j}_$i.log | head -1) $(grep -o '"frame_events_ms": \[[^]]*\]' $OUT/drvx_${xc}_${j}_$i.log | head -1)"
         done
       done ;;
+    benchx)  # bench runs per flag set, ROUNDS alternating: benchx:CFG,STEPS,ROUNDS,"FLAGS1|FLAGS2"
+      IFS=, read yc ys yr yf <<< "$arg"
+      IFS='|' read -ra yfl <<< "$yf"
+      for ((i = 1; i <= ${yr:-2}; i++)); do
+        for j in "${!yfl[@]}"; do
+          TAILN=0 run benchx_${yc}_s${ys}_${j}_$i 150 python bench.py --config $yc --steps $ys --warmup 5 --cpu-seconds 0 --no-verify ${yfl[$j]}
+          echo "benchx $yc s$ys [${yfl[$j]}] $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/benchx_${yc}_s${ys}_${j}_$i.log | head -1) $(grep -o '"kernel_ms": [0-9.]*' $OUT/benchx_${yc}_s${ys}_${j}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/benchx_${yc}_s${ys}_${j}_$i.log | head -1)"
+        done
+      done ;;
     drvab)  # the driver's 20-frame command, ROUNDS alternating rounds over base + build/variants/*.so
       IFS=, read dc dr <<< "$arg"
       for ((i = 1; i <= ${dr:-4}; i++)); do

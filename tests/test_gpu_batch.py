@@ -48,6 +48,7 @@ def batched(r, cams, ps, row0, rows, step, block):
     ("refraction", 128, 640, 360, 4, 4, 8, 8, 5),      # an 8-way block-cyclic band, 8 frames
     ("glass_cube", 64, 320, 200, 1, 2, 2, 2, 1),
     ("terrain", 64, 384, 216, 4, 2, 4, 4, 2),
+    ("terrain", 64, 3840, 2160, 4, 2, 2, 1, 0),        # 2 x 64 800 tiles: split into two launches
 ])
 def test_batch_equals_single_frames(built, scene, n, w, h, R, T, nf, ranks, rank):
     block = 16 if ranks > 1 else 1

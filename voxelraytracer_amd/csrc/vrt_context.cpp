@@ -1514,13 +1514,31 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
                       q.atlas_texture_size == p[0].atlas_texture_size;
     if (!same) return fail(ctx, VRT_ERR_INVALID, "the frames of a batch may differ only in camera and time");
   }
-  a.nframes = nframes;
-  a.frame_tiles = a.tiles;
-  a.tiles = a.frame_tiles * uint32_t(nframes);
-  hipEvent_t eb, ee;
-  launch_timing_events(ctx, eb, ee);
-  launch(ctx, s, a, nullptr, nullptr, nullptr, static_cast<hipStream_t>(hip_stream), eb, ee);
-  VRT_HIP(ctx, hipGetLastError());
+  // a launch holds at most kOrderMaxTiles tiles (the tile order's and the deferred list's slot):
+  // a larger batch is enqueued as consecutive launches of as many frames as fit
+  const uint32_t ft = a.tiles;
+  const int per = int(std::max<uint32_t>(1u, std::min<uint32_t>(uint32_t(nframes), kOrderMaxTiles / std::max(ft, 1u))));
+  const vrt::KArgs all = a;
+  for (int f0 = 0; f0 < nframes; f0 += per) {
+    const int nf = std::min(per, nframes - f0);
+    vrt::KArgs b = all;
+    if (f0 > 0) {  // frame f0 of the batch becomes the launch's frame 0
+      const vrt::KArgs::FrameB& z = all.fb[f0 - 1];
+      std::memcpy(b.inv_pv, z.inv_pv, sizeof(b.inv_pv));
+      b.time = z.time;
+      b.cur = z.cur;
+      b.prev = z.cur;
+      b.raw = z.raw;
+      for (int f = 1; f < nf; ++f) b.fb[f - 1] = all.fb[f0 + f - 1];
+    }
+    b.nframes = nf;
+    b.frame_tiles = ft;
+    b.tiles = ft * uint32_t(nf);
+    hipEvent_t eb, ee;
+    launch_timing_events(ctx, eb, ee);
+    launch(ctx, s, b, nullptr, nullptr, nullptr, static_cast<hipStream_t>(hip_stream), eb, ee);
+    VRT_HIP(ctx, hipGetLastError());
+  }
   return VRT_OK;
 }
 

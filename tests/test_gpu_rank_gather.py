@@ -79,7 +79,7 @@ def test_rank_comm_gather_one_rank(built, wire):
             b[..., 3] = 255   # rendered RGBA8 words: A = 255
         tiler = types.SimpleNamespace(
             width=w, height=h, channels=4, dtype=torch.uint8, world=1, rank=0, rmax=h, row_block=block,
-            lanes=lanes, bufs=bufs, part_streams=[[s] for s in st],
+            lanes=lanes, slots=lanes, batch=1, bufs=bufs, part_streams=[[s] for s in st],
             gathered=[torch.zeros((1, h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)],
             frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)])
         for lane in range(lanes):

@@ -94,6 +94,10 @@ class Stats(C.Structure):
 HIT_DTYPE = [("voxel_index", "<i4"), ("ray_length", "<f4"), ("steps", "<u4"), ("flags", "<u4")]
 
 # name -> (restype, argtypes): every function include/vrt.h declares
+# entry points added after ABI v12 (an older build loaded by VRT_LIB with VRT_LIB_ABI=<its version>
+# may lack exactly these)
+ADDED_IN = {"vrt_render_temporal_batch_async": 14}
+
 SIGNATURES = {
     "vrt_abi_version": (C.c_int, []),
     "vrt_create": (C.c_int, [C.c_uint32, C.POINTER(C.c_void_p)]),
@@ -242,9 +246,12 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     except ImportError:
         pass
     lib = C.CDLL(path)
+    older = int(os.environ.get("VRT_LIB_ABI", "0"))   # A/B against an older ABI's build (VRT_LIB)
     for name, (res, args) in SIGNATURES.items():
         if not hasattr(lib, name) and name.startswith("vrt_debug_"):
             continue   # diagnostic entry points exist only in diagnostic builds (make variant)
+        if not hasattr(lib, name) and os.environ.get("VRT_LIB") and older and older < ADDED_IN.get(name, 0):
+            continue   # an entry point newer than the declared ABI of the VRT_LIB build
         # every other symbol must be there: A/B variants (VRT_LIB) are built from this tree, and an
         # ABI/build mismatch fails here, at load time, not at the first call
         fn = getattr(lib, name)

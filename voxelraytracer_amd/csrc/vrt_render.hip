@@ -2085,7 +2085,10 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, const FrameView& fv,
 #ifndef VRT_EXACT_WAVES
 #define VRT_EXACT_WAVES VRT_MIN_WAVES
 #endif
-template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false>
+// FB: the frame-batch instance (KArgs::nframes > 1: per-frame camera, time and outputs, the frame
+// in a deferred entry's top bits); launches of one frame keep the instance without that decode
+// (it cost C1 4 %, C3 1 %: profiles/r05_s27)
+template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false, bool FB = false>
 __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -2112,7 +2115,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   }
   tile = __builtin_amdgcn_readfirstlane(tile);
   // frame batches: the tile's frame and its tile within the frame (wave-uniform)
-  const uint32_t fr = a.nframes > 1 ? uint32_t(__builtin_amdgcn_readfirstlane(int(tile / a.frame_tiles))) : 0u;
+  const uint32_t fr = FB ? uint32_t(__builtin_amdgcn_readfirstlane(int(tile / a.frame_tiles))) : 0u;
   const uint32_t ltile = tile - fr * a.frame_tiles;
   const uint32_t ty = ltile / a.tiles_x, tx = ltile - ty * a.tiles_x;
   const int px = pixel_x(tx, wave, lane_id());
@@ -2128,11 +2131,10 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
   if (valid) {
     Ctx c;
     init_ctx(c, a, vox);
-    const FrameView fv = frame_view(a, fr);
-    c.time = fv.time;
+    if constexpr (FB) c.time = frame_view(a, fr).time;
     __shared__ float4 ax_tab[kWgThreads * 3];
     c.ax = &ax_tab[threadIdx.x * kAxLane];
-    const Ray ray = primary_ray(a, fv.pv, c, px, frame_row(a, li));
+    const Ray ray = primary_ray(a, FB ? frame_view(a, fr).pv : a.inv_pv, c, px, frame_row(a, li));
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
     uint32_t steps = 0, flags = 0;
@@ -2173,7 +2175,9 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
       hr.flags = flags;
       hits[o] = hr;
     }
-    if (!deferred) store_pixel(a, fv, out, o, color);
+    // the frame's outputs read here, where they are used (kept live across the walks they were
+    // held in registers, and their spills cost the in-lane exact instance 4 %)
+    if (!deferred) store_pixel(a, FB ? frame_view(a, fr) : FrameView{a.inv_pv, a.time, a.cur, a.raw}, out, o, color);
   }
   if constexpr (DEFER) {  // the wave's deferred pixels to the exact pass's list: ballot compaction
     const unsigned long long m = __ballot(deferred);
@@ -2284,7 +2288,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 // whose frame time includes this pass's span: a sparse wave's span is its slowest walk, and a lone
 // wave's walks cost the same per step with 16 lanes as with 64 (C4 k = 8 band 0.0222 -> 0.0200 ms,
 // exact-pass span 58 -> 49 us; whole frames +1-3 %: more waves, profiles/r04_exact/)
-template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, uint32_t SB = VRT_SPARSE_BATCH>
+template <bool TEX, int CERT, int WAVES = VRT_EXACT_WAVES, uint32_t SB = VRT_SPARSE_BATCH, bool FB = false>
 __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                                      float4* __restrict__ out) {
   const uint32_t* ctr = a.defer;
@@ -2337,10 +2341,12 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     const uint32_t e = dense ? list[a.defer_seg - 64u * (idx + 1u) + lane] : list[idx];
     if (e == ~0u) continue;  // a lane of a dense chunk whose pixel the certified pass settled
     Ray ray;
-    {
+    if constexpr (FB) {
       const FrameView fv = frame_view(a, e >> 29);
       c.time = fv.time;
       ray = primary_ray(a, fv.pv, c, int(e & 0xFFFFu), frame_row(a, int((e >> 16) & 0x1FFFu)));
+    } else {
+      ray = primary_ray(a, a.inv_pv, c, int(e & 0xFFFFu), frame_row(a, int(e >> 16)));
     }
     Counters k;
 #pragma unroll
@@ -2352,11 +2358,16 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     __shared__ float lstk[VRT_LDS_STACK ? kStackWords * 64 : 1];
     (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, 64>(a, c, ray, color, k, steps, flags,
                                                                     hit_vidx, hit_len, &lstk[lane]);
-    // the pixel and its frame re-derived from e (only e stays live across the exact path)
-    uint32_t e2 = e;
-    asm volatile("" : "+v"(e2));  // not CSE'd with the decode above (whose results would stay live)
-    store_pixel(a, frame_view(a, e2 >> 29), out, size_t((e2 >> 16) & 0x1FFFu) * size_t(a.pitch) + size_t(e2 & 0xFFFFu),
-                color);
+    if constexpr (FB) {
+      // the pixel and its frame re-derived from e (only e stays live across the exact path)
+      uint32_t e2 = e;
+      asm volatile("" : "+v"(e2));  // not CSE'd with the decode above (whose results would stay live)
+      store_pixel(a, frame_view(a, e2 >> 29), out,
+                  size_t((e2 >> 16) & 0x1FFFu) * size_t(a.pitch) + size_t(e2 & 0xFFFFu), color);
+    } else {
+      store_pixel(a, FrameView{a.inv_pv, a.time, a.cur, a.raw}, out,
+                  size_t(e >> 16) * size_t(a.pitch) + size_t(e & 0xFFFFu), color);
+    }
 #ifdef VRT_STAMPS
     xlanes += uint32_t(__builtin_popcountll(__ballot(true))) | (dense ? 0x10000u : 0u);
 #endif
@@ -2646,10 +2657,16 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
         g2(a.exact_grid ? a.exact_grid
                         : std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #endif
-    auto k1 = a.textured ? render_kernel<false, true, 2, false, true> : render_kernel<false, false, 2, false, true>;
+    // frame batches (a.nframes > 1): colour-only only (the host launches textured frames one by one)
+    const bool fb = a.nframes > 1;
+    auto k1 = a.textured ? render_kernel<false, true, 2, false, true>
+                         : (fb ? render_kernel<false, false, 2, false, true, true> : render_kernel<false, false, 2, false, true>);
     auto k2 = a.textured ? exact_pass_kernel<true, 1>
-                         : ((a.exact_fat || VRT_FORCE_FAT) ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>
-                                       : exact_pass_kernel<false, 2>);
+                         : ((a.exact_fat || VRT_FORCE_FAT)
+                                ? (fb ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT, true>
+                                      : exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>)
+                                : (fb ? exact_pass_kernel<false, 2, VRT_EXACT_WAVES, VRT_SPARSE_BATCH, true>
+                                      : exact_pass_kernel<false, 2>));
     if (ev_begin)
       hipExtLaunchKernelGGL(k1, g1, dim3(kWgThreads), 0, s, ev_begin, nullptr, 0, a, vox, out, hit, cnt_rep);
     else
@@ -2663,10 +2680,15 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
   auto kern = a.textured ? (stats ? render_kernel<true, true>
                                   : (a.cert >= 1 ? render_kernel<false, true, 1> : render_kernel<false, true>))
                          : (stats ? render_kernel<true, false>
-                                  : (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true>
-                                                            : render_kernel<false, false, 2>)
-                                     : a.cert == 1 ? render_kernel<false, false, 1>
-                                                   : render_kernel<false, false, 0>));
+                            : a.nframes > 1
+                                ? (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true, false, true>
+                                                          : render_kernel<false, false, 2, false, false, true>)
+                                   : a.cert == 1 ? render_kernel<false, false, 1, false, false, true>
+                                                 : render_kernel<false, false, 0, false, false, true>)
+                                : (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true>
+                                                          : render_kernel<false, false, 2>)
+                                   : a.cert == 1 ? render_kernel<false, false, 1>
+                                                 : render_kernel<false, false, 0>));
   if (ev_begin || ev_end)
     hipExtLaunchKernelGGL(kern, grid, dim3(kWgThreads), 0, s, ev_begin, ev_end, 0, a, vox, out, hit, cnt_rep);
   else

@@ -50,8 +50,8 @@ if passes:
     s = json.loads(summ)
     if "fetch_bytes" in s and "write_bytes" in s:
         out = {"config": a.config, "output": a.output,
-               "kernel": "one frame's launch: vrt::render_kernel<false, false, 2, false, true> (certified "
-                         "pass) + vrt::exact_pass_kernel<false, 2> (deferred exact pass), summed",
+               "kernel": "one frame's launch, its kernels summed: " + " + ".join(
+                   sorted(k for k in s.get("per_kernel", {}) if "render" in k or "exact" in k)),
                "source": f"profiles/{os.path.basename(dst)}/pmc (rocprofv3 --pmc FETCH_SIZE and --pmc "
                          "WRITE_SIZE in separate passes over bench.py --steps 5 --warmup 1 "
                          "--device-warmup-ms 0: one launch = one frame)",

@@ -97,13 +97,13 @@ for st in "$@"; do
           echo "drvab ${ln} ${dc:-C3} $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/drvab_${ln}_${dc:-C3}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/drvab_${ln}_${dc:-C3}_$i.log | head -1)"
         done
       done; unset VRT_LIB ;;
-    benchab)  # steady-state bench (STEPS frames), ROUNDS alternating rounds over base + variants: benchab:CFG,STEPS,ROUNDS
-      IFS=, read bc bs br <<< "$arg"
+    benchab)  # steady-state bench (STEPS frames), ROUNDS alternating rounds over base + variants: benchab:CFG,STEPS,ROUNDS[,FLAGS]
+      IFS=, read bc bs br bf <<< "$arg"
       for ((i = 1; i <= ${br:-2}; i++)); do
         for lib in $(libs); do
           ln=$(basename $lib .so)
           if [ $lib = base ]; then unset VRT_LIB; else export VRT_LIB=$ROOT/$lib; fi
-          TAILN=0 run benchab_${ln}_${bc}_$i 150 python bench.py --config $bc --steps ${bs:-500} --warmup 20 --cpu-seconds 0 --no-verify
+          TAILN=0 run benchab_${ln}_${bc}_$i 150 python bench.py --config $bc --steps ${bs:-500} --warmup 20 --cpu-seconds 0 --no-verify $bf
           echo "benchab ${ln} ${bc} $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1) $(grep -o '"kernel_ms": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1) $(grep -o '"frame_latency_ms": [0-9.]*' $OUT/benchab_${ln}_${bc}_$i.log | head -1)"
         done
       done; unset VRT_LIB ;;

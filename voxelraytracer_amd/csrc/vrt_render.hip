@@ -2239,7 +2239,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 #endif
 }
 
-#if (defined(VRT_SPARSE_BATCH) || defined(VRT_SPARSE_BATCH_FAT) || defined(VRT_EXACT_PRIO) || \
+#if (defined(VRT_SPARSE_BATCH) || defined(VRT_SPARSE_BATCH_FAT) || defined(VRT_SPARSE_BATCH_TEX) || defined(VRT_EXACT_PRIO) || \
      defined(VRT_FORCE_FAT)) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_SPARSE_BATCH / VRT_EXACT_PRIO / VRT_FORCE_FAT are A/B knobs of make variant builds"
 #endif
@@ -2252,6 +2252,9 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
 #ifndef VRT_SPARSE_BATCH
 #define VRT_SPARSE_BATCH 32
 #endif
+#ifndef VRT_SPARSE_BATCH_TEX  // the same for textured frames: 64 (many more sparse pixels, texel-edge
+#define VRT_SPARSE_BATCH_TEX 64  // hits: at 32 the extra waves cost textured C3 0.0572 -> 0.0661 ms, C4
+#endif                           // 0.2329 -> 0.2894; profiles/r05_s30)
 #ifndef VRT_SPARSE_BATCH_FAT  // the same in the exact pass's 4-wave instance (short bands)
 #define VRT_SPARSE_BATCH_FAT 16
 #endif
@@ -2661,7 +2664,7 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     const bool fb = a.nframes > 1;
     auto k1 = a.textured ? render_kernel<false, true, 2, false, true>
                          : (fb ? render_kernel<false, false, 2, false, true, true> : render_kernel<false, false, 2, false, true>);
-    auto k2 = a.textured ? exact_pass_kernel<true, 1>
+    auto k2 = a.textured ? exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX>
                          : ((a.exact_fat || VRT_FORCE_FAT)
                                 ? (fb ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT, true>
                                       : exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>)

@@ -264,8 +264,6 @@ def frame_batch(args, split: int) -> int:
         return args.batch
     if split <= 1 or args.alpha != 1.0 or args.output != "rgba8" or args.scaling != "strong":
         return 1
-    if args.shading != "color":   # the library launches textured frames one by one (C3 textured
-        return 1                  # 8-way band 0.0211 ms unbatched vs 0.0272; profiles/r05_s31)
     return min(8, split)
 
 

@@ -67,6 +67,27 @@ def test_batch_equals_single_frames(built, scene, n, w, h, R, T, nf, ranks, rank
         assert not all(np.array_equal(ref[0], x) for x in ref[1:])   # the frames do differ
 
 
+@pytest.mark.parametrize("ranks,rank", [(1, 0), (8, 2)])
+def test_textured_batch_equals_single_frames(built, ranks, rank):
+    """Textured frames (the reference's default build) in a batch: the textured frame-batch
+    instances, deferred exact pass and in lane."""
+    w, h, n, R, T, nf = 480, 270, 128, 4, 4, 4
+    block = 16 if ranks > 1 else 1
+    row0, rows, step = block_band_spec(rank, ranks, h, block) if ranks > 1 else (0, h, 1)
+    atlas = vrt.make_atlas()
+    cams = cameras(w, h, nf)
+    ps = [vrt.textured_params(p, atlas) for p in params_for(R, T, nf)]
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("refraction", n), n)
+        for mode in (1, 2, 0):
+            r.set_exact_pass(mode)
+            ref = singles(r, cams, ps, row0, rows, step, block)
+            for rep in range(2):
+                got = batched(r, cams, ps, row0, rows, step, block)
+                for f in range(nf):
+                    assert np.array_equal(got[f], ref[f]), f"mode {mode} rep {rep} frame {f}"
+
+
 def test_batch_argument_checks(built):
     w, h = 64, 32
     cams, ps = cameras(w, h, 2), params_for(4, 4, 2)

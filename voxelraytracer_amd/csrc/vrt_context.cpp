@@ -1517,10 +1517,7 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
   // a launch holds at most kOrderMaxTiles tiles (the tile order's and the deferred list's slot):
   // a larger batch is enqueued as consecutive launches of as many frames as fit
   const uint32_t ft = a.tiles;
-  // textured frames launch one by one (the kernels' frame-batch instances are colour-only)
-  const int per = a.textured ? 1
-                             : int(std::max<uint32_t>(1u, std::min<uint32_t>(uint32_t(nframes),
-                                                                              kOrderMaxTiles / std::max(ft, 1u))));
+  const int per = int(std::max<uint32_t>(1u, std::min<uint32_t>(uint32_t(nframes), kOrderMaxTiles / std::max(ft, 1u))));
   const vrt::KArgs all = a;
   for (int f0 = 0; f0 < nframes; f0 += per) {
     const int nf = std::min(per, nframes - f0);

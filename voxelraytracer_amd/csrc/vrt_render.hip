@@ -2662,11 +2662,12 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
         g2(a.exact_grid ? a.exact_grid
                         : std::max(64u, a.tiles * uint32_t(kWgWaves) / (a.textured ? kDeferGridDiv : kDeferGridDivColor)));
 #endif
-    // frame batches (a.nframes > 1): colour-only only (the host launches textured frames one by one)
+    // frame batches (a.nframes > 1): their own instances
     const bool fb = a.nframes > 1;
-    auto k1 = a.textured ? render_kernel<false, true, 2, false, true>
+    auto k1 = a.textured ? (fb ? render_kernel<false, true, 2, false, true, true> : render_kernel<false, true, 2, false, true>)
                          : (fb ? render_kernel<false, false, 2, false, true, true> : render_kernel<false, false, 2, false, true>);
-    auto k2 = a.textured ? exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX>
+    auto k2 = a.textured ? (fb ? exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX, true>
+                               : exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX>)
                          : ((a.exact_fat || VRT_FORCE_FAT)
                                 ? (fb ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT, true>
                                       : exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>)
@@ -2683,7 +2684,9 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     return;
   }
   auto kern = a.textured ? (stats ? render_kernel<true, true>
-                                  : (a.cert >= 1 ? render_kernel<false, true, 1> : render_kernel<false, true>))
+                            : a.nframes > 1 ? (a.cert >= 1 ? render_kernel<false, true, 1, false, false, true>
+                                                           : render_kernel<false, true, 0, false, false, true>)
+                                            : (a.cert >= 1 ? render_kernel<false, true, 1> : render_kernel<false, true>))
                          : (stats ? render_kernel<true, false>
                             : a.nframes > 1
                                 ? (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true, false, true>

@@ -65,31 +65,35 @@ def test_rgb8_wire_assembly_matches_rgba8(built, k, width, height, block):
     assert torch.equal(frame.cpu(), reference_frame(bands, k, height, block))
 
 
-@pytest.mark.parametrize("wire", ["rgb8", "rgba8"])
-def test_rank_comm_gather_one_rank(built, wire):
+@pytest.mark.parametrize("wire,batch", [("rgb8", 1), ("rgba8", 1), ("rgb8", 3)])
+def test_rank_comm_gather_one_rank(built, wire, batch):
+    """GatherLib per frame slot (frame batches: `batch` slots per lane, each gathered on its lane's
+    communicator and stream)."""
     import voxelraytracer_amd as vrt
     from voxelraytracer_amd.tiles import GatherLib
 
     w, h, block, lanes = 96, 40, 16, 2
+    slots = lanes * batch
     with vrt.Renderer(0) as ren:
         ex = GatherLib(ren, lanes, 1, 0, lambda ids, n: ids, wire=wire)   # one rank: the ids stay here
         st = [torch.cuda.Stream() for _ in range(lanes)]
-        bufs = [torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)]
+        bufs = [torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(slots)]
         for b in bufs:
             b[..., 3] = 255   # rendered RGBA8 words: A = 255
         tiler = types.SimpleNamespace(
             width=w, height=h, channels=4, dtype=torch.uint8, world=1, rank=0, rmax=h, row_block=block,
-            lanes=lanes, slots=lanes, batch=1, bufs=bufs, part_streams=[[s] for s in st],
-            gathered=[torch.zeros((1, h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)],
-            frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda") for _ in range(lanes)])
-        for lane in range(lanes):
-            ex.run(tiler, lane)
+            lanes=lanes, slots=slots, batch=batch, bufs=bufs, part_streams=[[s] for s in st],
+            gathered=[torch.zeros((1, h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(slots)],
+            frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda") for _ in range(slots)])
+        for slot in range(slots):
+            ex.run(tiler, slot)
         torch.cuda.synchronize()
         assert ex.rgb8 == (wire == "rgb8")
-        for lane in range(lanes):
+        assert [a[-1] for a in ex.args] == [(g // batch) % lanes for g in range(slots)]   # lane communicators
+        for slot in range(slots):
             if not ex.rgb8:
-                assert torch.equal(tiler.gathered[lane][0], bufs[lane])  # ncclGather of one rank
-            assert torch.equal(tiler.frames[lane][:h], bufs[lane])       # assembly of one band
+                assert torch.equal(tiler.gathered[slot][0], bufs[slot])  # ncclGather of one rank
+            assert torch.equal(tiler.frames[slot][:h], bufs[slot])       # assembly of one band
         with pytest.raises(vrt.VrtError):
             ren.gather_band_async(lanes, bufs[0].data_ptr(), bufs[0].numel(), 0, 0)  # no such comm
         with pytest.raises(vrt.VrtError):   # joined once per context

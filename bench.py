@@ -130,6 +130,10 @@ def parse():
                     help="frames per launch of a rank's band (vrt_render_temporal_batch_async, "
                          "alpha 1): 0 automatic, min(8, K) for a K-way split (each launch then has "
                          "about a whole frame's waves), 1 off")
+    ap.add_argument("--rehearse-gather", action="store_true",
+                    help="with --rehearse-ranks K --rehearse-rank 0: also do rank 0's local share of the "
+                         "per-frame gather (pack its band to RGB8, assemble the K bands into the frame) "
+                         "on each frame's lane stream, as the N > 1 run does after its ncclGather")
     ap.add_argument("--row-block", type=int, default=0,
                     help="rows per block of a rank's band (vrt_render_*_blocks_pitched_async, ABI "
                          "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 16 for a "
@@ -404,6 +408,12 @@ def main():
     # equal; profiles/r03_s54)
     row_block = args.row_block or (16 if split and parts == 1 else 1)
     exchange = None
+    if args.rehearse_gather:
+        if not rehearse or args.rehearse_rank != 0 or not rgba8:
+            raise SystemExit("--rehearse-gather rehearses rank 0 of a split with RGBA8 output")
+        from voxelraytracer_amd.tiles import GatherRehearsal
+
+        exchange = GatherRehearsal(ren, lanes)
     if gather:   # the per-frame exchange: the library's RCCL path, or torch (gloo rehearsal)
         from voxelraytracer_amd.tiles import GatherLib, GatherTorch
 
@@ -412,7 +422,7 @@ def main():
     tiler = FrameTiler(w, frame_h, render_band, dev, world=rehearse or None,
                        rank=args.rehearse_rank if rehearse else None,
                        dtype=torch.uint8 if rgba8 else torch.float32, parts=parts,
-                       gather=gather, lanes=lanes,
+                       gather=gather or args.rehearse_gather, lanes=lanes,
                        independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs,
                        row_block=row_block, exchange=exchange, batch=batch,
                        launch_batch=launch_batch if batch > 1 else None)
@@ -530,7 +540,8 @@ def main():
         ro_el, ro_gpu, _ = timed_frames(args.steps)
         tiler.exchange_on = True
         t_ro = torch.tensor([ro_el, ro_gpu], dtype=torch.float64, device=dev)
-        dist.all_reduce(t_ro, op=dist.ReduceOp.MAX)
+        if world > 1:
+            dist.all_reduce(t_ro, op=dist.ReduceOp.MAX)
         ro_el, ro_gpu = t_ro.tolist()
         render_only = {"value": round(rays_per_frame * args.steps / ro_el / 1e6, 3),
                        "ms_per_step": round(ro_el / args.steps * 1e3, 4),
@@ -632,7 +643,7 @@ def main():
                 torch.cuda.synchronize(dev)
                 bad += int((got != ref).sum().item())
                 total += got.numel()
-            if tiler.gather:
+            if tiler.gather and world > 1:
                 full = tiler.collect()
                 torch.cuda.synchronize(dev)
                 if rank == 0:
@@ -646,7 +657,7 @@ def main():
         if gather_bad is not None:
             verify["gathered_frame_mismatched_elements"] = gather_bad
         seq_ok = True
-        if tiler.gather:
+        if tiler.gather and world > 1:
             # every rank enqueued lane g's gather for the same frames, in the same order per lane
             # communicator (a mismatch would pair different frames' bands, or hang)
             xl = torch.tensor(tiler.exchange_log(), dtype=torch.int64, device=dev)
@@ -678,9 +689,12 @@ def main():
 
     band_kind = (f"block-cyclic bands of {row_block}-row blocks" if row_block > 1 else
                  "cyclic row bands")
-    gather_how = ("RCCL ncclGather over xGMI, one communicator per lane, library assembly kernel"
-                  if isinstance(tiler.exchange, GatherLib) else "torch.distributed gather, "
-                  f"{args.backend} backend") if tiler.gather else None
+    gather_how = (("REHEARSAL of rank 0's local share: its band packed to RGB8 and the K bands "
+                   "assembled into the frame per frame, no collective (one GPU)")
+                  if args.rehearse_gather else
+                  ("RCCL ncclGather over xGMI, one communicator per lane, library assembly kernel"
+                   if isinstance(tiler.exchange, GatherLib) else "torch.distributed gather, "
+                   f"{args.backend} backend") if tiler.gather else None)
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = rays_per_frame * args.steps / elapsed / 1e6
@@ -802,6 +816,7 @@ def main():
                                 (f"REHEARSAL on one GPU: only rank {args.rehearse_rank}'s band "
                                  f"({band_kind}) of a {rehearse}-way strong split is rendered and "
                                  "timed; rays counted over the whole frame"
+                                 + (f"; with {gather_how}" if args.rehearse_gather else "")
                                  if rehearse else "single GPU, whole frame"))
                                + (f", {batch} frames per launch (frame batches: each launch renders the "
                                   f"band of {batch} consecutive frames, vrt_render_temporal_batch_async)"

@@ -2486,9 +2486,8 @@ __global__ void __launch_bounds__(256) pack_rgb8_kernel(const uint4* __restrict_
   for (uint64_t q = uint64_t(blockIdx.x) * 256 + threadIdx.x; q < quads; q += uint64_t(gridDim.x) * 256) {
     const uint4 p = rgba[q];
     const uint32_t a = p.x & 0xFFFFFFu, b = p.y & 0xFFFFFFu, c = p.z & 0xFFFFFFu, d = p.w & 0xFFFFFFu;
-    rgb[3 * q + 0] = a | (b << 24);
-    rgb[3 * q + 1] = (b >> 8) | (c << 16);
-    rgb[3 * q + 2] = (c >> 16) | (d << 8);
+    // one 12-byte store per work-item (a wave writes 768 contiguous bytes per instruction)
+    reinterpret_cast<uint3*>(rgb)[q] = make_uint3(a | (b << 24), (b >> 8) | (c << 16), (c >> 16) | (d << 8));
   }
 }
 
@@ -2505,7 +2504,8 @@ __global__ void __launch_bounds__(256) assemble_blocks_rgb8_kernel(const uint32_
   const uint32_t* src = bands + (uint64_t(j) * band_px + bi * uint64_t(width)) * 3u / 4u;
   uint4* dst = frame + uint64_t(y) * frame_pitch / 4u;
   for (uint32_t x = threadIdx.x; x < uint32_t(width) / 4u; x += 256u) {
-    const uint32_t u = src[3 * x], v = src[3 * x + 1], w = src[3 * x + 2];
+    const uint3 t = reinterpret_cast<const uint3*>(src)[x];  // one 12-byte load (768 B per wave)
+    const uint32_t u = t.x, v = t.y, w = t.z;
     dst[x] = make_uint4(0xFF000000u | (u & 0xFFFFFFu), 0xFF000000u | (u >> 24) | ((v & 0xFFFFu) << 8),
                         0xFF000000u | (v >> 16) | ((w & 0xFFu) << 16), 0xFF000000u | (w >> 8));
   }

@@ -204,6 +204,29 @@ class GatherLib:
                                            tiler.row_block, frame, self.words, st)
 
 
+class GatherRehearsal(GatherLib):
+    """Rank 0's local share of the per-frame exchange, for a one-GPU rehearsal of rank 0 of a
+    K-way split (bench.py --rehearse-gather): every frame's own band is packed to the RGB8 wire
+    format and the K gathered bands are assembled into the frame (vrt_assemble_blocks_rgb8_async)
+    on the frame's lane stream, exactly as GatherLib does after its ncclGather; the collective
+    itself (the other ranks' bands arriving over xGMI) is not rehearsed, so the gathered buffer
+    holds whatever it held. What it times: the packing and assembly work rank 0 adds to its own
+    rendering."""
+
+    def __init__(self, renderer, lanes: int):
+        self.ren, self.lanes, self.wire, self.args = renderer, lanes, "rgb8", None
+
+    def run(self, tiler, slot: int) -> None:
+        if self.args is None:
+            self._setup(tiler)
+        band, px, packed, gath, frame, st, _ = self.args[slot]
+        if not self.rgb8:
+            raise ValueError("the gather rehearsal is for RGBA8 bands (RGB8 wire)")
+        self.ren.pack_rgb8_async(band, px, packed, st)
+        self.ren.assemble_blocks_rgb8_async(gath, tiler.world, tiler.rmax, tiler.width, tiler.height,
+                                            tiler.row_block, frame, tiler.width, st)
+
+
 class FrameTiler:
     """Renders a sequence of frames across `world` ranks, `parts` streams per lane, `lanes`
     frames in flight per rank.
@@ -245,8 +268,9 @@ class FrameTiler:
         # `world`-way split on one GPU; no exchange may then be requested)
         self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
-        if world is not None and gather:
-            raise ValueError("a rehearsed split keeps its band (gather=False)")
+        if world is not None and gather and not (isinstance(exchange, GatherRehearsal) and rank == 0):
+            raise ValueError("a rehearsed split keeps its band (gather=False), except rank 0 with "
+                             "GatherRehearsal (its local share of the exchange)")
         if lanes < 1:
             raise ValueError("lanes >= 1")
         if batch < 1 or (batch > 1 and (not independent or parts != 1 or launch_batch is None)):

@@ -134,6 +134,10 @@ def parse():
                     help="with --rehearse-ranks K --rehearse-rank 0: also do rank 0's local share of the "
                          "per-frame gather (pack its band to RGB8, assemble the K bands into the frame) "
                          "on each frame's lane stream, as the N > 1 run does after its ncclGather")
+    ap.add_argument("--compositor", type=int, default=0, choices=[-1, 0, 1],
+                    help="with the per-frame gather (or --rehearse-gather): rank 0 renders no band, "
+                         "ranks 1..N-1 split every frame and rank 0 receives and assembles it "
+                         "(tiles.split_band_spec); 0 automatic (N >= 4 with the gather), 1 on, -1 off")
     ap.add_argument("--row-block", type=int, default=0,
                     help="rows per block of a rank's band (vrt_render_*_blocks_pitched_async, ABI "
                          "v11): rank r renders blocks r, r+N, ... of B adjacent rows; 0: 16 for a "
@@ -249,6 +253,8 @@ def pipeline_shape(args, world: int):
     _, _, w, h, _, _, _ = CONFIGS[args.config]
     frame_h = h * world if args.scaling == "weak" else h
     split = max(world, args.rehearse_ranks if world == 1 else 1)
+    if compositor_on(args, world):
+        split -= 1   # the renderers' split (rank 0 renders nothing)
     rows = -(-frame_h // split)
     waves = -(-w // 8) * -(-rows // 8)
     independent = args.alpha == 1.0
@@ -257,6 +263,19 @@ def pipeline_shape(args, world: int):
     lanes = args.lanes or ((8 if small else 4) if independent else 1)
     queues = args.queues or (8 if small and lanes == 8 else 4)
     return lanes, queues, batch
+
+
+def compositor_on(args, world: int) -> bool:
+    """Whether rank 0 is a compositor (renders no band; tiles.split_band_spec). Automatic with the
+    per-frame gather from 4 ranks: rank 0's share of the exchange (its receive and the assembly of
+    every frame) is then worth about one band's render, so rank 0 with a band of its own is the
+    slowest rank."""
+    if args.compositor == -1:
+        return False
+    gathered = (world > 1 and not args.no_gather) or (world == 1 and args.rehearse_gather)
+    if args.compositor == 1:
+        return gathered
+    return gathered and world >= 4
 
 
 def frame_batch(args, split: int) -> int:
@@ -407,6 +426,9 @@ def main():
     # neighbours in the band are adjacent too (16 vs 8 rows: C4 k = 8 -3 %, C3 k = 4 -5 %, others
     # equal; profiles/r03_s54)
     row_block = args.row_block or (16 if split and parts == 1 else 1)
+    compositor = compositor_on(args, world)
+    if compositor and (max(world, rehearse) < 3 or row_block < 2 and not gather):
+        raise SystemExit("--compositor needs a gathered split of at least 3 ranks")
     exchange = None
     if args.rehearse_gather:
         if not rehearse or args.rehearse_rank != 0 or not rgba8:
@@ -425,7 +447,7 @@ def main():
                        gather=gather or args.rehearse_gather, lanes=lanes,
                        independent=rgba8 and args.alpha == 1.0 or not rgba8, launch=launch_ptrs,
                        row_block=row_block, exchange=exchange, batch=batch,
-                       launch_batch=launch_batch if batch > 1 else None)
+                       launch_batch=launch_batch if batch > 1 else None, compositor=compositor)
 
     # One counted launch per part (outside the timed region, the exact STATS instance): rays and
     # algorithmic bytes per frame and per launch.
@@ -434,14 +456,17 @@ def main():
     own = None
     count_specs = tiler.specs
     if rehearse:   # the whole frame's rays: every rank's parts of the rehearsed split, own first
-        from voxelraytracer_amd.tiles import block_band_spec, part_spec
+        from voxelraytracer_amd.tiles import part_spec, split_band_spec
         order = [args.rehearse_rank] + [r_ for r_ in range(rehearse) if r_ != args.rehearse_rank]
-        count_specs = ([block_band_spec(r_, rehearse, frame_h, row_block) for r_ in order]
+        count_specs = ([split_band_spec(r_, rehearse, frame_h, row_block, compositor) for r_ in order]
                        if row_block > 1 else
                        [part_spec(r_, rehearse, s_, parts, frame_h) for r_ in order
                         for s_ in range(parts)])
     own_cnt = torch.zeros_like(cnt)
     for i_, (row0, rows, step) in enumerate(count_specs):
+        if rows == 0:   # a compositor rank 0: no band
+            part_bytes.append(0)
+            continue
         pc = torch.zeros_like(cnt)
         scratch = torch.zeros((rows, w, 4), dtype=torch.uint8 if rgba8 else torch.float32, device=dev)
         launch(row0, rows, step, scratch, scratch, pc.data_ptr(), row_block)
@@ -562,6 +587,15 @@ def main():
     lt_total, lt_n = ren.launch_timing()
     ren.set_launch_timing(0)
     launch_ms = lt_total / max(lt_n, 1)
+    # a compositor rank 0 launches no render: the roofline fields are renderer rank 1's
+    own_bytes = vrt.algorithmic_bytes(own, 8 if rgba8 else 16)
+    bytes_per_launch = float(np.mean(part_bytes)) * batch   # a launch renders `batch` frames
+    renderer_gpu_ms = frame_gpu_ms
+    if compositor and world > 1:
+        t_r = torch.tensor([launch_ms, bytes_per_launch, own_bytes, frame_gpu_ms], dtype=torch.float64,
+                           device=dev)
+        dist.broadcast(t_r, 1)
+        launch_ms, bytes_per_launch, own_bytes, renderer_gpu_ms = t_r.tolist()
     t = torch.tensor([elapsed, frame_gpu_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -636,6 +670,8 @@ def main():
             tiler.finish()
             torch.cuda.synchronize(dev)
             for s_, (row0, rows, step) in enumerate(tiler.specs):
+                if rows == 0:   # a compositor rank 0: no band
+                    continue
                 got = last_parts()[s_].contiguous()
                 ref = torch.zeros_like(got)
                 prev_c = prev_parts[s_].contiguous()
@@ -689,8 +725,12 @@ def main():
 
     band_kind = (f"block-cyclic bands of {row_block}-row blocks" if row_block > 1 else
                  "cyclic row bands")
-    gather_how = (("REHEARSAL of rank 0's local share: its band packed to RGB8 and the K bands "
-                   "assembled into the frame per frame, no collective (one GPU)")
+    if compositor:
+        band_kind += (" over ranks 1..N-1 (rank 0 renders nothing: it receives and assembles every "
+                      "frame, tiles.split_band_spec)")
+    gather_how = (("REHEARSAL of rank 0's local share: " + ("the K-1 renderers' bands" if compositor else
+                                                             "its band packed to RGB8 and the K bands")
+                   + " assembled into the frame per frame, no collective (one GPU)")
                   if args.rehearse_gather else
                   ("RCCL ncclGather over xGMI, one communicator per lane, library assembly kernel"
                    if isinstance(tiler.exchange, GatherLib) else "torch.distributed gather, "
@@ -715,11 +755,10 @@ def main():
         # reports per kernel): this rank's bytes of one launch over the mean launch duration. With
         # frames in flight, launches overlap (launches_in_flight on average), so the GPU's rate is
         # the per-launch rate times that: this rank's bytes per frame / GPU time per frame.
-        own_bytes = vrt.algorithmic_bytes(own, pixel_bytes)
-        bytes_per_launch = float(np.mean(part_bytes)) * batch   # a launch renders `batch` frames
-        per_launch = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        in_flight = launch_ms * parts / (frame_gpu_ms * batch)
-        achieved = own_bytes / (frame_gpu_ms * 1e-3) / 1e9
+        # (a compositor rank 0 alone, in a rehearsal, has no launch: no per-launch rate)
+        per_launch = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+        in_flight = launch_ms * parts / (renderer_gpu_ms * batch)
+        achieved = own_bytes / (renderer_gpu_ms * 1e-3) / 1e9
         lib_hash = lib_sha256()
         traffic = traffic_frame = hbm_frac = None
         valu = None
@@ -869,6 +908,9 @@ def main():
                                  "the latest end event of the lane streams around the K timed "
                                  "frames / K (with fill and drain of the pipeline)"),
                 "kernel_ms_max_over_ranks": round(frame_ms_max, 4),
+                "rank": (1 if compositor and world > 1 else rank),
+                "rank_is": ("the rank the per-launch fields describe (a compositor rank 0 renders "
+                            "nothing: renderer rank 1's launches)"),
                 "valu_issue": valu,
                 "lib_sha256": lib_hash[:16],
                 "profile": prof_note,
@@ -877,6 +919,7 @@ def main():
             "gather": (None if world == 1 else
                        {"per_frame": tiler.gather, "how": gather_how,
                         "band_rows_padded": getattr(tiler, "rmax", None),
+                        "compositor": compositor,
                         "bytes_to_rank0_per_frame": (
                             (tiler.exchange.bytes_per_rank(tiler) if isinstance(tiler.exchange, GatherLib)
                              else tiler.rmax * w * (4 if rgba8 else 16)) * (world - 1)

@@ -34,6 +34,15 @@ def test_bench_two_ranks_json(built, scaling, gather):
     two_ranks(scaling, gather, ["--backend", "gloo", "--same-device"])
 
 
+def test_bench_compositor_three_ranks(built):
+    """--compositor 1 with three ranks on cuda:0 (gloo): rank 0 renders nothing, ranks 1 and 2
+    split every frame (tiles.split_band_spec) and rank 0 assembles it; the gathered frames are
+    checked against collect() and the roofline fields are renderer rank 1's."""
+    out = two_ranks("strong", True, ["--backend", "gloo", "--same-device", "--compositor", "1"], n=3)
+    assert out["gather"]["compositor"] is True and "rank 0 renders nothing" in out["config"]["parallelism"]
+    assert out["roofline"]["rank"] == 1 and out["roofline"]["launch_ms"] > 0
+
+
 def _device_count():
     import torch
     return torch.cuda.device_count()   # counts devices without initialising HIP in this process
@@ -47,10 +56,10 @@ def test_bench_two_ranks_rccl(built, gather):
     two_ranks("strong", gather, [])
 
 
-def two_ranks(scaling, gather, backend_args):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+def two_ranks(scaling, gather, backend_args, n=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "6", "--warmup", "2",
            "--scaling", scaling, "--cpu-seconds", "0", "--watchdog-s", "100"] + backend_args
     cmd += [] if gather else ["--no-gather"]
     env = dict(os.environ, OMP_NUM_THREADS="4")
@@ -66,7 +75,7 @@ def two_ranks(scaling, gather, backend_args):
         time.sleep(3)
         os.killpg(p.pid, signal.SIGKILL)
         out_s, err_s = p.communicate()
-        pytest.fail("two-rank bench did not finish in 150 s; rank stacks:\n" + err_s[-20000:])
+        pytest.fail(f"{n}-rank bench did not finish in 150 s; rank stacks:\n" + err_s[-20000:])
     r = subprocess.CompletedProcess(cmd, p.returncode, out_s, err_s)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -76,14 +85,14 @@ def two_ranks(scaling, gather, backend_args):
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline",
               "cpu_baseline", "latency", "gather"):
         assert k in out, k
-    assert out["n_gpus"] == 2 and out["steps"] == 6 and out["scaling"] == scaling
+    assert out["n_gpus"] == n and out["steps"] == 6 and out["scaling"] == scaling
     assert out["value"] > 0 and out["ms_per_step"] > 0
-    assert out["config"]["frame"].startswith("1920x2160" if scaling == "weak" else "1920x1080")
+    assert out["config"]["frame"].startswith(f"1920x{1080 * n}" if scaling == "weak" else "1920x1080")
     assert out["roofline"]["kernel_ms_max_over_ranks"] >= out["roofline"]["kernel_ms"]
     assert out["cpu_baseline"] is None        # rank 0 at N=1 only
     assert out["verified"] is True
     assert out["latency"]["frame_latency_ms"] > 0
-    rows = 2160 if scaling == "weak" else 1080
+    rows = 1080 * n if scaling == "weak" else 1080
     if gather:   # every timed frame gathered and assembled on rank 0, checked against collect()
         assert out["collect"] is None and "every frame" in out["config"]["parallelism"]
         assert out["gather"]["per_frame"] is True and out["gather"]["render_only"]["value"] > 0
@@ -94,6 +103,7 @@ def two_ranks(scaling, gather, backend_args):
         ro = out["gather"]["render_only"]
         assert ro["ms_per_step"] > 0 and ro["kernel_ms_max_over_ranks"] > 0
         bpp = 3 if (out["gather"]["wire"] or "").startswith("RGB8") else 4   # RCCL: RGB8 wire
-        assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * bpp
+        assert out["gather"]["bytes_to_rank0_per_frame"] == out["gather"]["band_rows_padded"] * 1920 * bpp * (n - 1)
     else:   # one gather of the last frame after the timed region
         assert out["collect"]["rows"] == rows and out["collect"]["bytes"] == rows * 1920 * 4
+    return out

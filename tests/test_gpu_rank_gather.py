@@ -82,7 +82,7 @@ def test_rank_comm_gather_one_rank(built, wire, batch):
             b[..., 3] = 255   # rendered RGBA8 words: A = 255
         tiler = types.SimpleNamespace(
             width=w, height=h, channels=4, dtype=torch.uint8, world=1, rank=0, rmax=h, row_block=block,
-            lanes=lanes, slots=slots, batch=batch, bufs=bufs, part_streams=[[s] for s in st],
+            lanes=lanes, slots=slots, batch=batch, bufs=bufs, part_streams=[[s] for s in st], compositor=False,
             gathered=[torch.zeros((1, h, w, 4), dtype=torch.uint8, device="cuda") for _ in range(slots)],
             frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda") for _ in range(slots)])
         for slot in range(slots):
@@ -98,3 +98,31 @@ def test_rank_comm_gather_one_rank(built, wire, batch):
             ren.gather_band_async(lanes, bufs[0].data_ptr(), bufs[0].numel(), 0, 0)  # no such comm
         with pytest.raises(vrt.VrtError):   # joined once per context
             ren.comm_join([vrt.comm_unique_id()], 1, 0)
+
+
+def test_compositor_assembly_skips_rank0_chunk(built):
+    """A compositor rank 0 (tiles.split_band_spec): the gathered buffer's chunk 0 is rank 0's
+    unused send; the frame is assembled from chunks 1..K-1 as a (K-1)-way block-cyclic split
+    (GatherRehearsal runs GatherLib's assembly without the collective)."""
+    import voxelraytracer_amd as vrt
+    from voxelraytracer_amd.tiles import GatherRehearsal
+
+    k, w, h, block = 4, 96, 70, 16
+    plan, cap = vrt.block_band_plan(h, k - 1, block)
+    g = torch.Generator().manual_seed(11)
+    bands = torch.randint(0, 256, (k - 1, cap, w, 4), dtype=torch.uint8, generator=g)
+    bands[..., 3] = 255
+    gpacked = torch.cat([torch.full((1, cap, w, 3), 9, dtype=torch.uint8), bands[..., :3]]).reshape(-1).cuda()
+    with vrt.Renderer(0) as ren:
+        ex = GatherRehearsal(ren, 1)
+        st = torch.cuda.Stream()
+        tiler = types.SimpleNamespace(
+            width=w, height=h, channels=4, dtype=torch.uint8, world=k, rank=0, rmax=cap, row_block=block,
+            lanes=1, slots=1, batch=1, compositor=True, part_streams=[[st]],
+            bufs=[torch.zeros((cap, w, 4), dtype=torch.uint8, device="cuda")],
+            gathered=[None], frames=[torch.zeros((h + 1, w, 4), dtype=torch.uint8, device="cuda")])
+        ex._setup(tiler)
+        ex.gpacked[0].copy_(gpacked)
+        ex.run(tiler, 0)
+        torch.cuda.synchronize()
+    assert torch.equal(tiler.frames[0][:h].cpu(), reference_frame(bands, k - 1, h, block))

@@ -25,7 +25,7 @@ def free_port():
 
 
 def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1, gather=True,
-           lanes=1, row_block=1):
+           lanes=1, row_block=1, compositor=False):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -59,7 +59,7 @@ def worker(rank, world, port, n, w, h, frames, q, mode="f32", alpha=0.5, parts=1
 
     tiler = FrameTiler(w, h, render_band, torch.device("cpu"),
                        dtype=torch.uint8 if mode == "rgba8" else torch.float32, parts=parts,
-                       gather=gather, lanes=lanes, row_block=row_block)
+                       gather=gather, lanes=lanes, row_block=row_block, compositor=compositor)
     got = []
     for _ in range(frames):
         f = tiler.frame()
@@ -326,6 +326,57 @@ def test_block_band_spec_covers_the_frame():
         assert max(sp[1] for sp in specs) - min(sp[1] for sp in specs) <= b
     with pytest.raises(ValueError):
         block_band_spec(0, 2, 16, 3)
+
+
+def test_split_band_spec_compositor():
+    """The compositor split (bench.py --compositor): rank 0 renders no row, ranks 1..K-1 hold the
+    (K-1)-way block-cyclic split; without it, block_band_spec."""
+    from voxelraytracer_amd.tiles import band_frame_rows, block_band_spec, split_band_spec
+
+    assert split_band_spec(2, 4, 1080, 16) == block_band_spec(2, 4, 1080, 16)
+    for h, world, b in [(1080, 8, 16), (2160, 4, 16), (21, 3, 4), (18, 4, 1)]:
+        specs = [split_band_spec(r, world, h, b, True) for r in range(world)]
+        assert specs[0][1] == 0
+        assert specs[1:] == [block_band_spec(r - 1, world - 1, h, b) for r in range(1, world)]
+        rows = torch.cat([band_frame_rows(*sp, b) for sp in specs])
+        assert sorted(rows.tolist()) == list(range(h)), (h, world, b)
+    with pytest.raises(ValueError):
+        split_band_spec(0, 2, 16, 4, True)
+
+
+@pytest.mark.parametrize("world,lanes,row_block,mode", [(3, 2, 4, "f32"), (4, 1, 1, "f32"),
+                                                        (3, 2, 2, "rgba8")])
+def test_compositor_frames_match_single_process(built, world, lanes, row_block, mode):
+    """Gathered frames with a compositor rank 0 (it renders nothing; ranks 1..K-1 split the frame,
+    rank 0 assembles every frame): float frames, and the RGBA8 temporal sequence with dependent
+    lanes (each renderer's history is its own band), equal the single-process frames bit for bit."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h, frames, alpha = 16, 24, 18, 3, 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, w, h, frames, q, mode, alpha,
+                                              1, True, lanes, row_block, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, _ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    hist = np.zeros((h, w, 4), np.uint8)
+    assert len(got) == frames
+    for t in range(frames):
+        ref, _, _ = oracle.render(cam, vox, n, vrt.default_params(1, 2, time=float(t + 1),
+                                                                  ray_noise=0.05))
+        if mode == "rgba8":
+            _, hist = oracle.temporal(ref, hist, alpha)
+            assert np.array_equal(got[t], hist), t
+        else:
+            assert np.array_equal(got[t].view(np.uint32), ref.view(np.uint32)), t
 
 
 @pytest.mark.parametrize("world,h,row_block,lanes", [(2, 16, 8, 2), (3, 21, 4, 2)])

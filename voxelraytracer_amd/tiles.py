@@ -70,6 +70,22 @@ def block_band_spec(rank: int, world: int, height: int, block: int):
     return rank * block, rows, world * block
 
 
+def split_band_spec(rank: int, world: int, height: int, block: int, compositor: bool = False):
+    """(row0, rows, row_step) of rank's band of the frame split. compositor=False: block_band_spec
+    over all `world` ranks. compositor=True (world >= 3): rank 0 renders no rows — it receives and
+    assembles every frame — and ranks 1..world-1 split the frame block-cyclically among themselves
+    (rank r renders renderer r - 1's band of a (world - 1)-way split): with every frame gathered,
+    rank 0's exchange share (packing, the collective, the assembly of the whole frame) is worth
+    about one 8-way C3 band's render."""
+    if not compositor:
+        return block_band_spec(rank, world, height, block)
+    if world < 3:
+        raise ValueError("a compositor rank needs at least two renderers")
+    if rank == 0:
+        return 0, 0, (world - 1) * block
+    return block_band_spec(rank - 1, world - 1, height, block)
+
+
 def band_frame_rows(row0: int, rows: int, row_step: int, block: int = 1) -> torch.Tensor:
     """Frame row of every band row of a (block-)cyclic band, as an int64 index tensor."""
     i = torch.arange(rows, dtype=torch.int64)
@@ -191,17 +207,23 @@ class GatherLib:
         if self.args is None:
             self._setup(tiler)
         band, px, packed, gath, frame, st, comm = self.args[slot]
+        # a compositor rank 0 renders no rows: its chunk of the gather is not packed and not
+        # assembled (the bands of ranks 1.. start one padded band into the gathered buffer)
+        nb = tiler.world - 1 if tiler.compositor else tiler.world
         if self.rgb8:
-            self.ren.pack_rgb8_async(band, px, packed, st)
+            if not (tiler.compositor and tiler.rank == 0):
+                self.ren.pack_rgb8_async(band, px, packed, st)
             self.ren.gather_band_async(comm, packed, px * 3, gath, st)
             if tiler.rank == 0:
-                self.ren.assemble_blocks_rgb8_async(gath, tiler.world, tiler.rmax, tiler.width, tiler.height,
+                g0 = gath + (px * 3 if tiler.compositor else 0)
+                self.ren.assemble_blocks_rgb8_async(g0, nb, tiler.rmax, tiler.width, tiler.height,
                                                     tiler.row_block, frame, tiler.width, st)
             return
-        self.ren.gather_band_async(comm, band, px * tiler.channels * tiler.dtype.itemsize, gath, st)
+        bb = px * tiler.channels * tiler.dtype.itemsize
+        self.ren.gather_band_async(comm, band, bb, gath, st)
         if tiler.rank == 0:
-            self.ren.assemble_blocks_async(gath, tiler.world, tiler.rmax, self.words, tiler.height,
-                                           tiler.row_block, frame, self.words, st)
+            self.ren.assemble_blocks_async(gath + (bb if tiler.compositor else 0), nb, tiler.rmax, self.words,
+                                           tiler.height, tiler.row_block, frame, self.words, st)
 
 
 class GatherRehearsal(GatherLib):
@@ -222,9 +244,11 @@ class GatherRehearsal(GatherLib):
         band, px, packed, gath, frame, st, _ = self.args[slot]
         if not self.rgb8:
             raise ValueError("the gather rehearsal is for RGBA8 bands (RGB8 wire)")
-        self.ren.pack_rgb8_async(band, px, packed, st)
-        self.ren.assemble_blocks_rgb8_async(gath, tiler.world, tiler.rmax, tiler.width, tiler.height,
-                                            tiler.row_block, frame, tiler.width, st)
+        nb = tiler.world - 1 if tiler.compositor else tiler.world
+        if not tiler.compositor:
+            self.ren.pack_rgb8_async(band, px, packed, st)
+        self.ren.assemble_blocks_rgb8_async(gath + (px * 3 if tiler.compositor else 0), nb, tiler.rmax,
+                                            tiler.width, tiler.height, tiler.row_block, frame, tiler.width, st)
 
 
 class FrameTiler:
@@ -245,6 +269,8 @@ class FrameTiler:
     rank 0 (complete once that stream is synchronised) and None elsewhere. A returned band or
     frame stays valid until `lanes` more frames are enqueued. finish() makes the current stream
     wait for every frame enqueued so far and returns the last frame (rank 0 with gather) or band.
+    compositor=True (gathered block-cyclic bands, world >= 3): rank 0 renders no band — every
+    frame is split over ranks 1..world-1 (split_band_spec) and rank 0 only receives and assembles.
     independent=True declares that render_band does not read `prev` (u_Alpha = 1): frames on
     different lanes are then not ordered at all.
     launch (optional, CUDA): the lean form of render_band, launch(row0, rows, row_step,
@@ -263,7 +289,8 @@ class FrameTiler:
                  channels: int = 4, dtype=torch.float32, parts: int = 1, gather: bool = True,
                  lanes: int = 1, independent: bool = False, launch: Optional[Callable] = None,
                  world: Optional[int] = None, rank: Optional[int] = None, row_block: int = 1,
-                 exchange=None, batch: int = 1, launch_batch: Optional[Callable] = None):
+                 exchange=None, batch: int = 1, launch_batch: Optional[Callable] = None,
+                 compositor: bool = False):
         # world / rank: override the process group's (one process rehearsing rank `rank` of a
         # `world`-way split on one GPU; no exchange may then be requested)
         self.world = world or (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -282,11 +309,16 @@ class FrameTiler:
         self.width, self.height, self.parts = width, height, parts
         self.row_block = row_block
         self.gather = gather and self.world > 1
+        # split_band_spec's compositor split: rank 0 renders nothing and assembles the frames
+        self.compositor = compositor
+        if compositor and not (row_block > 1 or self.gather):
+            raise ValueError("the compositor split is a block-cyclic split")
         if row_block > 1 or self.gather:
             # block-cyclic band (row_block 1: cyclic rows), one part per lane; bands may be unequal
             if parts != 1:
                 raise ValueError("block-cyclic and gathered bands are one part per lane (parts=1)")
-            self.row0, self.rows, self.step = block_band_spec(self.rank, self.world, height, row_block)
+            self.row0, self.rows, self.step = split_band_spec(self.rank, self.world, height, row_block,
+                                                              compositor)
             self.specs = [(self.row0, self.rows, self.step)]
         else:
             self.row0, self.rows, self.step = band_spec(self.rank, self.world, height)
@@ -308,7 +340,7 @@ class FrameTiler:
         self.latest = None
         if self.gather:
             # every rank's band padded to the largest band's rows: equal gather sizes
-            specs = [block_band_spec(r, self.world, height, row_block) for r in range(self.world)]
+            specs = [split_band_spec(r, self.world, height, row_block, compositor) for r in range(self.world)]
             self.rmax = max(sp[1] for sp in specs)
             self.bufs = [torch.zeros((self.rmax, width, channels), dtype=dtype, device=device)
                          for _ in range(self.slots)]
@@ -384,8 +416,9 @@ class FrameTiler:
         completion events (CUDA streams, dependent lanes)."""
         if self.part_streams is None:
             for s, (row0, rows, step) in enumerate(self.specs):
-                self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
-                                 **self.block_kw)
+                if rows:
+                    self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
+                                     **self.block_kw)
             if self.gather and self.exchange_on:
                 self._log_exchange(lane)
                 self.exchange.run(self, lane)
@@ -404,8 +437,9 @@ class FrameTiler:
             with torch.cuda.stream(st):
                 if dep and self.part_done[prev_lane][s] is not None:
                     st.wait_event(self.part_done[prev_lane][s])   # the history rows of part s
-                self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
-                                 **self.block_kw)
+                if rows:
+                    self.render_band(row0, rows, step, self.part_rows(band, s), self.part_rows(prev, s),
+                                     **self.block_kw)
                 if self.gather and self.exchange_on:
                     if s == 0:
                         self._log_exchange(lane)
@@ -434,7 +468,8 @@ class FrameTiler:
                     st.wait_stream(cur)
             self.fresh = False
         row0, rows, step, outs, pitch, stream = self.plan[lane]
-        self.launch_batch(row0, rows, step, outs[:n], pitch, stream, **self.block_kw)
+        if rows:   # a compositor rank 0 renders nothing
+            self.launch_batch(row0, rows, step, outs[:n], pitch, stream, **self.block_kw)
         if self.gather and self.exchange_on:
             for j in range(n):
                 self._log_exchange(lane, k0 + j)
@@ -472,7 +507,8 @@ class FrameTiler:
                         st.wait_stream(cur)
                 self.fresh = False
             for args in self.plan[lane]:
-                self.launch(*args, **self.block_kw)
+                if args[1]:
+                    self.launch(*args, **self.block_kw)
             if self.gather and self.exchange_on:
                 self._log_exchange(lane)
                 if isinstance(self.exchange, GatherLib):
@@ -500,7 +536,8 @@ class FrameTiler:
             dist.gather(band, glist, dst=0, group=self.group)
             return assemble_cyclic(torch.stack(glist)) if self.rank == 0 else None
         # block-cyclic bands may differ by one block: gather them padded to the largest
-        specs = [block_band_spec(r, self.world, self.height, self.row_block) for r in range(self.world)]
+        specs = [split_band_spec(r, self.world, self.height, self.row_block, self.compositor)
+                 for r in range(self.world)]
         rmax = max(sp[1] for sp in specs)
         pad = band.new_zeros((rmax,) + tuple(band.shape[1:]))
         pad[:band.shape[0]] = band

@@ -211,7 +211,8 @@ int vrt_launch_timing(vrt_ctx* ctx, double* total_ms, uint64_t* launches);
  * Launches on a stream that is being captured into a graph use dispatch order. Every tile is
  * rendered exactly once in any case: images are identical with and without it.
  * ABI v8: the state is a pool allocated by vrt_create (ABI v9: 16 slots of 5 x 65536 words + a
- * header: bands up to 65536 tiles, i.e. 4096 x 2048 pixels; larger bands use dispatch order), a
+ * header; since v14 5 x 131072 words: launches up to 131072 tiles, i.e. 4096 x 4096 pixels; larger
+ * launches use dispatch order), a
  * slot per (band, stream), zeroed on the launch stream when it is (re)assigned. Reassigning the
  * least recently used slot (more than 16 band/stream pairs in use) synchronises the device once
  * (ABI v9: the old stream is never touched; its owner may have destroyed it). */
@@ -228,7 +229,7 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
  * resident waves (CUs x 4 x 7 x 2 waves: 14336, e.g. 1920 x 960 pixels, on MI355X); smaller bands
  * and the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path. off =
  * 0: the exact path runs in the pixel's own lane, with the heavy-first tile order
- * (vrt_set_tile_order). Bands over 65536 tiles, and launches on a stream being captured into a
+ * (vrt_set_tile_order). Launches over 131072 tiles, and launches on a stream being captured into a
  * graph, use the in-lane path. Images are identical either way. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
 
@@ -347,7 +348,9 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
  * rounds a launch is bound by its longest waves and by the hardware queues that overlap launches,
  * not by the GPU's throughput, and a batch of k frames gives it a whole frame's waves again (the
  * deferred exact pass, the tile order and the grid sizing then see one large launch). Bytes equal
- * nframes single-frame launches' (tests/test_gpu_batch.py). No hit records or counters. */
+ * nframes single-frame launches' (tests/test_gpu_batch.py). No hit records or counters. A batch
+ * of more than 131072 tiles (16x8 pixels) is enqueued as the fewest launches that hold it, of
+ * equal frame counts. */
 int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams,
                                     const vrt_params* params, int32_t row0, int32_t rows,
                                     int32_t row_step, int32_t row_block, int64_t pitch,

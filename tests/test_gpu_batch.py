@@ -48,7 +48,8 @@ def batched(r, cams, ps, row0, rows, step, block):
     ("refraction", 128, 640, 360, 4, 4, 8, 8, 5),      # an 8-way block-cyclic band, 8 frames
     ("glass_cube", 64, 320, 200, 1, 2, 2, 2, 1),
     ("terrain", 64, 384, 216, 4, 2, 4, 4, 2),
-    ("terrain", 64, 3840, 2160, 4, 2, 2, 1, 0),        # 2 x 64 800 tiles: split into two launches
+    ("terrain", 64, 3840, 2160, 4, 2, 3, 1, 0),        # 3 x 64 800 tiles: two launches (2 + 1)
+    ("refraction", 128, 3840, 2160, 4, 4, 7, 7, 0),    # 7 frames of a 7-way 4K band: one launch
 ])
 def test_batch_equals_single_frames(built, scene, n, w, h, R, T, nf, ranks, rank):
     block = 16 if ranks > 1 else 1

@@ -151,7 +151,7 @@ def test_tile_order_graph_capture(renderer):
 
 
 def test_tile_order_band_beyond_the_pool(renderer):
-    """A band of more tiles than a pool slot holds (65 536: here 7680 x 4320 = 259 200 tiles in
+    """A band of more tiles than a pool slot holds (131 072: here 7680 x 4320 = 259 200 tiles in
     one launch) renders in dispatch order; the frame equals the exact instance's."""
     n, w, h = 128, 7680, 4320
     renderer.upload_volume(vrt.build_scene("refraction", n), n)

@@ -41,7 +41,7 @@ constexpr int kParts = 2;              // interleaved row parts of a frame that 
 // are kParts interleaved parts, whose launches overlap each other's tails.
 constexpr int kLanes = 4;
 constexpr int kOrderSlots = 16;        // tile-order buffers per device (band geometry x stream)
-constexpr uint32_t kOrderMaxTiles = 1u << 16;  // bands up to 65536 16x8 tiles (4096 x 2048 pixels)
+constexpr uint32_t kOrderMaxTiles = 1u << 17;  // launches up to 131072 16x8 tiles (e.g. 7 frames of a 7-way 4K band)
 constexpr size_t kOrderSlotWords = vrt::kOrdHdr + 5u * size_t(kOrderMaxTiles) + 2u * vrt::kOrdClasses;  // KArgs::order
 // KArgs::defer: two sets of segment counters, then the list: a pixel per word, 8 segments of
 // ceil(tiles / 8) tiles' pixels each. Allocated per tile-order slot at its first deferred launch,
@@ -1515,9 +1515,12 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
     if (!same) return fail(ctx, VRT_ERR_INVALID, "the frames of a batch may differ only in camera and time");
   }
   // a launch holds at most kOrderMaxTiles tiles (the tile order's and the deferred list's slot):
-  // a larger batch is enqueued as consecutive launches of as many frames as fit
+  // a larger batch is enqueued as the fewest consecutive launches that fit, of equal frame counts
+  // (7 frames that fit 6 at a time: 4 + 3, not 6 + 1)
   const uint32_t ft = a.tiles;
-  const int per = int(std::max<uint32_t>(1u, std::min<uint32_t>(uint32_t(nframes), kOrderMaxTiles / std::max(ft, 1u))));
+  const int fit = int(std::max<uint32_t>(1u, std::min<uint32_t>(uint32_t(nframes), kOrderMaxTiles / std::max(ft, 1u))));
+  const int nlaunch = (nframes + fit - 1) / fit;
+  const int per = (nframes + nlaunch - 1) / nlaunch;
   const vrt::KArgs all = a;
   for (int f0 = 0; f0 < nframes; f0 += per) {
     const int nf = std::min(per, nframes - f0);

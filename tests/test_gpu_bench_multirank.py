@@ -56,6 +56,14 @@ def test_bench_two_ranks_rccl(built, gather):
     two_ranks("strong", gather, [])
 
 
+@pytest.mark.skipif(_device_count() < 4, reason="RCCL needs one GPU per rank (the driver's multi-GPU node)")
+def test_bench_four_ranks_rccl_compositor(built):
+    """The driver's N = 4 command: RCCL, the compositor split by default (rank 0 assembles, ranks
+    1-3 render), gathered frames checked bit for bit against collect()."""
+    out = two_ranks("strong", True, [], n=4)
+    assert out["gather"]["compositor"] is True and out["roofline"]["rank"] == 1
+
+
 def two_ranks(scaling, gather, backend_args, n=2):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),

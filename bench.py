@@ -686,10 +686,16 @@ def main():
                     gather_bad = (gather_bad or 0) + int((full != got_frame).sum().item())
             if prev_full is not None:
                 pairs.append((prev_full.cpu().numpy(), tiler.last().cpu().numpy()))
-        verify = {"verified": bad == 0, "frames": max(1, args.verify_frames),
+        own_ok = bad == 0
+        if world > 1:   # every rank's parts (a compositor rank 0 has none of its own)
+            bt = torch.tensor([bad, total], dtype=torch.int64, device=dev)
+            dist.all_reduce(bt)
+            bad, total = (int(x) for x in bt.tolist())
+        verify = {"verified": own_ok, "frames": max(1, args.verify_frames),
                   "mismatched_elements": bad, "elements": total,
                   "against": "exact walks (STATS instance, counters on) on a copy of the same "
-                             "history, every part of this rank"}
+                             "history, every part of " + ("every rank (elements summed)" if world > 1
+                                                          else "this rank")}
         if gather_bad is not None:
             verify["gathered_frame_mismatched_elements"] = gather_bad
         seq_ok = True
@@ -703,7 +709,7 @@ def main():
             seq_ok = bool(torch.equal(x_lo, x_hi))
             verify["gather_sequence_equal_all_ranks"] = seq_ok
             verify["gathers_per_lane"] = xl[0::2].tolist()
-        ok = torch.tensor([1 if bad == 0 and not gather_bad and seq_ok else 0], device=dev)
+        ok = torch.tensor([1 if own_ok and not gather_bad and seq_ok else 0], device=dev)
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         verify["verified_all_ranks"] = bool(ok.item())

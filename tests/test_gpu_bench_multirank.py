@@ -101,6 +101,7 @@ def two_ranks(scaling, gather, backend_args, n=2):
     assert out["verified"] is True
     assert out["latency"]["frame_latency_ms"] > 0
     rows = 1080 * n if scaling == "weak" else 1080
+    assert out["verify"]["elements"] == rows * 1920 * 4   # every rank's band, summed: the frame
     if gather:   # every timed frame gathered and assembled on rank 0, checked against collect()
         assert out["collect"] is None and "every frame" in out["config"]["parallelism"]
         assert out["gather"]["per_frame"] is True and out["gather"]["render_only"]["value"] > 0

@@ -24,6 +24,9 @@ its band in HBM, and every timed frame is gathered to rank 0 over RCCL (xGMI) an
 main.cpp:379-385): per frame, on the frame's lane stream, the render, the library's ncclGather
 (one communicator per lane, vrt_gather_band_async) and rank 0's assembly kernel
 (vrt_assemble_blocks_async), so the gathers of frames in flight overlap the renders of the others.
+From N = 4 rank 0 is a compositor (--compositor): it renders no band and assembles every frame,
+while ranks 1..N-1 split the frame (tiles.split_band_spec). A K-way band renders K frames per
+launch (8 from K = 7; vrt_render_temporal_batch_async).
 The JSON's "render_only" object times the same frames without the gather (labelled; --no-gather
 makes that the timed path and gathers the last frame once instead). Default --scaling strong: the
 config's frame (C3: 1920x1080) is split N ways, the reference's one frame per draw

@@ -119,6 +119,8 @@ def parse():
                          "launch, 0 off")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
                     help="certified pixels (vrt_set_certified): 0 automatic, 1 always, -1 never")
+    ap.add_argument("--cert-trees", type=int, default=1, choices=[0, 1],
+                    help="certified bounce trees of glass pixels (vrt_set_cert_trees): 1 on, 0 off")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
@@ -326,8 +328,18 @@ def main():
     # process with every thread's stack on stderr and a non-zero exit, never a silent wait or an
     # in-place restart
     watchdog_s = args.watchdog_s if args.watchdog_s >= 0 else (300.0 if world > 1 else 0.0)
-    if watchdog_s > 0:
-        faulthandler.dump_traceback_later(watchdog_s, exit=True)
+
+    def watchdog(phase_s=None):
+        """(Re-)arm the hang watchdog for the next phase (each phase gets the full budget; a
+        healthy but long run is never cut by the sum of its phases), or cancel it (0)."""
+        if watchdog_s <= 0:
+            return
+        if phase_s == 0:
+            faulthandler.cancel_dump_traceback_later()
+        else:
+            faulthandler.dump_traceback_later(phase_s or watchdog_s, exit=True)
+
+    watchdog()
     lanes, queues, batch = pipeline_shape(args, world)
     if args.queues or queues != 4:   # before HIP initialises (the GPU box exports 4)
         os.environ["GPU_MAX_HW_QUEUES"] = str(queues)
@@ -381,6 +393,7 @@ def main():
     ren = vrt.Renderer(local)
     ren.set_exact_pass(args.exact_pass)
     ren.set_certified(args.certified)
+    ren.set_cert_trees(args.cert_trees)
     ren.set_tile_order(args.tile_order)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
     kparams = params   # the kernel's params: textured frames use the atlas uploaded once
@@ -388,6 +401,15 @@ def main():
         ren.upload_atlas(atlas)
         kparams = type(params).from_buffer_copy(params)
         kparams.atlas_rgba = None   # the context's atlas: no per-call compare of its bytes
+
+    # u_Time per frame as the reference sets it (main.cpp:343-345: a frame counter, 1 for the first
+    # frame): every launch of the timed path takes its frame's number (tiler.k frames requested so
+    # far); the counted and the verifying launches below reuse the last frame's. With zero noise
+    # it decides only the sign of a zero direction component (RandomizeDirection, voxel.glsl:132-140).
+    # The sun stays where "Make day" puts it: the reference's day/night cycle would move
+    # it by ~1e-5 degrees per frame at these frame times.
+    def set_frame_time(k):
+        kparams.time = float(k)
 
     def launch(row0, rows, step, out, prev, cnt_ptr=0, row_block=1):
         sp = torch.cuda.current_stream(dev).cuda_stream   # the part's stream (FrameTiler)
@@ -403,10 +425,12 @@ def main():
                                   pitch=pitch, row_block=row_block)
 
     def render_band(row0, rows, step, out, prev, row_block=1):
+        set_frame_time(tiler.k)
         launch(row0, rows, step, out, prev, row_block=row_block)
 
     def launch_ptrs(row0, rows, step, out_ptr, prev_ptr, pitch, sp, row_block=1):
         # the lean form (FrameTiler's precomputed launches): one ctypes call per part launch
+        set_frame_time(tiler.k)
         if rgba8:
             ren.render_temporal_rows_async(cam, kparams, args.alpha, row0, rows, step, prev_ptr,
                                            out_ptr, 0, 0, 0, sp, pitch=pitch, row_block=row_block)
@@ -416,7 +440,14 @@ def main():
 
     def launch_batch(row0, rows, step, outs, pitch, sp, row_block=1):
         # frame batches (FrameTiler batch > 1): the band of len(outs) frames in one launch
-        ren.render_temporal_batch_async([cam] * len(outs), kparams, row0, rows, step, outs, None, sp,
+        k0 = tiler.k - len(outs)   # the batch's frames are k0 + 1 .. tiler.k
+        ps = []
+        for j in range(len(outs)):
+            q = type(kparams).from_buffer_copy(kparams)
+            q.time = float(k0 + 1 + j)
+            ps.append(q)
+        set_frame_time(tiler.k)
+        ren.render_temporal_batch_async([cam] * len(outs), ps, row0, rows, step, outs, None, sp,
                                         pitch=pitch, row_block=row_block)
 
     gather = world > 1 and not args.no_gather
@@ -509,6 +540,7 @@ def main():
                             "from ~1.9 to ~2.3 GHz over the first ~150 ms of this load "
                             "(DPM; profiles/r03_s2), so a fresh process's first frames run "
                             "~10 % slower than sustained rendering"}
+    watchdog()
     for _ in range(args.warmup):
         tiler.frame()
     tiler.finish()
@@ -516,6 +548,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    watchdog()   # the timed frames: scaled with --steps (a 20-frame run takes milliseconds)
     # Timed region: K frames. The device is idle here (synchronised above), so the lane streams
     # start without waiting on the main stream, and the closing device-wide synchronize waits for
     # every lane (no cross-queue joins inside the timed region: each costs a few us of queue
@@ -601,6 +634,21 @@ def main():
     lt_total, lt_n = ren.launch_timing()
     ren.set_launch_timing(0)
     launch_ms = lt_total / max(lt_n, 1)
+    watchdog()
+    # Exchange timing pass (after the timed region; GatherLib only): per frame, device events on its
+    # lane stream around the RGB8 pack + ncclGather (from the render's end, so a rank that arrives
+    # early also waits there for the slowest rank's band) and around rank 0's assembly
+    exchange_t = None
+    if tiler.gather and isinstance(tiler.exchange, GatherLib) and not args.rehearse_gather:
+        tiler.exchange.timing = []
+        for _ in range(max(16, 2 * lanes * batch)):
+            tiler.frame()
+        tiler.finish()
+        torch.cuda.synchronize(dev)
+        evs_x = tiler.exchange.timing
+        tiler.exchange.timing = None
+        exchange_t = (float(np.median([a_.elapsed_time(b_) for a_, b_, _ in evs_x])),
+                      float(np.median([b_.elapsed_time(c_) for _, b_, c_ in evs_x])))
     # a compositor rank 0 launches no render: the roofline fields are renderer rank 1's
     own_bytes = vrt.algorithmic_bytes(own, 8 if rgba8 else 16)
     bytes_per_launch = float(np.mean(part_bytes)) * batch   # a launch renders `batch` frames
@@ -640,14 +688,48 @@ def main():
         torch.cuda.synchronize(dev)
         lat.append(max(a.elapsed_time(b) for a in ea for b in eb))
     tiler.finish()
-    lat_t = torch.tensor([float(np.median(lat))], dtype=torch.float64, device=dev)
+    # Frame batches: a frame is launched only when its batch is full, so the batched pipeline's
+    # latency is one whole batch alone (request of its first frame to completion of the launch)
+    # plus the wait for the batch to fill (batch - 1 frame intervals at the timed frame rate)
+    blat = []
+    if batch > 1:
+        for _ in range(9):
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            lane_ = (tiler.k // tiler.batch) % tiler.lanes
+            sts_ = tiler.part_streams[lane_] if tiler.part_streams else [tiler.next_stream()]
+            ea = [torch.cuda.Event(enable_timing=True) for _ in sts_]
+            eb = [torch.cuda.Event(enable_timing=True) for _ in sts_]
+            for e, s_ in zip(ea, sts_):
+                e.record(s_)
+            for _ in range(batch):
+                tiler.frame()
+            tiler.flush()
+            for e, s_ in zip(eb, sts_):
+                e.record(s_)
+            torch.cuda.synchronize(dev)
+            blat.append(max(a.elapsed_time(b) for a in ea for b in eb))
+        tiler.finish()
+    lat_t = torch.tensor([float(np.median(lat)), float(np.median(blat)) if blat else 0.0],
+                         dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(lat_t, op=dist.ReduceOp.MAX)
     latency = {"frame_latency_ms": round(float(np.median(lat)), 4),
-               "frame_latency_ms_max_over_ranks": round(lat_t.item(), 4),
+               "frame_latency_ms_max_over_ranks": round(lat_t[0].item(), 4),
                "what": "one frame alone through the timed path (its lane's launches"
                        + (", gather and rank 0's assembly" if tiler.gather else "")
-                       + ", device events), median of 15"}
+                       + ", device events), median of 15"
+                       + ("; a batch of one: see batch_latency_ms for the batched pipeline" if batch > 1 else ""),
+               "frames_in_flight": lanes * batch,
+               "frames_in_flight_is": "lanes x frames per launch of the timed pipeline (the headline "
+                                      "value's frame rate relies on them; the reference's blocking "
+                                      "GL timer query keeps about one)"}
+    if blat:
+        latency["batch_latency_ms_max_over_ranks"] = round(lat_t[1].item(), 4)
+        latency["batch_latency_is"] = (f"one batch of {batch} frames alone through the timed path "
+                                       "(request of its first frame to the end of its launch and "
+                                       "exchange), median of 9")
     if world == 1 and not rehearse and rgba8:
         sync_ms = []
         for _ in range(9):
@@ -683,6 +765,7 @@ def main():
             got_frame = tiler.frame()
             tiler.finish()
             torch.cuda.synchronize(dev)
+            vtime = kparams.time   # this frame's u_Time: the reference launches below reuse it
             for s_, (row0, rows, step) in enumerate(tiler.specs):
                 if rows == 0:   # a compositor rank 0: no band
                     continue
@@ -699,7 +782,7 @@ def main():
                 if rank == 0:
                     gather_bad = (gather_bad or 0) + int((full != got_frame).sum().item())
             if prev_full is not None:
-                pairs.append((prev_full.cpu().numpy(), tiler.last().cpu().numpy()))
+                pairs.append((prev_full.cpu().numpy(), tiler.last().cpu().numpy(), vtime))
         own_ok = bad == 0
         if world > 1:   # every rank's parts (a compositor rank 0 has none of its own)
             bt = torch.tensor([bad, total], dtype=torch.int64, device=dev)
@@ -742,6 +825,23 @@ def main():
                        "ms": round((time.perf_counter() - t_c) * 1e3, 3),
                        "what": "one gather of every rank's band of the last frame to rank 0 and its "
                                "re-interleave, after the timed region"}
+
+    # Per-rank record (multi-rank runs): what a sub-linear scaling curve needs to name its cause
+    per_rank = None
+    if world > 1:
+        mine = torch.tensor([frame_gpu_ms, launch_ms, float(np.median(lat)),
+                             exchange_t[0] if exchange_t else -1.0, exchange_t[1] if exchange_t else -1.0],
+                            dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = []
+        for r_, t_ in enumerate(allr):
+            v_ = t_.tolist()
+            per_rank.append({"rank": r_, "kernel_ms": round(v_[0], 4), "launch_ms": round(v_[1], 4),
+                             "frame_latency_ms": round(v_[2], 4),
+                             "gather_ms": round(v_[3], 4) if v_[3] >= 0 else None,
+                             "assembly_ms": round(v_[4], 4) if v_[4] >= 0 and r_ == 0 else None})
+    watchdog(0)
 
     band_kind = (f"block-cyclic bands of {row_block}-row blocks" if row_block > 1 else
                  "cyclic row bands")
@@ -810,6 +910,8 @@ def main():
         frame_o = None
         cores = host_cores() if world == 1 else None
         cam1 = vrt.make_camera(w, h)
+        if pairs:   # the oracle renders the first verified frame (its u_Time)
+            params.time = pairs[0][2]
         if world == 1 and args.cpu_seconds > 0:
             threads = args.cpu_threads or cores["threads"]
             cpu, frame_o = cpu_baseline(cam1, vox_host, n, params, args.cpu_seconds, threads)
@@ -826,12 +928,13 @@ def main():
             import oracle
 
             worst, off1, nbytes = 0, 0, 0
-            for prev_np, got_np in pairs:
+            same_t = [pr for pr in pairs if pr[2] == params.time]   # frames of the oracle frame's u_Time
+            for prev_np, got_np, _ in same_t:
                 _, cur_o = oracle.temporal(frame_o, prev_np, args.alpha)
                 d = np.abs(got_np.astype(np.int16) - cur_o.astype(np.int16))
                 worst, off1, nbytes = max(worst, int(d.max())), off1 + int((d == 1).sum()), nbytes + d.size
-            oracle_check = {"frames": len(pairs), "max_lsb": worst, "bytes_off_by_one": off1,
-                            "bytes": nbytes, "ok": worst <= 1}
+            oracle_check = {"frames": len(same_t), "u_time": params.time, "max_lsb": worst,
+                            "bytes_off_by_one": off1, "bytes": nbytes, "ok": worst <= 1}
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",
             "value": round(value, 3),
@@ -954,7 +1057,24 @@ def main():
                         "wire": (("RGB8, 3 B per pixel" if tiler.exchange.rgb8 else "RGBA8/float as rendered")
                                  if isinstance(tiler.exchange, GatherLib) and tiler.exchange.args else
                                  ("as rendered" if tiler.gather else None)),
-                        "render_only": render_only}),
+                        "render_only": render_only,
+                        "per_rank": per_rank,
+                        "per_rank_is": ("each rank's kernel_ms (GPU time per timed frame), launch_ms, "
+                                        "single-frame latency, and from a pass after the timed region "
+                                        "the median per-frame gather_ms (device events on the lane "
+                                        "stream from the end of the frame's render across the RGB8 "
+                                        "pack and ncclGather: includes waiting for the slowest rank) "
+                                        "and rank 0's assembly_ms"),
+                        "rank0_ingress_gbs": (
+                            round(tiler.exchange.bytes_per_rank(tiler) * (world - 1)
+                                  / (per_rank[0]["gather_ms"] * 1e-3) / 1e9, 2)
+                            if per_rank and per_rank[0]["gather_ms"] and isinstance(tiler.exchange, GatherLib)
+                            else None),
+                        "rank0_ingress_is": ("bytes every other rank sends rank 0 per frame / rank 0's "
+                                             "median gather_ms (an upper bound of the link time: the "
+                                             "wait for late ranks is inside)"),
+                        "hardware_scaling_measured": ("this run" if world > 1 and args.backend == "nccl"
+                                                      and not args.same_device else None)}),
             "latency": latency,
             "device_warmup": device_warmup,
             "frame_events_ms": frame_events_ms,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VRT_ABI_VERSION 14
+#define VRT_ABI_VERSION 15
 
 typedef struct vrt_ctx vrt_ctx;
 
@@ -233,6 +233,15 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
  * graph, use the in-lane path. Images are identical either way. */
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
 
+/* ABI v15: certified bounce trees for stats-free colour-only frames with certified pixels
+ * (DESIGN.md §6 "Certified bounce trees"): on = 1 (default), off = 0. A pixel whose primary ray
+ * hits glass has its whole bounce tree (voxel.glsl:425-452) walked by certified walks from the
+ * certified hits' uncertain origins, the colour folded in the reference's order; any ray whose
+ * walk, start or direction could differ from the exact path's sends the pixel to the exact path
+ * (deferred or in lane, as above). With it on, the automatic certified mode (vrt_set_certified 0)
+ * certifies pixels whatever the volume's glass share. Images are identical either way. */
+int vrt_set_cert_trees(vrt_ctx* ctx, int32_t on);
+
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3
  * pairs, out = n float3. Synchronous. */
 int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
@@ -341,8 +350,8 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
 
 /* ABI v14: a FRAME BATCH: the same band of `nframes` (1..8) frames in ONE launch, at u_Alpha = 1
  * (each frame's RGB8 store is its output; no history is read), frame f with its own camera
- * cams[f] (same image size) and u_Time params[f].time, every other field of params[f] equal to
- * params[0]'s, written to d_cur_rgba8[f] (and d_raw_rgba8[f] when d_raw_rgba8 is not NULL; pitch
+ * cams[f] (same image size) and u_Time params[f].time, written to d_cur_rgba8[f] (and
+ * d_raw_rgba8[f] when d_raw_rgba8 is not NULL; pitch
  * pixels per band row in all of them). Band geometry as vrt_render_temporal_blocks_pitched_async;
  * bands of < 8192 rows. A band of a k-way split is 1/k of the frame's waves: below a few dispatch
  * rounds a launch is bound by its longest waves and by the hardware queues that overlap launches,
@@ -350,7 +359,9 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
  * deferred exact pass, the tile order and the grid sizing then see one large launch). Bytes equal
  * nframes single-frame launches' (tests/test_gpu_batch.py). No hit records or counters. A batch
  * of more than 131072 tiles (16x8 pixels) is enqueued as the fewest launches that hold it, of
- * equal frame counts. */
+ * equal frame counts. ABI v15: consecutive frames whose other params fields differ (the day/night
+ * cycle moves u_SunDir every frame, main.cpp:346-348) are split into launches of equal fields, in
+ * frame order on the stream (before v15: an error). */
 int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams,
                                     const vrt_params* params, int32_t row0, int32_t rows,
                                     int32_t row_step, int32_t row_block, int64_t pitch,

@@ -44,7 +44,7 @@ def test_struct_layouts():
 
 
 def test_abi_version(built):
-    assert vrt.lib().vrt_abi_version() == 14
+    assert vrt.lib().vrt_abi_version() == 15
 
 
 @pytest.mark.parametrize("scene", [0, 1, 2])

@@ -98,16 +98,37 @@ def test_batch_argument_checks(built):
         r.upload_volume(vrt.build_scene("refraction", 32), 32)
         with pytest.raises(vrt.VrtError):   # 9 frames
             r.render_temporal_batch_async(cameras(w, h, 9), params_for(4, 4, 9), 0, h, 1, ptrs)
-        bad = params_for(4, 4, 2)
-        bad[1].max_reflections = 3           # only camera and time may differ
-        with pytest.raises(vrt.VrtError):
-            r.render_temporal_batch_async(cams, bad, 0, h, 1, ptrs[:2])
+        with pytest.raises(ValueError):     # a params list shorter than the cameras
+            r.render_temporal_batch_async(cams, ps[:1], 0, h, 1, ptrs[:2])
+        with pytest.raises(ValueError):     # a raw-output list shorter than the cameras
+            r.render_temporal_batch_async(cams, ps, 0, h, 1, ptrs[:2], d_raws=ptrs[:1])
         with pytest.raises(vrt.VrtError):   # different image sizes
             r.render_temporal_batch_async([cams[0], vrt.make_camera(w + 16, h)], ps, 0, h, 1, ptrs[:2])
         with pytest.raises(vrt.VrtError):   # a null output
             r.render_temporal_batch_async(cams, ps, 0, h, 1, [ptrs[0], 0])
         r.render_temporal_batch_async(cams, ps, 0, h, 1, ptrs[:2])   # and a valid one passes
         torch.cuda.synchronize()
+
+
+def test_batch_with_per_frame_params(built):
+    """ABI v15: frames whose params differ beyond u_Time (the day/night cycle's sun, main.cpp:346-
+    348; here also the bounce limits and noise) share a batch call; the library splits them into
+    launches of equal params, in order. Bytes equal one launch per frame."""
+    w, h, nf = 320, 180, 6
+    cams = cameras(w, h, nf)
+    ps = params_for(4, 4, nf)
+    for f in range(nf):   # the sun moves every frame; frames 3-4 also change the bounce limits
+        ps[f].sun_dir = (vrt.abi.C.c_float * 3)(*vrt.sun_dir(45.0 + 0.5 * (f // 2)))
+    ps[3].max_reflections = ps[4].max_reflections = 1
+    ps[4].refraction_noise = 0.01
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("refraction", 64), 64)
+        for mode in (1, 2):
+            r.set_exact_pass(mode)
+            ref = singles(r, cams, ps, 0, h, 1, 1)
+            got = batched(r, cams, ps, 0, h, 1, 1)
+            for f in range(nf):
+                assert np.array_equal(got[f], ref[f]), f"mode {mode} frame {f}"
 
 
 @pytest.mark.parametrize("batch,lanes,frames", [(8, 4, 21), (4, 2, 9), (2, 3, 4)])

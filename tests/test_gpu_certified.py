@@ -128,28 +128,37 @@ def test_certified_glass_scenes(renderer, seed):
 
 
 def test_certified_modes(renderer):
-    """Automatic mode: on unless glass is > 1/8 of the non-empty voxels (the glass cube); every mode
-    renders the same image."""
+    """Automatic mode: with certified bounce trees (ABI v15, the default) always on; without them on
+    unless glass is > 1/8 of the non-empty voxels (the glass cube). Every mode, with and without
+    trees, renders the same image."""
     try:
         for scene, n, auto in (("glass_cube", 64, False), ("refraction", 64, True), ("terrain", 128, True)):
             vox = vrt.build_scene(scene, n)
             renderer.upload_volume(vox, n)
             renderer.set_certified(0)
+            renderer.set_cert_trees(1)
+            assert renderer.certified()
+            renderer.set_cert_trees(0)
             assert renderer.certified() == auto, scene
             renderer.set_certified(-1)
             assert not renderer.certified()
             cam = vrt.make_camera(96, 64)
             p = vrt.default_params(4, 4)
             imgs = []
-            for mode in (-1, 0, 1):
-                renderer.set_certified(mode)
-                imgs.append(stats_free(renderer, cam, p, 64, 96))
-            assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
-            assert np.array_equal(imgs[0].view(np.uint32), imgs[2].view(np.uint32))
+            for trees in (0, 1):
+                renderer.set_cert_trees(trees)
+                for mode in (-1, 0, 1):
+                    renderer.set_certified(mode)
+                    imgs.append(stats_free(renderer, cam, p, 64, 96))
+            for im in imgs[1:]:
+                assert np.array_equal(imgs[0].view(np.uint32), im.view(np.uint32))
         with pytest.raises(vrt.VrtError):
             renderer.set_certified(2)
+        with pytest.raises(vrt.VrtError):
+            renderer.set_cert_trees(2)
     finally:
         renderer.set_certified(1)
+        renderer.set_cert_trees(1)
 
 
 @pytest.mark.parametrize("seed", range(4))

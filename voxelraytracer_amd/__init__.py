@@ -302,6 +302,11 @@ class Renderer:
         bands of at least two rounds of resident waves), 2 always. Images are identical."""
         self._check(self._lib.vrt_set_exact_pass(self._h, int(mode)), "vrt_set_exact_pass")
 
+    def set_cert_trees(self, on):
+        """Certified bounce trees of glass pixels (ABI v15): True/1 on (default), False/0 off.
+        Images are identical."""
+        self._check(self._lib.vrt_set_cert_trees(self._h, int(on)), "vrt_set_cert_trees")
+
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0
 
@@ -390,10 +395,14 @@ class Renderer:
                                     d_curs, d_raws=None, stream: int = 0, pitch: int = 0,
                                     row_block: int = 1):
         """The same band of len(cams) frames in one launch at alpha 1 (vrt_render_temporal_batch_async,
-        ABI v14): cams / params / d_curs (/ d_raws) one per frame; params may differ only in time."""
+        ABI v14): cams / d_curs (/ d_raws) one per frame, params one Params or one per frame (ABI
+        v15: frames whose params differ beyond u_Time take launches of their own, in order)."""
         nf = len(cams)
         if isinstance(params, Params):
             params = [params] * nf
+        if len(params) != nf or len(d_curs) != nf or (d_raws is not None and len(d_raws) != nf):
+            raise ValueError(f"render_temporal_batch_async: {nf} cameras need as many params, outputs "
+                             "(and raw outputs, when given)")
         ca = (Camera * nf)(*cams)
         pa = (Params * nf)(*params)
         cur = (C.c_void_p * nf)(*d_curs)

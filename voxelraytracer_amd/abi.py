@@ -132,6 +132,7 @@ SIGNATURES = {
     "vrt_certified": (C.c_int, [C.c_void_p]),
     "vrt_set_tile_order": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_set_exact_pass": (C.c_int, [C.c_void_p, C.c_int32]),
+    "vrt_set_cert_trees": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_set_launch_timing": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_launch_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "vrt_render": (

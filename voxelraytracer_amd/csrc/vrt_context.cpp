@@ -140,6 +140,7 @@ struct vrt_ctx {
   std::vector<ncclComm_t> comms;
   int32_t layout_req = 0;               // vrt_set_skip_layout
   int32_t cert_req = 0;                 // vrt_set_certified
+  int32_t tree_req = 1;                 // vrt_set_cert_trees
   int tile_order = 1;                   // vrt_set_tile_order: 0 off, 1 automatic, 2 always
   int32_t exact_pass = 1;               // vrt_set_exact_pass: 0 off, 1 automatic, 2 always
   // vrt_set_launch_timing: timing events for the async band launches' device start / end
@@ -436,7 +437,10 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.prev = nullptr;
   a.cur = nullptr;
   a.raw = nullptr;
-  a.cert = s.octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || s.cert_auto ? 2 : 1);
+  // automatic mode: certified pixels unless glass dominates the volume, or always with certified
+  // bounce trees (which settle the glass pixels too)
+  a.cert = s.octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || s.cert_auto || ctx->tree_req ? 2 : 1);
+  a.tree = a.cert == 2 && p->color_only && ctx->tree_req ? 1 : 0;
   a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
   a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
   a.order = nullptr;
@@ -1343,7 +1347,15 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
 int vrt_certified(const vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
   const Shard& s = ctx->sh[0];
-  return s.octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || s.cert_auto) ? 1 : 0;
+  return s.octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || s.cert_auto || ctx->tree_req) ? 1 : 0;
+}
+
+int vrt_set_cert_trees(vrt_ctx* ctx, int32_t on) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (on < 0 || on > 1) return fail(ctx, VRT_ERR_INVALID, "certified trees must be 0 or 1");
+  ctx->tree_req = on;
+  ctx->err.clear();
+  return VRT_OK;
 }
 
 int vrt_volume_octants(const vrt_ctx* ctx) {
@@ -1471,23 +1483,21 @@ int vrt_render_temporal_blocks_pitched_async(vrt_ctx* ctx, const vrt_camera* cam
   return VRT_OK;
 }
 
-int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams, const vrt_params* p,
-                                    int32_t row0, int32_t rows, int32_t row_step, int32_t row_block, int64_t pitch,
-                                    uint32_t* const* d_cur_rgba8, uint32_t* const* d_raw_rgba8, void* hip_stream) {
-  if (!ctx) return VRT_ERR_INVALID;
-  if (nframes < 1 || nframes > vrt::kMaxBatch || !cams || !d_cur_rgba8)
-    return fail(ctx, VRT_ERR_INVALID, "nframes must be in [1, 8] with a camera and an output per frame");
-  int st = check_render_args(ctx, &cams[0], p);
-  if (st != VRT_OK) return st;
-  for (int f = 0; f < nframes; ++f) {
-    if (!d_cur_rgba8[f]) return fail(ctx, VRT_ERR_INVALID, "null output");
-    if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
-      return fail(ctx, VRT_ERR_INVALID, "the frames of a batch share the image size");
-  }
-  int32_t sh = 0;
-  if ((st = check_band(ctx, &cams[0], row0, rows, row_step, pitch, row_block, &sh)) != VRT_OK) return st;
-  if (nframes > 1 && rows >= 8192) return fail(ctx, VRT_ERR_UNSUPPORTED, "frame batches need bands of < 8192 rows");
-  if (rows == 0) return VRT_OK;
+// The per-launch fields of two frames' params agree (a frame batch's launch holds one copy of
+// them; only the camera and u_Time are per frame)
+static bool same_launch_params(const vrt_params& q, const vrt_params& r) {
+  return q.sun_dir[0] == r.sun_dir[0] && q.sun_dir[1] == r.sun_dir[1] && q.sun_dir[2] == r.sun_dir[2] &&
+         q.ray_noise == r.ray_noise && q.reflection_noise == r.reflection_noise &&
+         q.refraction_noise == r.refraction_noise && q.max_ray_length == r.max_ray_length &&
+         q.max_reflections == r.max_reflections && q.max_transparencies == r.max_transparencies &&
+         q.color_only == r.color_only && q.atlas_rgba == r.atlas_rgba && q.atlas_size == r.atlas_size &&
+         q.atlas_texture_size == r.atlas_texture_size;
+}
+
+// Frames [f0, f0 + nframes) of a batch whose per-launch params agree: the fewest launches that hold them
+static int batch_run(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams, const vrt_params* p, int32_t row0,
+                     int32_t rows, int32_t row_step, int32_t sh, int64_t pitch, uint32_t* const* d_cur_rgba8,
+                     uint32_t* const* d_raw_rgba8, void* hip_stream) {
   Shard& s = ctx->sh[0];
   vrt::KArgs a = make_args(ctx, s, &cams[0], p, row0, rows, row_step);
   a.row_blk_sh = sh;
@@ -1503,16 +1513,6 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
     b.time = p[f].time;
     b.cur = d_cur_rgba8[f];
     b.raw = d_raw_rgba8 ? d_raw_rgba8[f] : nullptr;
-    // every other parameter is one per launch
-    const vrt_params& q = p[f];
-    const bool same = q.sun_dir[0] == p[0].sun_dir[0] && q.sun_dir[1] == p[0].sun_dir[1] &&
-                      q.sun_dir[2] == p[0].sun_dir[2] && q.ray_noise == p[0].ray_noise &&
-                      q.reflection_noise == p[0].reflection_noise && q.refraction_noise == p[0].refraction_noise &&
-                      q.max_ray_length == p[0].max_ray_length && q.max_reflections == p[0].max_reflections &&
-                      q.max_transparencies == p[0].max_transparencies && q.color_only == p[0].color_only &&
-                      q.atlas_rgba == p[0].atlas_rgba && q.atlas_size == p[0].atlas_size &&
-                      q.atlas_texture_size == p[0].atlas_texture_size;
-    if (!same) return fail(ctx, VRT_ERR_INVALID, "the frames of a batch may differ only in camera and time");
   }
   // a launch holds at most kOrderMaxTiles tiles (the tile order's and the deferred list's slot):
   // a larger batch is enqueued as the fewest consecutive launches that fit, of equal frame counts
@@ -1541,6 +1541,38 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
     launch_timing_events(ctx, eb, ee);
     launch(ctx, s, b, nullptr, nullptr, nullptr, static_cast<hipStream_t>(hip_stream), eb, ee);
     VRT_HIP(ctx, hipGetLastError());
+  }
+  return VRT_OK;
+}
+
+int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_camera* cams, const vrt_params* p,
+                                    int32_t row0, int32_t rows, int32_t row_step, int32_t row_block, int64_t pitch,
+                                    uint32_t* const* d_cur_rgba8, uint32_t* const* d_raw_rgba8, void* hip_stream) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (nframes < 1 || nframes > vrt::kMaxBatch || !cams || !p || !d_cur_rgba8)
+    return fail(ctx, VRT_ERR_INVALID, "nframes must be in [1, 8] with a camera, params and an output per frame");
+  for (int f = 0; f < nframes; ++f) {
+    const int st = check_render_args(ctx, &cams[f], &p[f]);
+    if (st != VRT_OK) return st;
+    if (!d_cur_rgba8[f]) return fail(ctx, VRT_ERR_INVALID, "null output");
+    if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
+      return fail(ctx, VRT_ERR_INVALID, "the frames of a batch share the image size");
+  }
+  int32_t sh = 0;
+  int st = check_band(ctx, &cams[0], row0, rows, row_step, pitch, row_block, &sh);
+  if (st != VRT_OK) return st;
+  if (nframes > 1 && rows >= 8192) return fail(ctx, VRT_ERR_UNSUPPORTED, "frame batches need bands of < 8192 rows");
+  if (rows == 0) return VRT_OK;
+  // runs of consecutive frames whose per-launch params agree share a launch (the reference's
+  // day/night cycle moves u_SunDir every frame, main.cpp:346-348, 397-399: such frames take a
+  // launch each, in order on the stream)
+  for (int f0 = 0; f0 < nframes;) {
+    int f1 = f0 + 1;
+    while (f1 < nframes && same_launch_params(p[f1], p[f0])) ++f1;
+    st = batch_run(ctx, f1 - f0, cams + f0, p + f0, row0, rows, row_step, sh, pitch, d_cur_rgba8 + f0,
+                   d_raw_rgba8 ? d_raw_rgba8 + f0 : nullptr, hip_stream);
+    if (st != VRT_OK) return st;
+    f0 = f1;
   }
   return VRT_OK;
 }

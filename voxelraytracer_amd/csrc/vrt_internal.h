@@ -39,6 +39,9 @@ struct KArgs {
   // stats-free colour-only launches (vrt_set_certified): 0 exact walks only, 1 certified walks
   // for the exact path's shadow and air-medium secondary rays, 2 also whole pixels first
   int32_t cert;
+  // certified bounce trees (vrt_set_cert_trees, ABI v15): colour-only certified launches settle a
+  // glass primary hit's whole bounce tree by certified walks (cert_tree) where they can
+  int32_t tree;
   // tile dispatch order (stats-free launches, vrt_set_tile_order): nullptr = dispatch order, else
   // the band's order buffer: three sets of kOrdClasses list counters, the per-tile wave counters,
   // two rank sets of `tiles` words and two list sets of tiles + 8 words (see ordered_tile).

@@ -29,6 +29,16 @@
 #error "VRT_STAMPS / VRT_CERT_DIAG are diagnostic builds: use make variant"
 #endif
 
+// VRT_DIAG_PHASE (diagnostic builds only; wrong images): the certified pass stops after phase
+// 0 ray setup skipped / 1 primary ray / 2 primary certified walk / 3 shading without the shadow
+// walk, for a per-phase instruction budget by PMC differences (scripts/phase_budget.py)
+#if defined(VRT_DIAG_PHASE) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_DIAG_PHASE is a diagnostic build: use make variant"
+#endif
+#ifndef VRT_DIAG_PHASE
+#define VRT_DIAG_PHASE 9
+#endif
+
 namespace vrt {
 
 // ------------------------------------------------------------------ GLSL vector semantics --
@@ -146,6 +156,12 @@ __device__ __forceinline__ float4 mat_color(uint32_t m) {
 }
 
 constexpr float kAmbient = 0.3f;
+
+// Colour-only glass (voxel.glsl:85: colour vec4(0)) adds col.rgb * col.a * brightness = +0 for any
+// finite brightness (glass's lit brightness is finite: kd = ks = 1, exponent 1; RayColor, :184-188),
+// so a glass hit's colour does not depend on its shadow bit: the stats-free paths skip its shadow
+// walk (TraceWithShadow, :400-402). Images unchanged.
+__device__ __forceinline__ bool shadow_free_hit(uint32_t byte, bool tex) { return !tex && mat_id(byte) == 2u; }
 
 // ----------------------------------------------------------------------------- ray state --
 
@@ -901,7 +917,7 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
     if (CSH) {
       const float lit = lit_brightness<TEX>(h, c.sun_n, ray.dir);
       int blocked = 0;
-      if (lit != kAmbient) {
+      if (lit != kAmbient && !shadow_free_hit(h.voxel, TEX)) {
         blocked = cert_shadow_exact(c, h);
         if (blocked < 0) blocked = march_shadow<STATS>(c, sr, k, steps, flags) ? 1 : 0;
       }
@@ -1260,7 +1276,7 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
                                                const Hit& hh, f3& color, float4 col = float4()) {
   const float lit = lit_brightness<TEX>(hh, c.sun_n, ray.dir);
   float brightness = kAmbient;
-  if (lit != kAmbient) {  // otherwise in shadow or not, the brightness is the ambient term
+  if (lit != kAmbient && !shadow_free_hit(h.byte, TEX) && VRT_DIAG_PHASE > 3) {  // otherwise the brightness is the ambient term (or irrelevant)
     const f3 S = c.sun_n;
     if (!(dot3(hh.normal, S) > 0.0f) || !fast_path_ok(S)) { CERT_DIAG(5); return false; }  // back face
     // shadow origin: the exact hit point; start cell: the air cell in front of the hit face
@@ -1369,6 +1385,172 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
   }
   h.res = CERT_UNSURE;
   return h;
+}
+
+// ------------------------------------------------------------ certified bounce trees --------
+//
+// The colour of a glass pixel's bounce tree (voxel.glsl:425-452) depends on the exact hit points
+// only through the walks' outcomes: reflection and refraction directions, Fresnel energies, the
+// sky colour and the brightness are functions of directions and face normals alone
+// (:162-165, :203-246, :386-423) once RandomizeDirection is the identity (noise 0, no -0
+// component), and the accumulated rayLength enters only through the `< u_MaxRayLength` test. So
+// every ray of the tree is walked by a certified walk from its uncertain origin: the parent's
+// certified hit, known to its bound eu along the parent (cert_start checks the start cell and
+// turns the origin uncertainty into per-axis crossing-order bounds; cert_march carries in-volume
+// refraction). Any unsure step sends the whole pixel to the exact path.
+//
+// A ray in flight is a TreeRay: the Ray the reference would carry (pos and len approximate, dir,
+// energy, medium and depths exact) plus its certified start. The DFS keeps the ray the reference
+// pops next in registers (the last-pushed child), so only a reflection ray pushed under a
+// refraction ray waits, in one per-lane LDS slot (component-major, conflict-free ds_write_b32); a
+// tree that would hold two such rays at once (never at the BASELINE configs: one glass voxel or
+// one-voxel glass walls) goes to the exact path.
+struct TreeRay {
+  Ray ray;
+  int cx, cy, cz;  // start cell (the exact walk's first cell)
+  float e0;        // origin uncertainty (parameter along the parent)
+  f3 ed;           // per-axis crossing-order uncertainty from it
+};
+constexpr int kTreeWords = 14;
+template <int NL>
+__device__ __forceinline__ void tree_put(float* __restrict__ b, const TreeRay& t) {
+  b[0 * NL] = t.ray.pos.x;
+  b[1 * NL] = t.ray.pos.y;
+  b[2 * NL] = t.ray.pos.z;
+  b[3 * NL] = t.ray.dir.x;
+  b[4 * NL] = t.ray.dir.y;
+  b[5 * NL] = t.ray.dir.z;
+  b[6 * NL] = t.ray.len;
+  b[7 * NL] = t.ray.energy;
+  b[8 * NL] = t.e0;
+  b[9 * NL] = t.ed.x;
+  b[10 * NL] = t.ed.y;
+  b[11 * NL] = t.ed.z;
+  // cells in [0, 1024); a stored ray is a reflection ray: medium air
+  b[12 * NL] = __uint_as_float(uint32_t(t.cx) | uint32_t(t.cy) << 10 | uint32_t(t.cz) << 20);
+  b[13 * NL] = __uint_as_float(uint32_t(t.ray.rdepth) | uint32_t(t.ray.tdepth) << 16);
+}
+template <int NL>
+__device__ __forceinline__ TreeRay tree_get(const float* __restrict__ b) {
+  TreeRay t;
+  t.ray.pos = mk(b[0 * NL], b[1 * NL], b[2 * NL]);
+  t.ray.dir = mk(b[3 * NL], b[4 * NL], b[5 * NL]);
+  t.ray.len = b[6 * NL];
+  t.ray.energy = b[7 * NL];
+  t.e0 = b[8 * NL];
+  t.ed = mk(b[9 * NL], b[10 * NL], b[11 * NL]);
+  const uint32_t w = __float_as_uint(b[12 * NL]);
+  t.cx = int(w & 1023u);
+  t.cy = int((w >> 10) & 1023u);
+  t.cz = int((w >> 20) & 1023u);
+  const uint32_t dp = __float_as_uint(b[13 * NL]);
+  t.ray.rdepth = int(dp & 0xffffu);
+  t.ray.tdepth = int(dp >> 16);
+  t.ray.voxel = 0u;
+  return t;
+}
+
+// The certified start of a child ray from the certified hit h of its parent (direction d0 there):
+// the start cell, checked inside the volume, and cert_start's bounds. false: unsure.
+__device__ __forceinline__ bool tree_start(const Ctx& c, const CertResult& h, const Hit& hh, const f3 d0,
+                                           TreeRay& t) {
+  if (!fast_path_ok(t.ray.dir)) return false;
+  const uint32_t n = uint32_t(c.n);
+  if (uint32_t(t.cx) >= n || uint32_t(t.cy) >= n || uint32_t(t.cz) >= n) return false;
+  const f3 rn = mk(__builtin_amdgcn_rcpf(t.ray.dir.x), __builtin_amdgcn_rcpf(t.ray.dir.y),
+                   __builtin_amdgcn_rcpf(t.ray.dir.z));
+  t.e0 = h.eu;
+  return cert_start(hh.point, d0, t.ray.dir, rn, h.axis, h.eu, t.cx, t.cy, t.cz, t.ed);
+}
+
+// GetReflectionRay (voxel.glsl:203-215) of a certified hit: the direction must not depend on the
+// point (RandomizeDirection's zero-noise identity); it starts back in the cell before the face
+template <bool TEX>
+__device__ __forceinline__ bool tree_reflection(const Ctx& c, const Ray& ray, const CertResult& h, const Hit& hh,
+                                                TreeRay& t) {
+  if (!(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))) return false;
+  t.ray = reflection_ray(c, ray, hh);
+  cell_before(h, ray.dir, t.cx, t.cy, t.cz);
+  return tree_start(c, h, hh, ray.dir, t);
+}
+
+// GetRefractionRay (voxel.glsl:217-246) of a certified hit: the probes at point +- normal / 2
+// (:219-220) read the exact point's cells when the point is robust on the other axes (cert_start
+// checks it); total internal reflection turns it into the reflection ray, back before the face
+template <bool TEX>
+__device__ __forceinline__ bool tree_refraction(const Ctx& c, const Ray& ray, const CertResult& h, const Hit& hh,
+                                                TreeRay& t) {
+  const float eta = mat_refr(get_voxel(c, hh.point + hh.normal * 0.5f)) /
+                    mat_refr(get_voxel(c, hh.point - hh.normal * 0.5f));
+  const f3 rd = refract3(normalize3(ray.dir), hh.normal, eta);
+  const bool tir = rd.x == 0.0f && rd.y == 0.0f && rd.z == 0.0f;
+  if (tir ? !(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))
+          : !(c.refr_noise == 0.0f && zero_noise_exact(rd)))
+    return false;
+  Counters kk;
+#pragma unroll
+  for (int q = 0; q < VRT_CNT_COUNT; ++q) kk.c[q] = 0;
+  t.ray = refraction_ray<TEX>(c, ray, hh, kk);
+  t.cx = h.cx;  // into the hit cell, or (total internal reflection) back before it
+  t.cy = h.cy;
+  t.cz = h.cz;
+  if ((comp(t.ray.dir, h.axis) > 0.0f) != (comp(ray.dir, h.axis) > 0.0f)) cell_before(h, ray.dir, t.cx, t.cy, t.cz);
+  return tree_start(c, h, hh, ray.dir, t);
+}
+
+// The bounce tree of a glass primary hit h0 of ray0 (fragment main, voxel.glsl:425-452) by
+// certified walks, colour folded in the reference's DFS order as TraceWithShadow does (:395-423):
+// each ray's RayMarch by cert_march, its hit shaded with a certified shadow (none for glass),
+// a miss with the sky colour. Colour-only (TEX false) frames. Returns false, colour untouched,
+// when any walk, start or direction could differ from the exact path's.
+// lts: this lane's word 0 of the LDS slot (NL lanes per workgroup).
+template <int NL>
+__device__ __forceinline__ bool cert_tree(const Ctx& c, int max_refl, int max_transp, const Ray& ray0,
+                                          const CertResult& h0, f3& color_out, float* __restrict__ lts) {
+  f3 color = mk(0.0f, 0.0f, 0.0f);
+  Ray ray = ray0;
+  CertResult h = h0;
+  bool pending = false;  // a reflection ray waits in the LDS slot
+  for (;;) {
+    bool next = false;
+    TreeRay t;
+    if (h.res == CERT_MISS) {
+      apply_sky_color(c, ray, color);
+    } else {
+      const Hit hh = cert_hit_record(ray, h);
+      if (!cert_shade_hit<false>(c, ray, h, hh, color)) return false;
+      // children (:440-448): the reflection ray is pushed first, the refraction ray second and
+      // popped first; the stack (R + T + 1 entries) never fills with at most one ray waiting
+      const uint32_t m = mat_id(h.byte);
+      const bool pr = mat_reflective(m) && ray.rdepth < max_refl;
+      const bool pt = mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f;
+      if (pr && pt) {
+        if (pending) return false;
+        TreeRay r;
+        if (!tree_reflection<false>(c, ray, h, hh, r)) return false;
+        tree_put<NL>(lts, r);
+        pending = true;
+        if (!tree_refraction<false>(c, ray, h, hh, t)) return false;
+        next = true;
+      } else if (pr) {
+        if (!tree_reflection<false>(c, ray, h, hh, t)) return false;
+        next = true;
+      } else if (pt) {
+        if (!tree_refraction<false>(c, ray, h, hh, t)) return false;
+        next = true;
+      }
+    }
+    if (!next) {
+      if (!pending) break;
+      pending = false;
+      t = tree_get<NL>(lts);
+    }
+    ray = t.ray;
+    h = cert_march(c, ray, t.cx, t.cy, t.cz, t.e0, t.ed);
+    if (h.res == CERT_UNSURE) return false;
+  }
+  color_out = color;
+  return true;
 }
 
 // The exact walk's start cell from P along D (voxel.glsl:306-309: first planes d < 0 ? ceil(p - 1)
@@ -1637,9 +1819,16 @@ __device__ __forceinline__ bool cert_texel(const Ctx& c, const Ray& ray, const C
   return true;
 }
 
-template <bool TEX = false>
-__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out) {
+// TREE (colour-only): a glass primary hit's bounce tree by certified walks too (cert_tree; lts its
+// LDS slot), instead of leaving the whole pixel to the exact path.
+template <bool TEX = false, bool TREE = false, int NL = kWgThreads>
+__device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out, int max_refl = 0,
+                                           int max_transp = 0, float* __restrict__ lts = nullptr) {
   const f3 P = ray0.pos, D = ray0.dir;
+  if (VRT_DIAG_PHASE <= 1) {
+    color_out = D;
+    return true;
+  }
   if (!fast_path_ok(D)) { CERT_DIAG(0); return false; }
   int cx, cy, cz;
   if (!exact_start_cell(c, P, D, cx, cy, cz) || !start_layers_clear<false>(c, P, D, cx, cy, cz, 0u)) {
@@ -1653,6 +1842,10 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
 #ifdef VRT_CERT_DIAG
   cert_diag_iters(10, h.iters);
 #endif
+  if (VRT_DIAG_PHASE == 2) {
+    color_out = mk(float(h.res), float(h.byte), h.u);
+    return true;
+  }
   if (h.res == CERT_UNSURE) { CERT_DIAG(1); return false; }
   f3 color = mk(0.0f, 0.0f, 0.0f);
   if (h.res == CERT_MISS) {
@@ -1662,9 +1855,8 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
     return true;
   }
   if (mat_id(h.byte) == 2u) {  // only glass spawns secondary rays (:440-448)
-    // (certifying the glass pixels' bounce stacks too was correct but slower: the call site alone
-    // made the kernel 3x slower out of line, and inline C3 lost 20-45 %, profiles/r01_v46_*, r01_v48_*)
     CERT_DIAG(3);
+    if constexpr (TREE && !TEX) return cert_tree<NL>(c, max_refl, max_transp, ray0, h, color_out, lts);
     return false;
   }
   const Hit hh = cert_hit_record(ray0, h);
@@ -2088,7 +2280,10 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, const FrameView& fv,
 // FB: the frame-batch instance (KArgs::nframes > 1: per-frame camera, time and outputs, the frame
 // in a deferred entry's top bits); launches of one frame keep the instance without that decode
 // (it cost C1 4 %, C3 1 %: profiles/r05_s27)
-template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false, bool FB = false>
+// TREE (colour-only CERT 2): glass pixels' bounce trees by certified walks (cert_tree), one
+// kTreeWords LDS slot per lane.
+template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false, bool FB = false,
+          bool TREE = false>
 __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
@@ -2132,9 +2327,25 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     Ctx c;
     init_ctx(c, a, vox);
     if constexpr (FB) c.time = frame_view(a, fr).time;
-    __shared__ float4 ax_tab[kWgThreads * 3];
-    c.ax = &ax_tab[threadIdx.x * kAxLane];
+    // one LDS pool: the exact path's axis table and bounce-stack bottom (in-lane instances), and
+    // the certified tree's slots (TREE), which are live only before the exact path starts
+    constexpr int kAxFloats = DEFER ? 0 : kWgThreads * 3 * 4;
+    constexpr int kStkFloats = DEFER || !VRT_LDS_STACK ? 0 : kStackWords * kWgThreads;
+    constexpr int kTreeFloats = TREE ? kTreeWords * kWgThreads : 0;
+    constexpr int kPool = std::max(std::max(kAxFloats + kStkFloats, kTreeFloats), 4);
+    __shared__ float4 lds_pool[kPool / 4];
+    c.ax = &lds_pool[threadIdx.x * kAxLane];
+#if VRT_DIAG_PHASE == 0
+    Ray ray;
+    ray.pos = mk(float(px), float(li), 0.0f);
+    ray.dir = ray.pos;
+    ray.len = 0.0f;
+    ray.energy = 1.0f;
+    ray.voxel = 0;
+    ray.rdepth = ray.tdepth = 0;
+#else
     const Ray ray = primary_ray(a, FB ? frame_view(a, fr).pv : a.inv_pv, c, px, frame_row(a, li));
+#endif
     k.c[VRT_CNT_PIXELS] = 1;
     k.c[VRT_CNT_PRIMARY_RAYS] = 1;
     uint32_t steps = 0, flags = 0;
@@ -2147,7 +2358,12 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     // colour in LDS, or storing certified pixels before the exact path and re-deriving the
     // primary ray there, was 4-6 % slower.
     f3 color = mk(0.0f, 0.0f, 0.0f);
-    const bool need_exact = CERT < 2 || !cert_pixel<TEX>(c, ray, color);
+    float* tstk = nullptr;
+    if constexpr (TREE) {
+      static_assert(CERT == 2 && !TEX && !STATS, "certified trees: stats-free colour-only certified instances");
+      tstk = reinterpret_cast<float*>(lds_pool) + threadIdx.x;
+    }
+    const bool need_exact = CERT < 2 || !cert_pixel<TEX, TREE>(c, ray, color, a.max_refl, a.max_transp, tstk);
 #ifdef VRT_STAMPS
     const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
     const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
@@ -2161,7 +2377,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     } else if (need_exact) {
       color = mk(0.0f, 0.0f, 0.0f);
       heavy = true;
-      __shared__ float lstk[VRT_LDS_STACK ? kStackWords * kWgThreads : 1];
+      float* lstk = reinterpret_cast<float*>(lds_pool) + kAxFloats;
       (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
                                                          hit_len, &lstk[threadIdx.x]);
     }
@@ -2665,6 +2881,8 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     // frame batches (a.nframes > 1): their own instances
     const bool fb = a.nframes > 1;
     auto k1 = a.textured ? (fb ? render_kernel<false, true, 2, false, true, true> : render_kernel<false, true, 2, false, true>)
+              : a.tree   ? (fb ? render_kernel<false, false, 2, false, true, true, true>
+                               : render_kernel<false, false, 2, false, true, false, true>)
                          : (fb ? render_kernel<false, false, 2, false, true, true> : render_kernel<false, false, 2, false, true>);
     auto k2 = a.textured ? (fb ? exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX, true>
                                : exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX>)
@@ -2693,8 +2911,10 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
                                                           : render_kernel<false, false, 2, false, false, true>)
                                    : a.cert == 1 ? render_kernel<false, false, 1, false, false, true>
                                                  : render_kernel<false, false, 0, false, false, true>)
-                                : (a.cert == 2 ? (a.order ? render_kernel<false, false, 2, true>
-                                                          : render_kernel<false, false, 2>)
+                                : (a.cert == 2 ? (a.tree ? (a.order ? render_kernel<false, false, 2, true, false, false, true>
+                                                                    : render_kernel<false, false, 2, false, false, false, true>)
+                                                 : a.order ? render_kernel<false, false, 2, true>
+                                                           : render_kernel<false, false, 2>)
                                    : a.cert == 1 ? render_kernel<false, false, 1>
                                                  : render_kernel<false, false, 0>));
   if (ev_begin || ev_end)

@@ -173,6 +173,9 @@ class GatherLib:
         ids = share_ids(ids, lanes)
         renderer.comm_join(ids, world, rank)
         self.ren, self.lanes, self.wire, self.args = renderer, lanes, wire, None
+        # timing (bench.py, after its timed region): None, or a list collecting per exchanged frame
+        # the events (start, after the pack + ncclGather, after rank 0's assembly) on its lane stream
+        self.timing = None
 
     def _setup(self, tiler) -> None:
         self.rgb8 = (self.wire == "rgb8" and tiler.dtype == torch.uint8 and tiler.channels == 4
@@ -186,6 +189,7 @@ class GatherLib:
             if tiler.rank == 0:
                 self.gpacked = [torch.empty(tiler.world * px * 3, dtype=torch.uint8, device=dev)
                                 for _ in range(tiler.slots)]
+        self.tstreams = [tiler.part_streams[g // tiler.batch][0] for g in range(tiler.slots)]
         self.args = []
         for g in range(tiler.slots):   # (band, pixels, packed, gathered, frame, stream, communicator)
             self.args.append((tiler.bufs[g].data_ptr(), tiler.bufs[g].numel() // tiler.channels,
@@ -207,6 +211,10 @@ class GatherLib:
         if self.args is None:
             self._setup(tiler)
         band, px, packed, gath, frame, st, comm = self.args[slot]
+        evs = None
+        if self.timing is not None:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            evs[0].record(self.tstreams[slot])   # completes when the frame's render has
         # a compositor rank 0 renders no rows: its chunk of the gather is not packed and not
         # assembled (the bands of ranks 1.. start one padded band into the gathered buffer)
         nb = tiler.world - 1 if tiler.compositor else tiler.world
@@ -214,16 +222,23 @@ class GatherLib:
             if not (tiler.compositor and tiler.rank == 0):
                 self.ren.pack_rgb8_async(band, px, packed, st)
             self.ren.gather_band_async(comm, packed, px * 3, gath, st)
+            if evs:
+                evs[1].record(self.tstreams[slot])
             if tiler.rank == 0:
                 g0 = gath + (px * 3 if tiler.compositor else 0)
                 self.ren.assemble_blocks_rgb8_async(g0, nb, tiler.rmax, tiler.width, tiler.height,
                                                     tiler.row_block, frame, tiler.width, st)
-            return
-        bb = px * tiler.channels * tiler.dtype.itemsize
-        self.ren.gather_band_async(comm, band, bb, gath, st)
-        if tiler.rank == 0:
-            self.ren.assemble_blocks_async(gath + (bb if tiler.compositor else 0), nb, tiler.rmax, self.words,
-                                           tiler.height, tiler.row_block, frame, self.words, st)
+        else:
+            bb = px * tiler.channels * tiler.dtype.itemsize
+            self.ren.gather_band_async(comm, band, bb, gath, st)
+            if evs:
+                evs[1].record(self.tstreams[slot])
+            if tiler.rank == 0:
+                self.ren.assemble_blocks_async(gath + (bb if tiler.compositor else 0), nb, tiler.rmax,
+                                               self.words, tiler.height, tiler.row_block, frame, self.words, st)
+        if evs:
+            evs[2].record(self.tstreams[slot])
+            self.timing.append(evs)
 
 
 class GatherRehearsal(GatherLib):
@@ -237,6 +252,7 @@ class GatherRehearsal(GatherLib):
 
     def __init__(self, renderer, lanes: int):
         self.ren, self.lanes, self.wire, self.args = renderer, lanes, "rgb8", None
+        self.timing = None
 
     def run(self, tiler, slot: int) -> None:
         if self.args is None:

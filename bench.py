@@ -119,8 +119,9 @@ def parse():
                          "launch, 0 off")
     ap.add_argument("--certified", type=int, default=0, choices=[-1, 0, 1],
                     help="certified pixels (vrt_set_certified): 0 automatic, 1 always, -1 never")
-    ap.add_argument("--cert-trees", type=int, default=1, choices=[0, 1],
-                    help="certified bounce trees of glass pixels (vrt_set_cert_trees): 1 on, 0 off")
+    ap.add_argument("--cert-trees", type=int, default=1, choices=[0, 1, 2],
+                    help="certified bounce trees of glass pixels (vrt_set_cert_trees): 1 automatic "
+                         "(glass-heavy volumes), 2 always, 0 off")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "multi-rank rehearsal test)")
@@ -928,12 +929,16 @@ def main():
             import oracle
 
             worst, off1, nbytes = 0, 0, 0
-            same_t = [pr for pr in pairs if pr[2] == params.time]   # frames of the oracle frame's u_Time
-            for prev_np, got_np, _ in same_t:
-                _, cur_o = oracle.temporal(frame_o, prev_np, args.alpha)
+            frames_o = {params.time: frame_o}   # one oracle frame per verified frame's u_Time
+            for prev_np, got_np, t_ in pairs:
+                if t_ not in frames_o:
+                    params.time = t_
+                    frames_o[t_], _, _ = oracle.render(cam1, vox_host, n, params,
+                                                       threads=args.cpu_threads or cores["threads"])
+                _, cur_o = oracle.temporal(frames_o[t_], prev_np, args.alpha)
                 d = np.abs(got_np.astype(np.int16) - cur_o.astype(np.int16))
                 worst, off1, nbytes = max(worst, int(d.max())), off1 + int((d == 1).sum()), nbytes + d.size
-            oracle_check = {"frames": len(same_t), "u_time": params.time, "max_lsb": worst,
+            oracle_check = {"frames": len(pairs), "u_time": sorted(frames_o), "max_lsb": worst,
                             "bytes_off_by_one": off1, "bytes": nbytes, "ok": worst <= 1}
         out = {
             "metric": "Mrays/sec + achieved HBM GB/s, 1920x1080 @ 128^3 voxels, 4 bounces",

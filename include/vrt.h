@@ -234,12 +234,16 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
 int vrt_set_exact_pass(vrt_ctx* ctx, int32_t on);
 
 /* ABI v15: certified bounce trees for stats-free colour-only frames with certified pixels
- * (DESIGN.md §6 "Certified bounce trees"): on = 1 (default), off = 0. A pixel whose primary ray
- * hits glass has its whole bounce tree (voxel.glsl:425-452) walked by certified walks from the
- * certified hits' uncertain origins, the colour folded in the reference's order; any ray whose
- * walk, start or direction could differ from the exact path's sends the pixel to the exact path
- * (deferred or in lane, as above). With it on, the automatic certified mode (vrt_set_certified 0)
- * certifies pixels whatever the volume's glass share. Images are identical either way. */
+ * (DESIGN.md §6 "Certified bounce trees"): 1 = automatic (default), 2 = always, 0 = off. A pixel
+ * whose primary ray hits glass has its whole bounce tree (voxel.glsl:425-452) walked by certified
+ * walks from the certified hits' uncertain origins, the colour folded in the reference's order;
+ * any ray whose walk, start or direction could differ from the exact path's sends the pixel to the
+ * exact path (deferred or in lane, as above). The certified pass that runs the trees is its own
+ * kernel instance (more registers per lane); automatic mode uses it for the volumes whose glass is
+ * more than 1/8 of the non-empty voxels, where the automatic certified mode (vrt_set_certified 0)
+ * would otherwise render every pixel exactly, so the certified mode is then on for them too; in
+ * glass-light volumes the few glass pixels keep the deferred exact path. Images are identical in
+ * every mode. */
 int vrt_set_cert_trees(vrt_ctx* ctx, int32_t on);
 
 /* Diagnostic: the kernel's RandomizeDirection (voxel.glsl:132-140) for n (dir, pos) float3

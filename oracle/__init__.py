@@ -74,6 +74,9 @@ def lib():
         L.oracle_temporal_from_raw.restype = None
         L.oracle_temporal_from_raw.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p,
                                                C.c_uint64]
+        L.oracle_trace_pixel.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                         C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_trace_pixel.restype = C.c_int
         _lib = L
     return _lib
 
@@ -186,3 +189,19 @@ def get_color(atlas, atlas_size: int, tex_size: int, voxel: int, point, index: i
     lib().oracle_get_color(a.ctypes.data, atlas_size, tex_size, int(textured), voxel,
                            pt.ctypes.data, index, out.ctypes.data)
     return out
+
+
+def trace_pixel(cam: Camera, vox: np.ndarray, n: int, params: Params, px: int, py: int, cap: int = 256):
+    """Debug: the reference's ray tree of one pixel (colour-only) as records of 24 floats (code 1:
+    a TraceWithShadow call: [1, found, voxel, index, point xyz, len, pos xyz, dir xyz, len0,
+    energy, medium, rdepth, tdepth]; code 10: an in-volume refraction: [10, index, crossing xyz,
+    len, new dir xyz, new medium, energy, step]) and the pixel's colour."""
+    L = lib()
+    vox = np.ascontiguousarray(vox, dtype=np.uint8)
+    out = np.zeros((cap, 24), np.float32)
+    rgba = np.zeros(4, np.float32)
+    k = L.oracle_trace_pixel(C.byref(cam), vox.ctypes.data, n, C.byref(params), px, py, out.ctypes.data,
+                             cap, rgba.ctypes.data)
+    if k < 0:
+        raise RuntimeError(f"oracle_trace_pixel: {k}")
+    return out[:k], rgba

@@ -305,6 +305,19 @@ static int march_shadow(const ctx_t* c, const ray_t* ray, cnt_t* k, uint32_t* st
   return 0;
 }
 
+/* Debug trace of one pixel's ray tree (oracle_trace_pixel; single-threaded, test tooling only):
+ * 24-float records, code 1 = a TraceWithShadow call (the ray as it entered RayMarch and its
+ * result), code 10 = an in-volume refraction inside RayMarch (crossing point, new ray). */
+static float* g_tr = NULL;
+static int g_tr_n = 0, g_tr_cap = 0;
+static float* tr_rec(float code) {
+  if (!g_tr || g_tr_n >= g_tr_cap) return NULL;
+  float* r = g_tr + 24 * g_tr_n++;
+  for (int i = 0; i < 24; i++) r[i] = 0.0f;
+  r[0] = code;
+  return r;
+}
+
 /* RayMarch (:302-384). `ray` is inout: in-volume refraction mutates it (:361). */
 static isect_t march(const ctx_t* c, ray_t* ray, cnt_t* k, uint32_t* steps, uint32_t* flags) {
   isect_t miss;
@@ -353,6 +366,12 @@ static isect_t march(const ctx_t* c, ray_t* ray, cnt_t* k, uint32_t* steps, uint
         internalReflection++;
         if (internalReflection > 10) { ray->dir = oldDir; ray->voxel = 0; }
       }
+      float* r = tr_rec(10.0f);
+      if (r) {
+        r[1] = (float)index; r[2] = cur.x; r[3] = cur.y; r[4] = cur.z; r[5] = rayLength;
+        r[6] = ray->dir.x; r[7] = ray->dir.y; r[8] = ray->dir.z; r[9] = (float)ray->voxel;
+        r[10] = ray->energy; r[11] = (float)it;
+      }
       rayVoxel = ray->voxel;
       t = vdiv(sub(next_plane(ray->dir, cur), ray->pos), ray->dir);
       stepDir = sign3(ray->dir);
@@ -378,7 +397,17 @@ static v3 skybox(const ctx_t* c, const ray_t* ray, v3 color) {
 /* TraceWithShadow (:395-423) */
 static isect_t trace_with_shadow(const ctx_t* c, ray_t* ray, v3* color, cnt_t* k,
                                  uint32_t* steps, uint32_t* flags) {
+  float* tr = tr_rec(1.0f);
+  if (tr) {
+    tr[9] = ray->pos.x; tr[10] = ray->pos.y; tr[11] = ray->pos.z; tr[12] = ray->dir.x; tr[13] = ray->dir.y;
+    tr[14] = ray->dir.z; tr[15] = ray->len; tr[16] = ray->energy; tr[17] = (float)ray->voxel;
+    tr[18] = (float)ray->rdepth; tr[19] = (float)ray->tdepth;
+  }
   isect_t is = march(c, ray, k, steps, flags);
+  if (tr) {
+    tr[1] = (float)is.found; tr[2] = (float)is.voxel; tr[3] = (float)is.index; tr[4] = is.point.x;
+    tr[5] = is.point.y; tr[6] = is.point.z; tr[7] = is.len;
+  }
   if (is.found) {
     ray_t sr;   /* GetShadowRay :191-201 */
     sr.voxel = is.voxel;
@@ -559,6 +588,38 @@ EXPORT int oracle_render(const vrt_camera* cam, const uint8_t* vox, int n, const
   if (counters)
     for (int q = 0; q < VRT_CNT_COUNT; q++) counters[q] += j.total.c[q];
   return VRT_OK;
+}
+
+/* Debug: the ray tree of pixel (px, frame row py) as 24-float records (see tr_rec), at most cap;
+ * returns the record count (<0: error), rgba the pixel's colour. */
+EXPORT int oracle_trace_pixel(const vrt_camera* cam, const uint8_t* vox, int n, const vrt_params* p, int px,
+                              int py, float* out, int cap, float rgba[4]) {
+  if (!cam || !vox || !p || !out || !p->color_only) return VRT_ERR_INVALID;
+  ctx_t c;
+  memset(&c, 0, sizeof c);
+  c.vox = vox;
+  c.n = n;
+  c.fn = (float)n;
+  c.sun = mk(p->sun_dir[0], p->sun_dir[1], p->sun_dir[2]);
+  c.time = p->time;
+  c.ray_noise = p->ray_noise;
+  c.refl_noise = p->reflection_noise;
+  c.refr_noise = p->refraction_noise;
+  c.max_len = p->max_ray_length;
+  c.max_refl = p->max_reflections;
+  c.max_transp = p->max_transparencies;
+  c.inv_pv = cam->inv_pv;
+  c.width = cam->width;
+  c.height = cam->height;
+  cnt_t k;
+  memset(&k, 0, sizeof k);
+  vrt_hit h;
+  g_tr = out;
+  g_tr_n = 0;
+  g_tr_cap = cap;
+  shade_pixel(&c, px, py, rgba, &h, &k);
+  g_tr = NULL;
+  return g_tr_n;
 }
 
 /* Trace ONE ray through RayMarch (for hand-built DDA known-answer tests). Returns found. */

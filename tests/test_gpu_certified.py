@@ -18,10 +18,13 @@ import voxelraytracer_amd as vrt
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def renderer(built):
+@pytest.fixture(scope="module", params=["trees", "no_trees"])
+def renderer(built, request):
     r = vrt.Renderer(0)
     r.set_certified(1)   # every case below exercises the certified walks, whatever the scene
+    # ... with certified bounce trees forced on (every glass pixel tries one) and off
+    r.tree_mode = 2 if request.param == "trees" else 0
+    r.set_cert_trees(r.tree_mode)
     yield r
     r.close()
 
@@ -128,16 +131,17 @@ def test_certified_glass_scenes(renderer, seed):
 
 
 def test_certified_modes(renderer):
-    """Automatic mode: with certified bounce trees (ABI v15, the default) always on; without them on
-    unless glass is > 1/8 of the non-empty voxels (the glass cube). Every mode, with and without
-    trees, renders the same image."""
+    """Automatic mode: on unless glass is > 1/8 of the non-empty voxels (the glass cube), and with
+    certified bounce trees (ABI v15: automatic, i.e. for exactly those volumes, or always) on for
+    every volume. Every mode, with and without trees, renders the same image."""
     try:
         for scene, n, auto in (("glass_cube", 64, False), ("refraction", 64, True), ("terrain", 128, True)):
             vox = vrt.build_scene(scene, n)
             renderer.upload_volume(vox, n)
             renderer.set_certified(0)
-            renderer.set_cert_trees(1)
-            assert renderer.certified()
+            for trees in (1, 2):
+                renderer.set_cert_trees(trees)
+                assert renderer.certified()
             renderer.set_cert_trees(0)
             assert renderer.certified() == auto, scene
             renderer.set_certified(-1)
@@ -145,7 +149,7 @@ def test_certified_modes(renderer):
             cam = vrt.make_camera(96, 64)
             p = vrt.default_params(4, 4)
             imgs = []
-            for trees in (0, 1):
+            for trees in (0, 1, 2):
                 renderer.set_cert_trees(trees)
                 for mode in (-1, 0, 1):
                     renderer.set_certified(mode)
@@ -155,10 +159,10 @@ def test_certified_modes(renderer):
         with pytest.raises(vrt.VrtError):
             renderer.set_certified(2)
         with pytest.raises(vrt.VrtError):
-            renderer.set_cert_trees(2)
+            renderer.set_cert_trees(3)
     finally:
         renderer.set_certified(1)
-        renderer.set_cert_trees(1)
+        renderer.set_cert_trees(renderer.tree_mode)
 
 
 @pytest.mark.parametrize("seed", range(4))

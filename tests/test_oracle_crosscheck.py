@@ -106,3 +106,25 @@ def test_texture_coordinate_known_answers(built):
     # colour-only mode returns the material table colour (:71-87)
     assert np.allclose(oracle.get_color(atlas, S, 128, 3, pt, 2, textured=False),
                        [0.05, 0.5, 0.1, 1.0])
+
+
+def test_oracle_trace_pixel(built):
+    """The oracle's per-pixel ray-tree trace (debug tooling for certified trees): the traced pixel's
+    colour equals oracle.render's, and a glass pixel of the glass cube traces its primary hit, its
+    refraction ray's in-volume refraction out of the wall and its reflection ray, DFS order."""
+    import oracle
+    import voxelraytracer_amd as vrt
+
+    n, w, h = 16, 40, 30
+    vox = vrt.build_scene("glass_cube", n)
+    cam = vrt.make_camera(w, h)
+    p = vrt.default_params(1, 2)
+    img, _, _ = oracle.render(cam, vox, n, p)
+    for px, py in ((3, 4), (20, 15), (37, 27)):
+        recs, rgba = oracle.trace_pixel(cam, vox, n, p, px, py)
+        assert np.array_equal(rgba.view(np.uint32), img[py, px].view(np.uint32))
+        calls = recs[recs[:, 0] == 1]
+        assert calls[0, 1] == 1 and calls[0, 2] == 2          # the primary hits glass
+        assert calls[1, 17] == 2 and calls[1, 19] == 1        # popped first: the refraction ray
+        assert (recs[:, 0] == 10).any()                       # it leaves the wall by in-volume refraction
+        assert calls[2, 18] == 1                               # then the reflection ray

@@ -82,3 +82,45 @@ def test_abi_capacity_never_drops():
     for seed in range(300):
         for R, T in [(4, 4), (8, 8), (12, 4)]:
             assert reference_order(seed, R + T + 1, R, T)[1] == 0
+
+
+def cert_tree_order(seed, R, T):
+    """cert_tree (vrt_render.hip): the ray the reference pops next is held in registers, a
+    reflection ray pushed under a refraction ray waits in ONE per-lane LDS slot; a tree that needs a
+    second waiting ray gives up (None: the pixel takes the exact path)."""
+    ray = ("p", 0, 0)
+    order, pending = [ray[0]], None
+    while True:
+        name, rd, td = ray
+        refl, refr = tree_children(seed, name)
+        pr, pt = refl and rd < R, refr and td < T
+        if pr and pt:
+            if pending is not None:
+                return None
+            pending = (name + "r", rd + 1, td)
+            ray = (name + "t", rd, td + 1)
+        elif pr:
+            ray = (name + "r", rd + 1, td)
+        elif pt:
+            ray = (name + "t", rd, td + 1)
+        else:
+            if pending is None:
+                break
+            ray, pending = pending, None
+        order.append(ray[0])
+    return order
+
+
+@pytest.mark.parametrize("R,T", [(0, 0), (1, 2), (4, 2), (4, 4), (8, 8), (12, 4)])
+def test_cert_tree_order_matches_reference(R, T):
+    """Every tree cert_tree keeps (one waiting ray at most) is folded in the reference's DFS order.
+    (The BASELINE frames' glass trees never need a second slot: a refraction ray leaves C1's one-voxel
+    wall or C3's glass voxel into air or out of the volume, so only the primary hit has two
+    children.)"""
+    kept = 0
+    for seed in range(400):
+        got = cert_tree_order(seed, R, T)
+        if got is not None:
+            kept += 1
+            assert got == reference_order(seed, R + T + 1, R, T)[0], seed
+    assert kept > 0

@@ -302,10 +302,10 @@ class Renderer:
         bands of at least two rounds of resident waves), 2 always. Images are identical."""
         self._check(self._lib.vrt_set_exact_pass(self._h, int(mode)), "vrt_set_exact_pass")
 
-    def set_cert_trees(self, on):
-        """Certified bounce trees of glass pixels (ABI v15): True/1 on (default), False/0 off.
-        Images are identical."""
-        self._check(self._lib.vrt_set_cert_trees(self._h, int(on)), "vrt_set_cert_trees")
+    def set_cert_trees(self, mode):
+        """Certified bounce trees of glass pixels (ABI v15): 1 automatic (default: glass-heavy
+        volumes), 2 always, 0 off. Images are identical."""
+        self._check(self._lib.vrt_set_cert_trees(self._h, int(mode)), "vrt_set_cert_trees")
 
     def volume_device_ptr(self) -> int:
         return self._lib.vrt_volume_device_ptr(self._h) or 0

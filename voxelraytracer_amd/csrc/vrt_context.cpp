@@ -437,10 +437,11 @@ vrt::KArgs make_args(const vrt_ctx* ctx, const Shard& s, const vrt_camera* cam, 
   a.prev = nullptr;
   a.cur = nullptr;
   a.raw = nullptr;
-  // automatic mode: certified pixels unless glass dominates the volume, or always with certified
-  // bounce trees (which settle the glass pixels too)
-  a.cert = s.octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || s.cert_auto || ctx->tree_req ? 2 : 1);
-  a.tree = a.cert == 2 && p->color_only && ctx->tree_req ? 1 : 0;
+  // automatic mode: certified pixels unless glass dominates the volume, where certified bounce
+  // trees (automatic: exactly those volumes) settle the glass pixels instead
+  const bool trees = ctx->tree_req == 2 || (ctx->tree_req == 1 && !s.cert_auto);
+  a.cert = s.octants != 8 || ctx->cert_req < 0 ? 0 : (ctx->cert_req > 0 || s.cert_auto || trees ? 2 : 1);
+  a.tree = a.cert == 2 && p->color_only && trees ? 1 : 0;
   a.tiles_x = uint32_t((a.width + vrt::kTileW - 1) / vrt::kTileW);
   a.tiles = a.tiles_x * uint32_t((a.rows + vrt::kTileH - 1) / vrt::kTileH);
   a.order = nullptr;
@@ -1347,12 +1348,12 @@ int vrt_set_certified(vrt_ctx* ctx, int32_t mode) {
 int vrt_certified(const vrt_ctx* ctx) {
   if (!ctx) return VRT_ERR_INVALID;
   const Shard& s = ctx->sh[0];
-  return s.octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || s.cert_auto || ctx->tree_req) ? 1 : 0;
+  return s.octants == 8 && ctx->cert_req >= 0 && (ctx->cert_req > 0 || s.cert_auto || ctx->tree_req != 0) ? 1 : 0;
 }
 
 int vrt_set_cert_trees(vrt_ctx* ctx, int32_t on) {
   if (!ctx) return VRT_ERR_INVALID;
-  if (on < 0 || on > 1) return fail(ctx, VRT_ERR_INVALID, "certified trees must be 0 or 1");
+  if (on < 0 || on > 2) return fail(ctx, VRT_ERR_INVALID, "certified trees must be 0, 1 or 2");
   ctx->tree_req = on;
   ctx->err.clear();
   return VRT_OK;

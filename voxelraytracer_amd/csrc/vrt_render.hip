@@ -38,6 +38,21 @@
 #ifndef VRT_DIAG_PHASE
 #define VRT_DIAG_PHASE 9
 #endif
+// VRT_TREE_CUT (diagnostic builds only; images stay exact): certified trees give up (exact path)
+// at bit 0 reflection children, bit 1 refraction children, bit 2 in-volume refraction restarts
+#if defined(VRT_TREE_CUT) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_TREE_CUT is a diagnostic build: use make variant"
+#endif
+#ifndef VRT_TREE_CUT
+#define VRT_TREE_CUT 0
+#endif
+// VRT_PREFIX (A/B builds only): 0 turns off the certified prefix of the exact primary walk
+#if defined(VRT_PREFIX) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_PREFIX is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_PREFIX
+#define VRT_PREFIX 1
+#endif
 
 namespace vrt {
 
@@ -530,10 +545,13 @@ constexpr float kSkipMargin = 1.0f / 256.0f;
 
 // LEN0Z: the caller guarantees len0 == +0 (the primary ray, voxel.glsl:430), so
 // s = rayLength - ray.rayLength is rayLength itself (x - (+0) == x): one VALU less per step.
+// s_init > 0: a first skip window [0, s_init) known from a certified walk of the same ray
+// (CertResult::us: every crossing before it settled, each in the volume and not an event), so
+// those steps replay only the state update; else the first step samples.
 template <bool SHADOW, bool STATS, bool LEN0Z = false>
 __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 dir, const f3 rcp,
                                          float len0, uint32_t medium, WalkState& w, int& axis_out,
-                                         int32_t& vidx_out, uint32_t& v_out) {
+                                         int32_t& vidx_out, uint32_t& v_out, float s_init = -1.0f) {
   // fast path: every dir component is non-zero, so sign(d) = copysign(1, d)
   const f3 step = mk(__builtin_copysignf(1.0f, dir.x), __builtin_copysignf(1.0f, dir.y),
                      __builtin_copysignf(1.0f, dir.z));
@@ -557,6 +575,7 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
   // Skip windows also end where the length test could first fail: s = fl(len - len0) is
   // monotone in len, so s < fl(max_len - len0) implies len < max_len (NaN: no window at all).
   const float s_len = LEN0Z ? c.max_len : c.max_len - len0;
+  float s_first = VRT_PREFIX && s_init > 0.0f ? __builtin_fminf(s_init, s_len) : -1.0f;
   f3 t = w.t;
   float len = w.len;
   uint32_t it = w.it, ties = w.ties;
@@ -591,7 +610,8 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
     // recorded by the stopping (sampled) step only; lanes that leave on the bound: no event
     uint32_t x_v = SHADOW ? 0u : medium, x_axis = 0u, x_out = 0u;  // x_out: sample was outside
     int32_t x_vidx = -1;
-    float s_lim = -1.0f;  // no skip window yet: the first step samples
+    float s_lim = s_first;  // no skip window yet (-1: the first step samples), or the certified prefix
+    s_first = -1.0f;
     for (;;) {
       if (k >= k_max) break;  // wave-uniform step bound (scalar branch)
       ++k;
@@ -685,10 +705,10 @@ __device__ __forceinline__ int skip_walk(const Ctx& c, const f3 pos, const f3 di
 template <bool STATS>
 __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir, float len0,
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
-                                        uint32_t& v) {
+                                        uint32_t& v, float s_init = -1.0f) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
     const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
-    return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v);
+    return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v, s_init);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
 }
@@ -797,8 +817,10 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
 
 // RayMarch (voxel.glsl:302-384); `ray` is inout (in-volume refraction rewrites it, :361)
 // PRIMARY: the primary ray (len 0, medium air: every event is a hit, no in-volume refraction)
+// s_init (PRIMARY only): the certified prefix of the primary walk (skip_walk)
 template <bool STATS, bool TEX, bool PRIMARY = false>
-__device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags) {
+__device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags,
+                     float s_init = -1.0f) {
   Hit h;
   h.found = false;
   h.vidx = -1;
@@ -816,7 +838,8 @@ __device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint3
     int axis;
     int32_t vidx;
     uint32_t v;
-    r = walk_ray<STATS>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v);
+    r = walk_ray<STATS>(c, ray.pos, ray.dir, ray.len, PRIMARY ? 0u : medium, w, axis, vidx, v,
+                        PRIMARY ? s_init : -1.0f);
     if (r != WALK_EVENT) break;
     f3 normal = mk(0.0f, 0.0f, 0.0f);
     set_comp(normal, axis, -gsign(comp(ray.dir, axis)));
@@ -936,8 +959,8 @@ __device__ __forceinline__ void shade(const Ctx& c, const Ray& ray, const Hit& h
 // TraceWithShadow (voxel.glsl:395-423) and the colour update it performs
 template <bool STATS, bool TEX, bool PRIMARY = false, bool CSH = false>
 __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& color, Counters& k,
-                                                 uint32_t& steps, uint32_t& flags) {
-  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags);
+                                                 uint32_t& steps, uint32_t& flags, float s_init = -1.0f) {
+  const Hit h = march<STATS, TEX, PRIMARY>(c, ray, k, steps, flags, s_init);
   shade<STATS, TEX, CSH>(c, ray, h, color, k, steps, flags);
   return h;
 }
@@ -973,7 +996,7 @@ __device__ __forceinline__ Hit trace_with_shadow(const Ctx& c, Ray& ray, f3& col
 // (-2 % at C3, profiles/r01_v45_ab_wave_priority.log).
 constexpr int kStackPrio = 3;
 #ifdef VRT_CERT_DIAG  // diagnostic build only (scripts/cert_diag.py): outcome counts per pixel
-__device__ unsigned long long g_cert_diag[16];
+__device__ unsigned long long g_cert_diag[32];
 #define CERT_DIAG(i) atomicAdd(&g_cert_diag[i], 1ull)
 __device__ __forceinline__ void cert_diag_iters(int slot, int it) {
   atomicAdd(&g_cert_diag[slot], (unsigned long long)it);
@@ -998,6 +1021,9 @@ struct CertResult {
   int cx, cy, cz;  // hit cell
   float u;         // crossing parameter of the hit
   float eu;        // bound of the exact walk's parameter error there
+  // every step of the exact walk with parameter s < us samples an in-volume cell that is not an
+  // event (the certified crossings before the last one the walk settled); 0: none known
+  float us;
 #ifdef VRT_CERT_DIAG
   int iters;
 #endif
@@ -1044,6 +1070,7 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   r.cx = r.cy = r.cz = 0;
   r.u = 0.0f;
   r.eu = 0.0f;
+  r.us = 0.0f;
   const int sx = D.x > 0.0f ? 1 : -1, sy = D.y > 0.0f ? 1 : -1, sz = D.z > 0.0f ? 1 : -1;
   const int ux = D.x > 0.0f ? 1 : 0, uy = D.y > 0.0f ? 1 : 0, uz = D.z > 0.0f ? 1 : 0;
   const f3 ar = mk(__builtin_fabsf(rcp.x), __builtin_fabsf(rcp.y), __builtin_fabsf(rcp.z));
@@ -1137,6 +1164,9 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
     // second smallest sig bounds every sig_b, b != a, from below, the latest back every back_b from
     // above, and ga + max gam every ga + gam_b; rounding is monotone), the flags only if it holds.
     const float tg = ga + gmax(gam.x, gmax(gam.y, gam.z));
+    // the crossings up to prev are settled (this one, at s1, may not be): an exact step at s <
+    // prev - tg has its real crossing before prev (gam_b <= tg), so it samples a settled cell
+    r.us = prev - tg - 1e-3f;
     uint32_t nf = 0u;
     if (__builtin_amdgcn_fmed3f(sig.x, sig.y, sig.z) - s1 < tg || s1 - mback < tg) {
       const bool ahx = a != 0 && sig.x - s1 < ga + gam.x, ahy = a != 1 && sig.y - s1 < ga + gam.y,
@@ -1321,14 +1351,17 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
   uint32_t medium = ray.voxel;
   int internal = 0;
   for (int seg = 0; seg < 32; ++seg) {
-    if (!fast_path_ok(ray.dir) || !(e0 < kCertMaxOrigin)) return h;
+    if (!fast_path_ok(ray.dir) || !(e0 < kCertMaxOrigin)) { CERT_DIAG(24); return h; }
     const f3 rcp = mk(__builtin_amdgcn_rcpf(ray.dir.x), __builtin_amdgcn_rcpf(ray.dir.y),
                       __builtin_amdgcn_rcpf(ray.dir.z));
     h = cert_walk<false>(c, ray.pos, ray.dir, rcp, c.max_len - ray.len, cx, cy, cz, e0, ed, ray.len,
                          medium);
+    if (h.res == CERT_UNSURE) CERT_DIAG(25);
     if (h.res != CERT_HIT || h.byte != 0u) return h;
+    CERT_DIAG(30);
     // in-volume refraction at the crossing into the air cell (h.cx, h.cy, h.cz)
     h.res = CERT_UNSURE;
+    if (VRT_TREE_CUT & 4) return h;
     const Hit eh = cert_hit_record(ray, h);
     const f3 D0 = ray.dir;
     // the probes at point +- normal/2 (:219-220) read the exact point's cells if the point is
@@ -1339,16 +1372,20 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
                      h.eu * __builtin_fabsf(D0.z) + 2e-5f);
     if ((h.axis != 0 && !(fr.x >= dm.x && 1.0f - fr.x >= dm.x)) ||
         (h.axis != 1 && !(fr.y >= dm.y && 1.0f - fr.y >= dm.y)) ||
-        (h.axis != 2 && !(fr.z >= dm.z && 1.0f - fr.z >= dm.z)))
+        (h.axis != 2 && !(fr.z >= dm.z && 1.0f - fr.z >= dm.z))) {
+      CERT_DIAG(26);
       return h;
+    }
     // position-independent directions only (RandomizeDirection's zero-noise identity)
     const float eta = mat_refr(get_voxel(c, eh.point + eh.normal * 0.5f)) /
                       mat_refr(get_voxel(c, eh.point - eh.normal * 0.5f));
     const f3 rd = refract3(normalize3(D0), eh.normal, eta);
     const bool tir = rd.x == 0.0f && rd.y == 0.0f && rd.z == 0.0f;
     if (tir ? !(c.refl_noise == 0.0f && zero_noise_exact(reflect3(D0, eh.normal)))
-            : !(c.refr_noise == 0.0f && zero_noise_exact(rd)))
+            : !(c.refr_noise == 0.0f && zero_noise_exact(rd))) {
+      CERT_DIAG(27);
       return h;
+    }
     Counters kk;
 #pragma unroll
     for (int q = 0; q < VRT_CNT_COUNT; ++q) kk.c[q] = 0;
@@ -1365,11 +1402,11 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
     // restart cell: the crossed cell, or the one before it when the direction turned back
     int nx = h.cx, ny = h.cy, nz = h.cz;
     if ((comp(nr.dir, h.axis) > 0.0f) != (comp(D0, h.axis) > 0.0f)) cell_before(h, D0, nx, ny, nz);
-    if (!fast_path_ok(nr.dir)) return h;
+    if (!fast_path_ok(nr.dir)) { CERT_DIAG(28); return h; }
     const f3 rcpn = mk(__builtin_amdgcn_rcpf(nr.dir.x), __builtin_amdgcn_rcpf(nr.dir.y),
                        __builtin_amdgcn_rcpf(nr.dir.z));
     f3 edn;
-    if (!cert_start(eh.point, D0, nr.dir, rcpn, h.axis, h.eu, nx, ny, nz, edn)) return h;
+    if (!cert_start(eh.point, D0, nr.dir, rcpn, h.axis, h.eu, nx, ny, nz, edn)) { CERT_DIAG(28); return h; }
     ray = nr;
     const uint32_t n = uint32_t(c.n);
     if (uint32_t(nx) >= n || uint32_t(ny) >= n || uint32_t(nz) >= n) {
@@ -1383,6 +1420,7 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
     e0 = h.eu;
     ed = edn;
   }
+  CERT_DIAG(29);
   h.res = CERT_UNSURE;
   return h;
 }
@@ -1402,8 +1440,7 @@ __device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz,
 // A ray in flight is a TreeRay: the Ray the reference would carry (pos and len approximate, dir,
 // energy, medium and depths exact) plus its certified start. The DFS keeps the ray the reference
 // pops next in registers (the last-pushed child), so only a reflection ray pushed under a
-// refraction ray waits, in one per-lane LDS slot (component-major, conflict-free ds_write_b32); a
-// tree that would hold two such rays at once (never at the BASELINE configs: one glass voxel or
+// refraction ray waits, in one per-lane LDS slot; a tree that would hold two such rays at once (never at the BASELINE configs: one glass voxel or
 // one-voxel glass walls) goes to the exact path.
 struct TreeRay {
   Ray ray;
@@ -1411,39 +1448,36 @@ struct TreeRay {
   float e0;        // origin uncertainty (parameter along the parent)
   f3 ed;           // per-axis crossing-order uncertainty from it
 };
+// The slot: 12 words in the lane's own 3 float4s (lane-major; in the in-lane instances the exact
+// walk's axis table, c.ax) and 2 words component-major at b[0], b[NL] (there the bounce stack's
+// bottom entry): both regions belong to this lane alone, and it is done with the tree before its
+// exact path (if any) uses them. (A slot striped over the whole workgroup's pool would overwrite
+// the other wave's axis table in the middle of its exact walks.)
 constexpr int kTreeWords = 14;
 template <int NL>
-__device__ __forceinline__ void tree_put(float* __restrict__ b, const TreeRay& t) {
-  b[0 * NL] = t.ray.pos.x;
-  b[1 * NL] = t.ray.pos.y;
-  b[2 * NL] = t.ray.pos.z;
-  b[3 * NL] = t.ray.dir.x;
-  b[4 * NL] = t.ray.dir.y;
-  b[5 * NL] = t.ray.dir.z;
-  b[6 * NL] = t.ray.len;
-  b[7 * NL] = t.ray.energy;
-  b[8 * NL] = t.e0;
-  b[9 * NL] = t.ed.x;
-  b[10 * NL] = t.ed.y;
-  b[11 * NL] = t.ed.z;
+__device__ __forceinline__ void tree_put(float4* __restrict__ a, float* __restrict__ b, const TreeRay& t) {
+  a[0] = make_float4(t.ray.pos.x, t.ray.pos.y, t.ray.pos.z, t.ray.dir.x);
+  a[1] = make_float4(t.ray.dir.y, t.ray.dir.z, t.ray.len, t.ray.energy);
+  a[2] = make_float4(t.e0, t.ed.x, t.ed.y, t.ed.z);
   // cells in [0, 1024); a stored ray is a reflection ray: medium air
-  b[12 * NL] = __uint_as_float(uint32_t(t.cx) | uint32_t(t.cy) << 10 | uint32_t(t.cz) << 20);
-  b[13 * NL] = __uint_as_float(uint32_t(t.ray.rdepth) | uint32_t(t.ray.tdepth) << 16);
+  b[0] = __uint_as_float(uint32_t(t.cx) | uint32_t(t.cy) << 10 | uint32_t(t.cz) << 20);
+  b[NL] = __uint_as_float(uint32_t(t.ray.rdepth) | uint32_t(t.ray.tdepth) << 16);
 }
 template <int NL>
-__device__ __forceinline__ TreeRay tree_get(const float* __restrict__ b) {
+__device__ __forceinline__ TreeRay tree_get(const float4* __restrict__ a, const float* __restrict__ b) {
   TreeRay t;
-  t.ray.pos = mk(b[0 * NL], b[1 * NL], b[2 * NL]);
-  t.ray.dir = mk(b[3 * NL], b[4 * NL], b[5 * NL]);
-  t.ray.len = b[6 * NL];
-  t.ray.energy = b[7 * NL];
-  t.e0 = b[8 * NL];
-  t.ed = mk(b[9 * NL], b[10 * NL], b[11 * NL]);
-  const uint32_t w = __float_as_uint(b[12 * NL]);
+  const float4 a0 = a[0], a1 = a[1], a2 = a[2];
+  t.ray.pos = mk(a0.x, a0.y, a0.z);
+  t.ray.dir = mk(a0.w, a1.x, a1.y);
+  t.ray.len = a1.z;
+  t.ray.energy = a1.w;
+  t.e0 = a2.x;
+  t.ed = mk(a2.y, a2.z, a2.w);
+  const uint32_t w = __float_as_uint(b[0]);
   t.cx = int(w & 1023u);
   t.cy = int((w >> 10) & 1023u);
   t.cz = int((w >> 20) & 1023u);
-  const uint32_t dp = __float_as_uint(b[13 * NL]);
+  const uint32_t dp = __float_as_uint(b[NL]);
   t.ray.rdepth = int(dp & 0xffffu);
   t.ray.tdepth = int(dp >> 16);
   t.ray.voxel = 0u;
@@ -1456,7 +1490,7 @@ __device__ __forceinline__ bool tree_start(const Ctx& c, const CertResult& h, co
                                            TreeRay& t) {
   if (!fast_path_ok(t.ray.dir)) return false;
   const uint32_t n = uint32_t(c.n);
-  if (uint32_t(t.cx) >= n || uint32_t(t.cy) >= n || uint32_t(t.cz) >= n) return false;
+  if (uint32_t(t.cx) >= n || uint32_t(t.cy) >= n || uint32_t(t.cz) >= n) { CERT_DIAG(31); return false; }
   const f3 rn = mk(__builtin_amdgcn_rcpf(t.ray.dir.x), __builtin_amdgcn_rcpf(t.ray.dir.y),
                    __builtin_amdgcn_rcpf(t.ray.dir.z));
   t.e0 = h.eu;
@@ -1469,6 +1503,7 @@ template <bool TEX>
 __device__ __forceinline__ bool tree_reflection(const Ctx& c, const Ray& ray, const CertResult& h, const Hit& hh,
                                                 TreeRay& t) {
   if (!(c.refl_noise == 0.0f && zero_noise_exact(reflect3(ray.dir, hh.normal)))) return false;
+  if (VRT_TREE_CUT & 1) return false;
   t.ray = reflection_ray(c, ray, hh);
   cell_before(h, ray.dir, t.cx, t.cy, t.cz);
   return tree_start(c, h, hh, ray.dir, t);
@@ -1480,6 +1515,7 @@ __device__ __forceinline__ bool tree_reflection(const Ctx& c, const Ray& ray, co
 template <bool TEX>
 __device__ __forceinline__ bool tree_refraction(const Ctx& c, const Ray& ray, const CertResult& h, const Hit& hh,
                                                 TreeRay& t) {
+  if (VRT_TREE_CUT & 2) return false;
   const float eta = mat_refr(get_voxel(c, hh.point + hh.normal * 0.5f)) /
                     mat_refr(get_voxel(c, hh.point - hh.normal * 0.5f));
   const f3 rd = refract3(normalize3(ray.dir), hh.normal, eta);
@@ -1500,17 +1536,21 @@ __device__ __forceinline__ bool tree_refraction(const Ctx& c, const Ray& ray, co
 
 // The bounce tree of a glass primary hit h0 of ray0 (fragment main, voxel.glsl:425-452) by
 // certified walks, colour folded in the reference's DFS order as TraceWithShadow does (:395-423):
-// each ray's RayMarch by cert_march, its hit shaded with a certified shadow (none for glass),
-// a miss with the sky colour. Colour-only (TEX false) frames. Returns false, colour untouched,
-// when any walk, start or direction could differ from the exact path's.
-// lts: this lane's word 0 of the LDS slot (NL lanes per workgroup).
+// each ray's RayMarch by cert_march, its hit shaded with a certified shadow (none for glass), a
+// miss with the sky colour. Colour-only (TEX false) frames. Returns false, colour untouched, when
+// any walk, start or direction could differ from the exact path's.
+// (Walking the primary ray through this loop too, one walk call site for every ray, made the
+// certified pass 3x slower: every pixel then carried the tree's registers; r06_s4.)
+// lta / ltb: this lane's LDS slot (tree_put; NL lanes per workgroup).
 template <int NL>
 __device__ __forceinline__ bool cert_tree(const Ctx& c, int max_refl, int max_transp, const Ray& ray0,
-                                          const CertResult& h0, f3& color_out, float* __restrict__ lts) {
+                                          const CertResult& h0, f3& color_out, float4* __restrict__ lta,
+                                          float* __restrict__ ltb) {
   f3 color = mk(0.0f, 0.0f, 0.0f);
   Ray ray = ray0;
   CertResult h = h0;
   bool pending = false;  // a reflection ray waits in the LDS slot
+  CERT_DIAG(16);
   for (;;) {
     bool next = false;
     TreeRay t;
@@ -1518,37 +1558,39 @@ __device__ __forceinline__ bool cert_tree(const Ctx& c, int max_refl, int max_tr
       apply_sky_color(c, ray, color);
     } else {
       const Hit hh = cert_hit_record(ray, h);
-      if (!cert_shade_hit<false>(c, ray, h, hh, color)) return false;
+      if (!cert_shade_hit<false>(c, ray, h, hh, color)) { CERT_DIAG(22); return false; }
       // children (:440-448): the reflection ray is pushed first, the refraction ray second and
       // popped first; the stack (R + T + 1 entries) never fills with at most one ray waiting
       const uint32_t m = mat_id(h.byte);
       const bool pr = mat_reflective(m) && ray.rdepth < max_refl;
       const bool pt = mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f;
       if (pr && pt) {
-        if (pending) return false;
+        if (pending) { CERT_DIAG(18); return false; }
         TreeRay r;
-        if (!tree_reflection<false>(c, ray, h, hh, r)) return false;
-        tree_put<NL>(lts, r);
+        if (!tree_reflection<false>(c, ray, h, hh, r)) { CERT_DIAG(19); return false; }
+        tree_put<NL>(lta, ltb, r);
         pending = true;
-        if (!tree_refraction<false>(c, ray, h, hh, t)) return false;
+        if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return false; }
         next = true;
       } else if (pr) {
-        if (!tree_reflection<false>(c, ray, h, hh, t)) return false;
+        if (!tree_reflection<false>(c, ray, h, hh, t)) { CERT_DIAG(19); return false; }
         next = true;
       } else if (pt) {
-        if (!tree_refraction<false>(c, ray, h, hh, t)) return false;
+        if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return false; }
         next = true;
       }
     }
     if (!next) {
       if (!pending) break;
       pending = false;
-      t = tree_get<NL>(lts);
+      t = tree_get<NL>(lta, ltb);
     }
     ray = t.ray;
     h = cert_march(c, ray, t.cx, t.cy, t.cz, t.e0, t.ed);
-    if (h.res == CERT_UNSURE) return false;
+    if (h.res == CERT_UNSURE) { CERT_DIAG(21); return false; }
+    CERT_DIAG(23);
   }
+  CERT_DIAG(17);
   color_out = color;
   return true;
 }
@@ -1819,11 +1861,13 @@ __device__ __forceinline__ bool cert_texel(const Ctx& c, const Ray& ray, const C
   return true;
 }
 
-// TREE (colour-only): a glass primary hit's bounce tree by certified walks too (cert_tree; lts its
+// TREE (colour-only): a glass primary hit's bounce tree by certified walks too (cert_tree; ltb and c.ax its
 // LDS slot), instead of leaving the whole pixel to the exact path.
+// us_out: the primary walk's certified prefix (CertResult::us) for the exact path, -1 if none.
 template <bool TEX = false, bool TREE = false, int NL = kWgThreads>
 __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& color_out, int max_refl = 0,
-                                           int max_transp = 0, float* __restrict__ lts = nullptr) {
+                                           int max_transp = 0, float* __restrict__ ltb = nullptr,
+                                           float* us_out = nullptr) {
   const f3 P = ray0.pos, D = ray0.dir;
   if (VRT_DIAG_PHASE <= 1) {
     color_out = D;
@@ -1839,6 +1883,7 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
   const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
   CertResult h = cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f,
                                   mk(0.0f, 0.0f, 0.0f), 0.0f, 0u);
+  if (us_out) *us_out = h.us;
 #ifdef VRT_CERT_DIAG
   cert_diag_iters(10, h.iters);
 #endif
@@ -1856,7 +1901,7 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
   }
   if (mat_id(h.byte) == 2u) {  // only glass spawns secondary rays (:440-448)
     CERT_DIAG(3);
-    if constexpr (TREE && !TEX) return cert_tree<NL>(c, max_refl, max_transp, ray0, h, color_out, lts);
+    if constexpr (TREE && !TEX) return cert_tree<NL>(c, max_refl, max_transp, ray0, h, color_out, c.ax, ltb);
     return false;
   }
   const Hit hh = cert_hit_record(ray0, h);
@@ -1865,6 +1910,19 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
   if (!cert_shade_hit<TEX>(c, ray0, h, hh, color, col)) return false;
   color_out = color;
   return true;
+}
+
+// The certified prefix of a primary walk for the exact path (the deferred exact pass re-walks the
+// primary ray certified: a few jumps): every exact step before it replays only the DDA state
+// update, without its sample (skip_walk's s_init). -1: none.
+__device__ __forceinline__ float primary_prefix(const Ctx& c, const Ray& ray0) {
+  const f3 P = ray0.pos, D = ray0.dir;
+  int cx, cy, cz;
+  if (!fast_path_ok(D) || !exact_start_cell(c, P, D, cx, cy, cz) ||
+      !start_layers_clear<false>(c, P, D, cx, cy, cz, 0u))
+    return -1.0f;
+  const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
+  return cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f, mk(0.0f, 0.0f, 0.0f), 0.0f, 0u).us;
 }
 
 // ---- RGB8 framebuffer store + temporal filter (oracle/vrt_oracle.c oracle_temporal) ----------
@@ -2157,11 +2215,12 @@ __device__ unsigned long long g_stamps3[kMaxStampWaves3][2];
 template <bool STATS, bool TEX, bool CSH = false, bool CSEC = false, int NL = kWgThreads>
 __device__ __forceinline__ bool exact_pixel(const KArgs& a, const Ctx& c, Ray ray, f3& color,
                                             Counters& k, uint32_t& steps, uint32_t& flags,
-                                            int32_t& hit_vidx, float& hit_len, float* __restrict__ lstk) {
+                                            int32_t& hit_vidx, float& hit_len, float* __restrict__ lstk,
+                                            float s_init = -1.0f) {
   StackRay stack[kMaxStack - 1 - VRT_LDS_STACK];  // the top entry lives in `ray`, the bottom one in LDS
   const int cap = a.max_refl + a.max_transp + 1;
   int sp = 0;
-  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags);
+  const Hit h0 = trace_with_shadow<STATS, TEX, true, CSH>(c, ray, color, k, steps, flags, s_init);
 #ifdef VRT_STAMPS
   const uint32_t st_wave = blockIdx.x * kWgWaves + (threadIdx.x >> 6);
   {
@@ -2282,9 +2341,15 @@ __device__ __forceinline__ void store_pixel(const KArgs& a, const FrameView& fv,
 // (it cost C1 4 %, C3 1 %: profiles/r05_s27)
 // TREE (colour-only CERT 2): glass pixels' bounce trees by certified walks (cert_tree), one
 // kTreeWords LDS slot per lane.
+#if defined(VRT_TREE_WAVES) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_TREE_WAVES is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_TREE_WAVES  // resident waves per SIMD of the certified pass with certified trees
+#define VRT_TREE_WAVES 5
+#endif
 template <bool STATS, bool TEX, int CERT = 0, bool ORD = false, bool DEFER = false, bool FB = false,
           bool TREE = false>
-__global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
+__global__ void __launch_bounds__(kWgThreads, TREE ? VRT_TREE_WAVES : (DEFER ? VRT_DEFER_WAVES : VRT_MIN_WAVES)) render_kernel(KArgs a, const uint16_t* __restrict__ vox,
                                                      float4* __restrict__ out,
                                                      vrt_hit* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
@@ -2329,10 +2394,10 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     if constexpr (FB) c.time = frame_view(a, fr).time;
     // one LDS pool: the exact path's axis table and bounce-stack bottom (in-lane instances), and
     // the certified tree's slots (TREE), which are live only before the exact path starts
-    constexpr int kAxFloats = DEFER ? 0 : kWgThreads * 3 * 4;
-    constexpr int kStkFloats = DEFER || !VRT_LDS_STACK ? 0 : kStackWords * kWgThreads;
-    constexpr int kTreeFloats = TREE ? kTreeWords * kWgThreads : 0;
-    constexpr int kPool = std::max(std::max(kAxFloats + kStkFloats, kTreeFloats), 4);
+    constexpr int kAxFloats = DEFER && !TREE ? 0 : kWgThreads * 3 * 4;
+    constexpr int kStkFloats = std::max(DEFER || !VRT_LDS_STACK ? 0 : kStackWords * kWgThreads,
+                                        TREE ? (kTreeWords - 12) * kWgThreads : 0);
+    constexpr int kPool = std::max(kAxFloats + kStkFloats, 4);
     __shared__ float4 lds_pool[kPool / 4];
     c.ax = &lds_pool[threadIdx.x * kAxLane];
 #if VRT_DIAG_PHASE == 0
@@ -2361,9 +2426,10 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
     float* tstk = nullptr;
     if constexpr (TREE) {
       static_assert(CERT == 2 && !TEX && !STATS, "certified trees: stats-free colour-only certified instances");
-      tstk = reinterpret_cast<float*>(lds_pool) + threadIdx.x;
+      tstk = reinterpret_cast<float*>(lds_pool) + kAxFloats + threadIdx.x;   // (and c.ax: tree_put)
     }
-    const bool need_exact = CERT < 2 || !cert_pixel<TEX, TREE>(c, ray, color, a.max_refl, a.max_transp, tstk);
+    float us = -1.0f;  // the primary walk's certified prefix, for the exact path
+    const bool need_exact = CERT < 2 || !cert_pixel<TEX, TREE>(c, ray, color, a.max_refl, a.max_transp, tstk, &us);
 #ifdef VRT_STAMPS
     const unsigned long long t_cert = __builtin_amdgcn_s_memrealtime();
     const unsigned long long n_exact = __builtin_popcountll(__ballot(need_exact));
@@ -2379,7 +2445,7 @@ __global__ void __launch_bounds__(kWgThreads, DEFER ? VRT_DEFER_WAVES : VRT_MIN_
       heavy = true;
       float* lstk = reinterpret_cast<float*>(lds_pool) + kAxFloats;
       (void)exact_pixel<STATS, TEX, CERT >= 1, CERT == 2>(a, c, ray, color, k, steps, flags, hit_vidx,
-                                                         hit_len, &lstk[threadIdx.x]);
+                                                         hit_len, &lstk[threadIdx.x], STATS ? -1.0f : us);
     }
     const uint32_t l2 = lane_id();
     const size_t o = size_t(pixel_row(ty, wave, l2)) * size_t(a.pitch) + size_t(pixel_x(tx, wave, l2));
@@ -2578,7 +2644,8 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     f3 color = mk(0.0f, 0.0f, 0.0f);
     __shared__ float lstk[VRT_LDS_STACK ? kStackWords * 64 : 1];
     (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, 64>(a, c, ray, color, k, steps, flags,
-                                                                    hit_vidx, hit_len, &lstk[lane]);
+                                                                    hit_vidx, hit_len, &lstk[lane],
+                                                                    primary_prefix(c, ray));
     if constexpr (FB) {
       // the pixel and its frame re-derived from e (only e stays live across the exact path)
       uint32_t e2 = e;
@@ -3006,9 +3073,9 @@ void launch_randomize(const float* dir, const float* pos, int n, float randomnes
 #ifdef VRT_CERT_DIAG
 // diagnostic build only: read and reset the certified-walk outcome counts (16 x u64)
 int debug_cert_diag(uint64_t* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cert_diag), 16 * 8) != hipSuccess) return VRT_ERR_DEVICE;
-  static const uint64_t zero[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_cert_diag), zero, 16 * 8) == hipSuccess ? VRT_OK : VRT_ERR_DEVICE;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cert_diag), 32 * 8) != hipSuccess) return VRT_ERR_DEVICE;
+  static const uint64_t zero[32] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cert_diag), zero, 32 * 8) == hipSuccess ? VRT_OK : VRT_ERR_DEVICE;
 }
 #endif
 

@@ -54,6 +54,7 @@ for st in "$@"; do
     fetch) pmc fetch ${arg:-C3} FETCH_SIZE ;;
     waits) pmc waits ${arg:-C3} SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM ;;
     sq) pmc sq ${arg:-C3} SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD ;;
+    util) pmc util ${arg:-C3} SQ_WAVES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
     sca) pmc sca ${arg:-C3} SQ_WAVES SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_INSTS_BRANCH ;;
     trace) run trace_${arg:-C3} 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_${arg:-C3}" -o run --output-format csv -- \
              python3 "$ROOT/bench.py" --config ${arg:-C3} --steps 20 --warmup 3 --cpu-seconds 0 ;;

@@ -1552,13 +1552,19 @@ __device__ __forceinline__ bool cert_tree(const Ctx& c, int max_refl, int max_tr
   bool pending = false;  // a reflection ray waits in the LDS slot
   CERT_DIAG(16);
   for (;;) {
+    // the sun vector opaque per ray, as in the exact path's bounce loop (trace_with_shadow): else
+    // the shadow walk's per-sun products are hoisted into VGPRs live across the whole tree and
+    // spilled on its entry
+    Ctx lc = c;
+    asm volatile("" : "+s"(lc.sun_n.x), "+s"(lc.sun_n.y), "+s"(lc.sun_n.z), "+s"(lc.sun_rcp.x),
+                 "+s"(lc.sun_rcp.y), "+s"(lc.sun_rcp.z));
     bool next = false;
     TreeRay t;
     if (h.res == CERT_MISS) {
       apply_sky_color(c, ray, color);
     } else {
       const Hit hh = cert_hit_record(ray, h);
-      if (!cert_shade_hit<false>(c, ray, h, hh, color)) { CERT_DIAG(22); return false; }
+      if (!cert_shade_hit<false>(lc, ray, h, hh, color)) { CERT_DIAG(22); return false; }
       // children (:440-448): the reflection ray is pushed first, the refraction ray second and
       // popped first; the stack (R + T + 1 entries) never fills with at most one ray waiting
       const uint32_t m = mat_id(h.byte);

@@ -145,3 +145,31 @@ def test_textured_certified_pixels_bit_identical(built, case):
     for t in range(3):
         assert np.array_equal(out["defer"][t], out["exact"][t]), f"deferred, frame {t}"
         assert np.array_equal(out["inlane"][t], out["exact"][t]), f"in-lane, frame {t}"
+
+
+LONE = [("glass_cube", 128, 1920, 1080, 1, 2), ("terrain", 128, 3840, 2160, 4, 2)]
+
+
+@pytest.mark.parametrize("case", LONE, ids=[f"{c[0]}_{c[2]}x{c[3]}" for c in LONE])
+def test_synchronous_frames_deferred(built, case):
+    """vrt_render_frame renders a glass-heavy volume's frame, or a frame of >= 8 rounds of
+    resident waves, as one deferred launch (certified pass + the exact pass's short-band
+    instance); the frames must equal the in-lane path's (exact pass off) and the counted exact
+    instance's, frame after frame through the history (u_Alpha 0.5 and 1)."""
+    scene, n, w, h, R, T = case
+    vox = vrt.build_scene(scene, n)
+    cam = vrt.make_camera(w, h)
+    got = {}
+    for mode in (1, 0):
+        with vrt.Renderer(0) as r:
+            r.upload_volume(vox, n)
+            r.set_exact_pass(mode)
+            got[mode] = [r.render_frame(cam, vrt.default_params(R, T, time=float(t + 1)), a)[0]
+                         for t, a in enumerate((1.0, 0.5, 1.0))]
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vox, n)
+        ref = [r.render_frame(cam, vrt.default_params(R, T, time=float(t + 1)), a, counters=True)[0]
+               for t, a in enumerate((1.0, 0.5, 1.0))]
+    for k in range(3):
+        assert np.array_equal(got[1][k], ref[k]), f"deferred, frame {k}"
+        assert np.array_equal(got[0][k], ref[k]), f"in-lane, frame {k}"

@@ -525,7 +525,19 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
   o->ev_last_valid = hipEventRecord(o->ev_last, st) == hipSuccess;
 }
 
-OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer) {
+// A frame that runs alone (synchronous calls) with the deferred exact pass, as one launch with the
+// exact pass's short-band instance: where the in-lane alternative's long waves are the frame
+// (glass-heavy volumes: every lane holds its bounce tree) or the certified pass is long enough to
+// carry the exact pass's ~50 us tail (>= 8 rounds of resident waves). Synchronous frames, device
+// timestamps: C1 0.330 -> 0.252 ms, C4 0.247 -> 0.212; C3 0.101 -> 0.103 and C2 0.129 -> 0.146
+// stay in lane, as two interleaved parts (profiles/r06_s12).
+bool lone_defers(const vrt_ctx* ctx, const Shard& s, const vrt::KArgs& a) {
+  return ctx->exact_pass > 0 && a.cert == 2 && !a.textured && a.rows < 8192 &&
+         (!s.cert_auto || a.tiles * uint32_t(vrt::kWgWaves) >= 8u * s.wave_slots);
+}
+
+OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer,
+                              bool lone = false) {
   // (the deferred list packs a pixel as frame | band row | column in 3 | 13 | 16 bits)
   const bool defer = allow_defer && ctx->exact_pass > 0 && a.cert == 2 && a.rows < 8192 &&
                      (ctx->exact_pass == 2 || a.tiles * uint32_t(vrt::kWgWaves) >= 2u * s.wave_slots);
@@ -564,7 +576,7 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
     a.defer_e = uint32_t(slot->defer_epoch & 1u);
     a.defer_seg = defer_seg_tiles(a.tiles, a.tiles_x) * uint32_t(vrt::kWgThreads);
     // bands of under 4 rounds: the exact pass's latency follows a short certified pass
-    a.exact_fat = !a.textured && a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots ? 1 : 0;
+    a.exact_fat = !a.textured && (lone || a.tiles * uint32_t(vrt::kWgWaves) < 4u * s.wave_slots) ? 1 : 0;
     if (VRT_EXACT_GRID_ADAPT && !a.exact_fat) {
       const uint32_t div = a.textured ? vrt::kDeferGridDiv : vrt::kDeferGridDivColor;  // launch_render's
       // the grid from an earlier frame's batch count on this slot (frames in flight: a few frames
@@ -608,9 +620,10 @@ OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipSt
 // the fold of the counter replicas into `cnt` (accumulating). ev_begin / ev_end: optional device
 // timestamps of the kernel's start and end.
 void launch(const vrt_ctx* ctx, Shard& s, vrt::KArgs a, float4* out, vrt_hit* hit, unsigned long long* cnt,
-            hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr, bool allow_defer = true) {
+            hipStream_t st, hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr, bool allow_defer = true,
+            bool lone = false) {
   const bool stats = hit || cnt;
-  OrderSlot* slot = stats ? nullptr : launch_state_begin(ctx, s, a, st, allow_defer);
+  OrderSlot* slot = stats ? nullptr : launch_state_begin(ctx, s, a, st, allow_defer || lone, lone);
   vrt::launch_render(a, stats, s.d_vox_pad, out, hit, cnt ? s.d_cnt_rep : nullptr, st, ev_begin, ev_end);
   slot_launched(s, slot, st);
   if (cnt) vrt::launch_reduce_counters(s.d_cnt_rep, cnt, st);
@@ -799,7 +812,10 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
   const bool single = counting || hits;  // one counter replica set: one counted launch
   // one_part: device-output frames consumed on their own stream (vrt_frame_stream)
   // k > 1: one launch per block-cyclic band (a band's blocks are not split into parts)
-  const int nparts = single || one_part || (overlap && !hist) || k > 1 ? 1 : kParts;
+  // a synchronous whole frame that lone_defers: one launch (certified pass + exact pass)
+  const bool lone = !overlap && !single && !hist && k == 1 &&
+                    lone_defers(ctx, ctx->sh[0], make_args(ctx, ctx->sh[0], cam, p, 0, h, 1));
+  const int nparts = single || one_part || (overlap && !hist) || lone || k > 1 ? 1 : kParts;
   for (int32_t j = 0; j < k; ++j) {
     Shard& s = ctx->sh[j];
     VRT_HIP(ctx, hipSetDevice(s.device));
@@ -847,10 +863,10 @@ int launch_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* p, float
         a.prev = hsrc + off;
         a.cur = s.d_ring[slot] + off;
         a.raw = hist ? s.d_rawbuf[slot] + off : nullptr;
-        launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.ls[g][q], kb, ke, overlap);
+        launch(ctx, s, a, nullptr, nullptr, counting ? s.d_cnt : nullptr, s.ls[g][q], kb, ke, overlap, lone);
       } else {
         launch(ctx, s, a, s.d_out + off, hits ? s.d_hit + off : nullptr, counting ? s.d_cnt : nullptr,
-               s.ls[g][q], kb, ke, overlap);
+               s.ls[g][q], kb, ke, overlap, lone);
       }
       VRT_HIP(ctx, hipGetLastError());
       VRT_HIP(ctx, hipEventRecord(s.ev_done[g][q], s.ls[g][q]));

@@ -2553,6 +2553,12 @@ __global__ void __launch_bounds__(kWgThreads, TREE ? VRT_TREE_WAVES : (DEFER ? V
 #ifndef VRT_EXACT_PRIO
 #define VRT_EXACT_PRIO 2
 #endif
+#if defined(VRT_FAT_WAVES) && !defined(VRT_DIAGNOSTIC_BUILD)
+#error "VRT_FAT_WAVES is an A/B knob of make variant builds"
+#endif
+#ifndef VRT_FAT_WAVES  // resident waves per SIMD of the exact pass's short-band instance
+#define VRT_FAT_WAVES 4
+#endif
 #ifndef VRT_FORCE_FAT  // the 4-wave exact-pass instance for every colour-only band (A/B only)
 #define VRT_FORCE_FAT 0
 #endif
@@ -2960,8 +2966,8 @@ void launch_render(const KArgs& a, bool stats, const uint16_t* vox, float4* out,
     auto k2 = a.textured ? (fb ? exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX, true>
                                : exact_pass_kernel<true, 1, VRT_EXACT_WAVES, VRT_SPARSE_BATCH_TEX>)
                          : ((a.exact_fat || VRT_FORCE_FAT)
-                                ? (fb ? exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT, true>
-                                      : exact_pass_kernel<false, 2, 4, VRT_SPARSE_BATCH_FAT>)
+                                ? (fb ? exact_pass_kernel<false, 2, VRT_FAT_WAVES, VRT_SPARSE_BATCH_FAT, true>
+                                      : exact_pass_kernel<false, 2, VRT_FAT_WAVES, VRT_SPARSE_BATCH_FAT>)
                                 : (fb ? exact_pass_kernel<false, 2, VRT_EXACT_WAVES, VRT_SPARSE_BATCH, true>
                                       : exact_pass_kernel<false, 2>));
     if (ev_begin)

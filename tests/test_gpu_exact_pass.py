@@ -3,7 +3,7 @@ its certified walks settle and appends the others to a list (per wave a ballot o
 lanes, one atomicAdd on one of 8 XCD-local segment counters, mbcnt ranks; waves with >= 32
 deferred pixels keep an 8x8 chunk in lane order); a second kernel renders the list with the exact
 path, a chunk or a batch of list entries to a wave (these band sizes are under four dispatch rounds:
-the 4-wave instance with 16-pixel sparse batches; whole frames, 64-pixel batches at 7 waves, are
+the short-band instance with 16-pixel sparse batches; whole frames, 64-pixel batches at 7 waves, are
 checked frame by frame in test_gpu_bench_path.py). Images must be bit-identical
 to the in-lane fallback and to the exact STATS instance, frame after frame, on scenes where many
 pixels defer (glass cube: most pixels; random sparse volumes with every byte; near-edge cameras)

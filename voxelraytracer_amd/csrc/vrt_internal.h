@@ -59,7 +59,7 @@ struct KArgs {
   // words per segment (a segment holds at most ceil(tiles / 8) tiles' pixels)
   uint32_t* defer;
   uint32_t defer_e, defer_seg;
-  int32_t exact_fat;  // the exact pass's 4-wave instance (colour-only bands of < 4 rounds of waves)
+  int32_t exact_fat;  // the exact pass's short-band instance (colour-only bands of < 4 rounds of waves, lone frames)
   // adaptive exact-pass grid (VRT_EXACT_GRID_ADAPT): workgroups of this launch's exact pass (0: the
   // tiles-based default) and the slot's host-mapped word its workgroup 0 stores the batch count in
   uint32_t exact_grid;

@@ -2557,9 +2557,9 @@ __global__ void __launch_bounds__(kWgThreads, TREE ? VRT_TREE_WAVES : (DEFER ? V
 #error "VRT_FAT_WAVES is an A/B knob of make variant builds"
 #endif
 #ifndef VRT_FAT_WAVES  // resident waves per SIMD of the exact pass's short-band instance
-#define VRT_FAT_WAVES 4
+#define VRT_FAT_WAVES 3
 #endif
-#ifndef VRT_FORCE_FAT  // the 4-wave exact-pass instance for every colour-only band (A/B only)
+#ifndef VRT_FORCE_FAT  // the short-band exact-pass instance for every colour-only band (A/B only)
 #define VRT_FORCE_FAT 0
 #endif
 
@@ -2577,11 +2577,14 @@ __global__ void __launch_bounds__(kWgThreads, TREE ? VRT_TREE_WAVES : (DEFER ? V
 // next launch on the stream (none of this launch's kernels reads it).
 // WAVES: resident waves per SIMD the instance is built for. 7 (72 VGPRs, ~1 KB of spills per lane)
 // for whole frames, where its waves share the CUs with the next frames' certified passes (fewer
-// cost 10-30 %, profiles/r03_s25); 4 (no spills: shorter exact walks) for colour-only bands of
-// under 4 dispatch rounds, whose frame time is the certified pass plus this pass's latency
-// (a.exact_fat: C4 k = 8 0.0229 -> 0.0222, C3 k = 2 0.0275 -> 0.0267 ms; textured bands get
-// slower, profiles/r03_s67)
-// SB: pixels per sparse batch. 64 for whole frames; 16 in the 4-wave instance of short bands,
+// cost 10-30 %, profiles/r03_s25; a spill-free 3-wave instance there: C3 0.0388 -> 0.049 ms per
+// frame at 8.7 instead of 17.4 MB of HBM writes, r06_s11); VRT_FAT_WAVES = 3 (no spills: shorter
+// exact walks; 168 VGPRs) for colour-only bands of under 4 dispatch rounds and synchronous frames,
+// whose frame time is the certified pass plus this pass's latency (a.exact_fat: C4 k = 8 0.0229 ->
+// 0.0222, C3 k = 2 0.0275 -> 0.0267 ms at 4 waves, profiles/r03_s67; 3 waves, which no longer
+// spill where 4 now do: C4 synchronous frame 0.2125 -> 0.2059 ms, bands of C3/C4 k = 4, 8
+// unchanged, r06_s14; textured bands get slower)
+// SB: pixels per sparse batch. 64 for whole frames; 16 in the short-band instance,
 // whose frame time includes this pass's span: a sparse wave's span is its slowest walk, and a lone
 // wave's walks cost the same per step with 16 lanes as with 64 (C4 k = 8 band 0.0222 -> 0.0200 ms,
 // exact-pass span 58 -> 49 us; whole frames +1-3 %: more waves, profiles/r04_exact/)

@@ -394,7 +394,8 @@ def main():
     ren = vrt.Renderer(local)
     ren.set_exact_pass(args.exact_pass)
     ren.set_certified(args.certified)
-    ren.set_cert_trees(args.cert_trees)
+    if args.cert_trees != 1 or hasattr(ren._lib, "vrt_set_cert_trees"):   # (an ABI < 15 build: A/B only)
+        ren.set_cert_trees(args.cert_trees)
     ren.set_tile_order(args.tile_order)
     ren.upload_volume_device(vox_dev.data_ptr(), n, sptr)
     kparams = params   # the kernel's params: textured frames use the atlas uploaded once

@@ -96,7 +96,7 @@ HIT_DTYPE = [("voxel_index", "<i4"), ("ray_length", "<f4"), ("steps", "<u4"), ("
 # name -> (restype, argtypes): every function include/vrt.h declares
 # entry points added after ABI v12 (an older build loaded by VRT_LIB with VRT_LIB_ABI=<its version>
 # may lack exactly these)
-ADDED_IN = {"vrt_render_temporal_batch_async": 14}
+ADDED_IN = {"vrt_render_temporal_batch_async": 14, "vrt_set_cert_trees": 15}
 
 SIGNATURES = {
     "vrt_abi_version": (C.c_int, []),

@@ -1918,19 +1918,6 @@ __device__ __forceinline__ bool cert_pixel(const Ctx& c, const Ray& ray0, f3& co
   return true;
 }
 
-// The certified prefix of a primary walk for the exact path (the deferred exact pass re-walks the
-// primary ray certified: a few jumps): every exact step before it replays only the DDA state
-// update, without its sample (skip_walk's s_init). -1: none.
-__device__ __forceinline__ float primary_prefix(const Ctx& c, const Ray& ray0) {
-  const f3 P = ray0.pos, D = ray0.dir;
-  int cx, cy, cz;
-  if (!fast_path_ok(D) || !exact_start_cell(c, P, D, cx, cy, cz) ||
-      !start_layers_clear<false>(c, P, D, cx, cy, cz, 0u))
-    return -1.0f;
-  const f3 rcp = mk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y), __builtin_amdgcn_rcpf(D.z));
-  return cert_walk<false>(c, P, D, rcp, c.max_len - ray0.len, cx, cy, cz, 0.0f, mk(0.0f, 0.0f, 0.0f), 0.0f, 0u).us;
-}
-
 // ---- RGB8 framebuffer store + temporal filter (oracle/vrt_oracle.c oracle_temporal) ----------
 // GL float -> UNORM8 store into the RGB8 FBO attachments (FrameBuffer.cpp:8): clamp to [0,1]
 // (NaN -> 0), scale by 255, round half to even (pinned in DESIGN.md); a texel reads back b / 255.
@@ -2659,8 +2646,7 @@ __global__ void __launch_bounds__(64, WAVES) exact_pass_kernel(KArgs a, const ui
     f3 color = mk(0.0f, 0.0f, 0.0f);
     __shared__ float lstk[VRT_LDS_STACK ? kStackWords * 64 : 1];
     (void)exact_pixel<false, TEX, CERT >= 1, CERT == 2 && !TEX, 64>(a, c, ray, color, k, steps, flags,
-                                                                    hit_vidx, hit_len, &lstk[lane],
-                                                                    primary_prefix(c, ray));
+                                                                    hit_vidx, hit_len, &lstk[lane]);
     if constexpr (FB) {
       // the pixel and its frame re-derived from e (only e stays live across the exact path)
       uint32_t e2 = e;

@@ -19,7 +19,9 @@
  *     into block-cyclic bands of 16 adjacent rows (ABI v12; device j renders row blocks j, j+k,
  *     ..., one launch per band; vrt_frame_row_block), rendered on context-owned streams: frame f
  *     on lane f % 4. On one device a frame that runs alone (synchronous calls) or reads its
- *     history is two interleaved row parts on two streams; a device-output frame at u_Alpha = 1
+ *     history is two interleaved row parts on two streams (a synchronous colour-only certified
+ *     frame of a glass-heavy volume or of >= 8 rounds of resident waves: one deferred launch, see
+ *     vrt_set_exact_pass); a device-output frame at u_Alpha = 1
  *     is one launch, and up to four frames are in flight (ABI v9). The *_async band entry points
  *     run on the context's first (root) device.
  */
@@ -227,7 +229,11 @@ int vrt_set_tile_order(vrt_ctx* ctx, int32_t on);
  * It pays when other work overlaps the exact pass and the launch is large: the async band entry
  * points and the device-output frames (frames in flight) use it for bands of at least two rounds of
  * resident waves (CUs x 4 x 7 x 2 waves: 14336, e.g. 1920 x 960 pixels, on MI355X); smaller bands
- * and the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path. off =
+ * and the synchronous whole-frame calls (vrt_render, vrt_render_frame) keep the in-lane path, except
+ * a synchronous colour-only frame (u_Alpha = 1 for vrt_render_frame) of a glass-heavy volume or of
+ * >= 8 rounds of resident waves, which is one deferred launch with the exact pass's short-band
+ * instance (its in-lane alternative waits on the glass trees, or the long certified pass carries
+ * the exact pass's tail; C1 0.330 -> 0.25 ms, C4 0.247 -> 0.21). off =
  * 0: the exact path runs in the pixel's own lane, with the heavy-first tile order
  * (vrt_set_tile_order). Launches over 131072 tiles, and launches on a stream being captured into a
  * graph, use the in-lane path. Images are identical either way. */
@@ -376,7 +382,8 @@ int vrt_render_temporal_batch_async(vrt_ctx* ctx, int32_t nframes, const vrt_cam
  * context: render, filter against the last filtered frame, copy the new filtered frame to the
  * HOST buffer out_rgba8 (W*H*4 bytes). The history starts black and restarts black when the image
  * size changes. stats may be NULL. Each device renders its row band as two interleaved parts on
- * two context-owned streams (one launch's tail overlaps the other's); ABI v9: every device's DMA
+ * two context-owned streams (one launch's tail overlaps the other's), or as one deferred launch
+ * (vrt_set_exact_pass: glass-heavy volumes, large frames); ABI v9: every device's DMA
  * engine writes its band straight into its rows of a pinned staging frame owned by the context
  * (the k copies run in parallel), which is then copied to out_rgba8. */
 int vrt_render_frame(vrt_ctx* ctx, const vrt_camera* cam, const vrt_params* params, float alpha,

@@ -532,7 +532,7 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 // timestamps: C1 0.330 -> 0.252 ms, C4 0.247 -> 0.212; C3 0.101 -> 0.103 and C2 0.129 -> 0.146
 // stay in lane, as two interleaved parts (profiles/r06_s12).
 bool lone_defers(const vrt_ctx* ctx, const Shard& s, const vrt::KArgs& a) {
-  return ctx->exact_pass > 0 && a.cert == 2 && !a.textured && a.rows < 8192 &&
+  return ctx->exact_pass > 0 && a.cert == 2 && !a.textured && a.rows < 8192 && a.tiles <= kOrderMaxTiles &&
          (!s.cert_auto || a.tiles * uint32_t(vrt::kWgWaves) >= 8u * s.wave_slots);
 }
 

@@ -528,12 +528,14 @@ void slot_launched(Shard& s, OrderSlot* o, hipStream_t st) {
 // A frame that runs alone (synchronous calls) with the deferred exact pass, as one launch with the
 // exact pass's short-band instance: where the in-lane alternative's long waves are the frame
 // (glass-heavy volumes: every lane holds its bounce tree) or the certified pass is long enough to
-// carry the exact pass's ~50 us tail (>= 8 rounds of resident waves). Synchronous frames, device
+// carry the exact pass's ~50 us tail (>= 8 rounds of resident waves); frames of at least two rounds
+// (the deferral's own bound, launch_state_begin) within one list slot. Synchronous frames, device
 // timestamps: C1 0.330 -> 0.252 ms, C4 0.247 -> 0.212; C3 0.101 -> 0.103 and C2 0.129 -> 0.146
 // stay in lane, as two interleaved parts (profiles/r06_s12).
 bool lone_defers(const vrt_ctx* ctx, const Shard& s, const vrt::KArgs& a) {
+  const uint32_t waves = a.tiles * uint32_t(vrt::kWgWaves);
   return ctx->exact_pass > 0 && a.cert == 2 && !a.textured && a.rows < 8192 && a.tiles <= kOrderMaxTiles &&
-         (!s.cert_auto || a.tiles * uint32_t(vrt::kWgWaves) >= 8u * s.wave_slots);
+         waves >= 2u * s.wave_slots && (!s.cert_auto || waves >= 8u * s.wave_slots);
 }
 
 OrderSlot* launch_state_begin(const vrt_ctx* ctx, Shard& s, vrt::KArgs& a, hipStream_t st, bool allow_defer,

@@ -257,6 +257,16 @@ int vrt_set_cert_trees(vrt_ctx* ctx, int32_t on);
 int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n,
                         float randomness, float seed, float* out);
 
+/* Diagnostic: the kernels' fast correctly rounded reciprocal (the hardware reciprocal plus one
+ * Newton step) and square root (the hardware square root plus its residual fix) checked against
+ * the IEEE division and square root over all 2^32 float bit patterns on the context's first
+ * device. out[7]: patterns the kernels take the reciprocal for, mismatches among them (must be 0),
+ * mismatches of normal-range patterns with an all-ones significand and of the remaining non-NaN
+ * patterns (both take the division), the first mismatching pattern of the first kind (~0 if none),
+ * positive patterns the kernels take the square root for, mismatches among them (must be 0).
+ * Synchronous. */
+int vrt_debug_fast_math(vrt_ctx* ctx, uint64_t* out);
+
 /* Diagnostic (test rehearsal of the multi-GPU path on a one-GPU box): a one-device context takes
  * the k-device path through RCCL with a one-rank communicator (ncclCommInitAll over its device):
  * the volume upload goes through ncclBroadcast (in place) and vrt_render_frame_device through

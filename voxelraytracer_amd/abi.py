@@ -126,6 +126,7 @@ SIGNATURES = {
     "vrt_build_scene_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_uint32, C.c_void_p]),
     "vrt_debug_packed_volume": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "vrt_debug_collectives": (C.c_int, [C.c_void_p]),
+    "vrt_debug_fast_math": (C.c_int, [C.c_void_p, C.c_void_p]),
     "vrt_volume_octants": (C.c_int, [C.c_void_p]),
     "vrt_set_skip_layout": (C.c_int, [C.c_void_p, C.c_int32]),
     "vrt_set_certified": (C.c_int, [C.c_void_p, C.c_int32]),

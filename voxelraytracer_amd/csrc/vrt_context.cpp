@@ -1382,6 +1382,18 @@ int vrt_volume_octants(const vrt_ctx* ctx) {
   return ctx->sh[0].d_vox_pad ? ctx->sh[0].octants : 0;
 }
 
+int vrt_debug_fast_math(vrt_ctx* ctx, uint64_t* out) {
+  if (!ctx) return VRT_ERR_INVALID;
+  if (!out) return fail(ctx, VRT_ERR_INVALID, "null output");
+  DeviceGuard guard;
+  VRT_HIP(ctx, hipSetDevice(ctx->sh[0].device));
+  unsigned long long c[7];
+  const int st = vrt::run_fast_math_check(c);
+  if (st != VRT_OK) return fail(ctx, st, "vrt_debug_fast_math");
+  for (int i = 0; i < 7; ++i) out[i] = c[i];
+  return VRT_OK;
+}
+
 int vrt_debug_randomize(vrt_ctx* ctx, const float* dir, const float* pos, int32_t n, float randomness,
                         float seed, float* out) {
   if (!ctx) return VRT_ERR_INVALID;

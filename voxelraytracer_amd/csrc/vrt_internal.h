@@ -159,6 +159,7 @@ void launch_volume_passes(const uint8_t* vox, uint8_t* tmp, uint16_t* packed, ui
 // glass and non-empty voxel counts into out[0..1] (accumulating)
 void launch_glass_share(const uint8_t* vox, uint64_t total, unsigned long long* out, hipStream_t s);
 void launch_build_scene(uint8_t* vox, int scene, uint32_t n, const float* noise, hipStream_t s);
+int run_fast_math_check(unsigned long long* host_out);  // vrt_debug_fast_math (7 counters)
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,
                       float* out, hipStream_t s);
 // frame rows [0, height) from k block-cyclic bands of 2^sh-row blocks, band_words words apart

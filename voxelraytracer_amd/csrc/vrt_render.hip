@@ -74,6 +74,40 @@ __device__ __forceinline__ void set_comp(f3& a, int i, float f) {
   else if (i == 1) a.y = f;
   else a.z = f;
 }
+// RN(1 / d) from the hardware reciprocal (within 1 ulp) and one Newton step on its exact residual
+// (e = 1 - d y by fma): bit-identical to the IEEE division 1.0f / d for every d with a biased
+// exponent in [2, 252], i.e. |d| in [2^-125, 2^126) (exhaustive over all 2^32 bit patterns on the
+// GPU, 4 211 080 714 of them in that range, 0 mismatches: vrt_debug_fast_math,
+// tests/test_gpu_fast_math.py); 3 VALU instead of the division's 11. Operands the caller cannot
+// bound take rcp_rn (exponent test, else the division).
+__device__ __forceinline__ bool rcp_rn_ok(float d) {
+  const uint32_t e = (__float_as_uint(d) >> 23) & 0xFFu;
+  return e >= 2u && e <= 252u;
+}
+__device__ __forceinline__ float rcp_newton(float d) {
+  const float y = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(__builtin_fmaf(-d, y, 1.0f), y, y);
+}
+__device__ __forceinline__ float rcp_rn(float d) { return rcp_rn_ok(d) ? rcp_newton(d) : 1.0f / d; }
+// RN(sqrt(s)) for s with a biased exponent in [95, 252], i.e. s in [2^-32, 2^126): the hardware
+// square root moved to the neighbour its fma residuals pick (the correctly rounded sequence without
+// the scaling of s < 2^-32 and the special-value select, which such s never need): bit-identical
+// to the IEEE square root on every such s (exhaustive, vrt_debug_fast_math; below 2^-32 the
+// unscaled hardware root is off by more than the fix can mend: 2.2 M mismatches when [2^-125,
+// 2^-32) was included). Other s take the IEEE square root.
+__device__ __forceinline__ bool sqrt_fix_ok(float s) {
+  const uint32_t e = (__float_as_uint(s) >> 23) & 0xFFu;
+  return e >= 95u && e <= 252u;
+}
+__device__ __forceinline__ float sqrt_fix(float s) {
+  const float y = __builtin_amdgcn_sqrtf(s);
+  const float ym = __uint_as_float(__float_as_uint(y) - 1u), yp = __uint_as_float(__float_as_uint(y) + 1u);
+  const float rm = __builtin_fmaf(-ym, y, s), rp = __builtin_fmaf(-yp, y, s);
+  const float z = rm <= 0.0f ? ym : y;
+  return rp > 0.0f ? yp : z;
+}
+__device__ __forceinline__ float sqrt_rn(float s) { return sqrt_fix_ok(s) ? sqrt_fix(s) : __builtin_sqrtf(s); }
+
 // RN(1 / RN(sqrt(s))) for s within 1024 ulps of 1 (bits b), in closed form: for s = 1 + k 2^-23
 // (k >= 0) the correctly rounded square root is 1 + floor(k/2) 2^-23 and its reciprocal
 // 1 - floor(k/2) 2^-23; for s = 1 - k 2^-24 they are 1 - ceil(k/2) 2^-24 and 1 + ceil(m/2) 2^-23,
@@ -91,7 +125,7 @@ __device__ __forceinline__ float near_one_rsqrt(uint32_t b) {
 __device__ __forceinline__ f3 normalize3(f3 v) {
   const float s = v.x * v.x + v.y * v.y + v.z * v.z;
   const uint32_t b = __float_as_uint(s);
-  const float inv = b - (0x3F800000u - 1024u) <= 2048u ? near_one_rsqrt(b) : 1.0f / __builtin_sqrtf(s);
+  const float inv = b - (0x3F800000u - 1024u) <= 2048u ? near_one_rsqrt(b) : rcp_rn(sqrt_rn(s));
   return v * inv;
 }
 __device__ __forceinline__ float gsign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
@@ -107,7 +141,7 @@ __device__ __forceinline__ f3 refract3(f3 i, f3 n, float eta) {
   const float d = dot3(n, i);
   const float k = 1.0f - eta * eta * (1.0f - d * d);
   if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-  const float s = eta * d + __builtin_sqrtf(k);
+  const float s = eta * d + sqrt_rn(k);
   return eta * i - s * n;
 }
 __device__ __forceinline__ f3 sign3(f3 d) { return mk(gsign(d.x), gsign(d.y), gsign(d.z)); }
@@ -707,7 +741,8 @@ __device__ __forceinline__ int walk_ray(const Ctx& c, const f3 pos, const f3 dir
                                         uint32_t medium, WalkState& w, int& axis, int32_t& vidx,
                                         uint32_t& v, float s_init = -1.0f) {
   if (__builtin_expect(fast_path_ok(dir), 1)) {
-    const f3 rcp = mk(opaque(1.0f / dir.x), opaque(1.0f / dir.y), opaque(1.0f / dir.z));
+    // (fast_path_ok: every |d| in [2^-64, 1e4], so rcp_newton is RN(1/d))
+    const f3 rcp = mk(opaque(rcp_newton(dir.x)), opaque(rcp_newton(dir.y)), opaque(rcp_newton(dir.z)));
     return skip_walk<false, STATS>(c, pos, dir, rcp, len0, medium, w, axis, vidx, v, s_init);
   }
   return dda_walk<false, true>(c, pos, dir, dir, len0, medium, w, axis, vidx, v);
@@ -2111,7 +2146,7 @@ __device__ __forceinline__ bool markstein_safe(float x) {
 }
 __device__ __forceinline__ f3 div3_rn(float x, float y, float z, float d) {
   if (markstein_safe(x) && markstein_safe(y) && markstein_safe(z) && markstein_safe(d)) {
-    const float r = 1.0f / d;
+    const float r = rcp_newton(d);  // |d| in [2^-60, 2^60]: RN(1/d)
     return mk(div_rn(x, d, r), div_rn(y, d, r), div_rn(z, d, r));
   }
   return mk(x / d, y / d, z / d);
@@ -3063,6 +3098,61 @@ void launch_assemble_blocks_rgb8(const uint8_t* bands, uint64_t band_px, int32_t
   hipLaunchKernelGGL(assemble_blocks_rgb8_kernel, dim3(uint32_t(height)), dim3(256), 0, s,
                      reinterpret_cast<const uint32_t*>(bands), band_px, k, sh, width, reinterpret_cast<uint4*>(frame),
                      frame_pitch);
+}
+
+// Diagnostic (vrt_debug_fast_math): every float bit pattern, rcp_newton against the IEEE
+// division. out: {patterns with rcp_rn_ok, their mismatches, mismatches of normal-range patterns
+// with an all-ones significand, mismatches of the other (non-NaN) patterns, the first mismatching
+// pattern with rcp_rn_ok (or ~0); then sqrt_fix against the IEEE square root: positive patterns
+// with sqrt_fix_ok, their mismatches}
+__global__ void fast_math_check_kernel(unsigned long long* out) {
+  const uint64_t per = 256;
+  const uint64_t base = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) * per;
+  uint32_t ok = 0, bad_ok = 0, bad_ones = 0, bad_other = 0, sq_ok = 0, sq_bad = 0;
+  for (uint64_t i = 0; i < per; ++i) {
+    const uint32_t u = uint32_t(base + i);
+    const float d = __uint_as_float(u);
+    const uint32_t ex = (u >> 23) & 0xFFu;
+    const bool in_range = ex >= 2u && ex <= 252u;
+    const bool fine = rcp_rn_ok(d);
+    const bool same = __float_as_uint(rcp_newton(d)) == __float_as_uint(1.0f / d);
+    ok += fine ? 1u : 0u;
+    if (sqrt_fix_ok(d) && d > 0.0f) {
+      ++sq_ok;
+      if (__float_as_uint(sqrt_fix(d)) != __float_as_uint(__builtin_sqrtf(d))) ++sq_bad;
+    }
+    if (!same && !(d != d)) {
+      if (fine) {
+        ++bad_ok;
+        atomicMin(&out[4], (unsigned long long)u);
+      } else if (in_range) {
+        ++bad_ones;
+      } else {
+        ++bad_other;
+      }
+    }
+  }
+  atomicAdd(&out[0], (unsigned long long)ok);
+  atomicAdd(&out[1], (unsigned long long)bad_ok);
+  atomicAdd(&out[2], (unsigned long long)bad_ones);
+  atomicAdd(&out[3], (unsigned long long)bad_other);
+  atomicAdd(&out[5], (unsigned long long)sq_ok);
+  atomicAdd(&out[6], (unsigned long long)sq_bad);
+}
+
+int run_fast_math_check(unsigned long long* host_out) {
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, 7 * sizeof(unsigned long long)) != hipSuccess) return VRT_ERR_OOM;
+  const unsigned long long init[7] = {0, 0, 0, 0, ~0ull, 0, 0};
+  hipError_t e = hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    // 2^32 patterns: 2^24 threads of 256 patterns each
+    hipLaunchKernelGGL(fast_math_check_kernel, dim3(1u << 16), dim3(256), 0, nullptr, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(host_out, d, sizeof(init), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return e == hipSuccess ? VRT_OK : VRT_ERR_DEVICE;
 }
 
 void launch_randomize(const float* dir, const float* pos, int n, float randomness, float seed,

@@ -1,0 +1,153 @@
+"""GPU: certified bounce trees (vrt_set_cert_trees, ABI v15) in the certified pass's tree instance,
+with the deferred exact pass (vrt_set_exact_pass 2) and in lane: a glass pixel's tree
+(voxel.glsl:425-452) walked ray by ray with certified walks, trees that cannot be certified
+rendered by the exact path. Frames must be bit-identical to the exact STATS instance, frame after
+frame (temporal history read at alpha 0.5), on glass-heavy volumes at full size, bands with row
+steps, frame batches, noise (every tree then takes the exact path), lattice cameras (ties; exact
+march continuations after in-volume refraction that start on or just before a lattice plane) and
+the modes toggled between frames on one stream."""
+import numpy as np
+import pytest
+import torch
+
+import voxelraytracer_amd as vrt
+from voxelraytracer_amd.tiles import block_band_spec
+
+pytestmark = pytest.mark.gpu
+
+
+def frames(r, cam, n_frames, R, T, alpha, row0, rows, step, w, counters=False, **kw):
+    hist = torch.zeros((rows, w, 4), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
+    out = []
+    for t in range(n_frames):
+        p = vrt.default_params(R, T, time=float(t + 1), **kw)
+        r.render_temporal_rows_async(cam, p, alpha, row0, rows, step, hist.data_ptr(), hist.data_ptr(),
+                                     d_counters=cnt.data_ptr() if counters else 0,
+                                     stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        out.append(hist.cpu().numpy().copy())
+    return out
+
+
+def glass_volume(n, seed):
+    rng = np.random.default_rng(seed)
+    vox = np.zeros((n, n, n), np.uint8)
+    m = rng.random((n, n, n)) < 0.04
+    vox[m] = rng.choice(np.array([2, 2, 2, 1, 3], np.uint8), size=int(m.sum()))
+    vox[n // 4: n // 2, n // 4: n // 2, n // 4: n // 2] = 2
+    vox[:, :2, :] = 1
+    return vox.reshape(-1)
+
+
+CASES = [
+    # scene, n, w, h, R, T, row0, rows, step, noise
+    ("glass_cube", 128, 1920, 1080, 1, 2, 0, 1080, 1, {}),
+    ("glass_cube", 128, 1920, 1080, 4, 4, 0, 1080, 1, {}),
+    ("glass_cube", 64, 640, 360, 2, 6, 3, 90, 4, {}),
+    ("glass", 64, 480, 270, 4, 4, 0, 270, 1, {}),
+    ("glass", 32, 320, 200, 3, 5, 1, 67, 3, {}),
+    ("glass_cube", 64, 320, 180, 1, 2, 0, 180, 1, dict(refraction_noise=0.01)),
+    ("refraction", 128, 480, 270, 4, 4, 0, 270, 1, {}),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}{c[1]}_{c[2]}x{c[3]}_{c[4]}{c[5]}_s{c[8]}" for c in CASES])
+def test_cert_trees_are_bit_identical(built, case):
+    scene, n, w, h, R, T, row0, rows, step, kw = case
+    vox = glass_volume(n, n) if scene == "glass" else vrt.build_scene(scene, n)
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vox, n)
+        r.set_certified(1)
+        r.set_cert_trees(2)
+        r.set_exact_pass(2)   # deferred at any size
+        cam = vrt.make_camera(w, h)
+        a = frames(r, cam, 2, R, T, 0.5, row0, rows, step, w, **kw)
+        r.set_exact_pass(0)
+        b = frames(r, cam, 2, R, T, 0.5, row0, rows, step, w, **kw)
+        ref = frames(r, cam, 2, R, T, 0.5, row0, rows, step, w, counters=True, **kw)
+    for k in range(2):
+        assert np.array_equal(a[k], ref[k]), f"deferred, frame {k}: {int(np.any(a[k] != ref[k], -1).sum())} px"
+        assert np.array_equal(b[k], ref[k]), f"in lane, frame {k}"
+
+
+@pytest.mark.parametrize("trees", [2, 0])
+def test_cert_trees_lattice_cameras(built, trees):
+    """Cameras on lattice points and diagonals: many trees start on ties and take the exact path,
+    whose march continuations into air after an in-volume refraction are certified walks. At (1, 2,
+    -3) one pixel's continuation started 8e-6 before the glass cube's face plane x = 63, so the
+    exact walk sampled the face voxel (63, 8, 25) at a y crossing 3.7e-6 after the start, which
+    the certified continuation, started beyond the plane, did not see (every certified mode
+    differed in that pixel until cert_continuation checked that layer)."""
+    n, w, h = 64, 320, 180
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("glass_cube", n), n)
+        r.set_certified(1)
+        r.set_cert_trees(trees)
+        for ep in (2, 0):
+            r.set_exact_pass(ep)
+            for pos, rot in [((0.0, 0.0, 0.0), (-45.0, -45.0, 0.0)), ((1.0, 2.0, -3.0), (0.0, 0.0, 0.0)),
+                             ((-2.5, 0.5, 1.5), (-35.26439, 45.0, 0.0)), ((0.5, 0.5, -40.0), (0.0, 0.0, 0.0)),
+                             ((3.0, -1.0, -7.0), (0.0, 90.0, 0.0)), ((0.0, 0.0, -20.0), (-45.0, 0.0, 0.0))]:
+                cam = vrt.make_camera(w, h, pos=pos, rot=rot)
+                a = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w)
+                ref = frames(r, cam, 1, 4, 4, 1.0, 0, h, 1, w, counters=True)
+                bad = np.argwhere(np.any(a[0] != ref[0], axis=-1))
+                assert bad.size == 0, (pos, rot, ep, bad[:5].tolist())
+
+
+def test_cert_trees_toggled_between_frames(built):
+    """Trees and the exact pass switched on and off between frames on one stream."""
+    n, w, h = 64, 480, 270
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("glass_cube", n), n)
+        r.set_certified(1)
+        r.set_exact_pass(2)
+        cam = vrt.make_camera(w, h)
+        hist = torch.zeros((h, w, 4), dtype=torch.uint8, device="cuda")
+        ref = torch.zeros_like(hist)
+        cnt = torch.zeros(len(vrt.COUNTER_NAMES), dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        try:
+            for t, (trees, ep) in enumerate([(2, 2), (1, 2), (2, 2), (0, 2), (2, 2), (2, 0), (2, 2),
+                                             (2, 2), (0, 0), (2, 2)]):
+                p = vrt.default_params(4, 4, time=float(t + 1))
+                r.set_cert_trees(trees)
+                r.set_exact_pass(ep)
+                r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, hist.data_ptr(), hist.data_ptr(), stream=s)
+                r.render_temporal_rows_async(cam, p, 0.5, 0, h, 1, ref.data_ptr(), ref.data_ptr(),
+                                             d_counters=cnt.data_ptr(), stream=s)
+                torch.cuda.synchronize()
+                assert torch.equal(hist, ref), f"frame {t}"
+        finally:
+            r.set_cert_trees(1)
+
+
+@pytest.mark.parametrize("ranks,rank,nf", [(1, 0, 3), (8, 3, 8)])
+def test_cert_trees_frame_batches(built, ranks, rank, nf):
+    """Frame batches (one launch, up to 8 frames: their own cameras and times) with certified
+    trees equal one launch per frame."""
+    w, h, n = 640, 360, 64
+    block = 16 if ranks > 1 else 1
+    row0, rows, step = block_band_spec(rank, ranks, h, block) if ranks > 1 else (0, h, 1)
+    cams = [vrt.make_camera(w, h, pos=(0.5 * f, 0.25 * f, -2.0), rot=(-10.0 + f, 20.0 + 2 * f, 0.0))
+            for f in range(nf)]
+    ps = [vrt.default_params(2, 4, time=float(f + 1)) for f in range(nf)]
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene("glass_cube", n), n)
+        r.set_certified(1)
+        r.set_cert_trees(2)
+        r.set_exact_pass(2)
+        s = torch.cuda.current_stream().cuda_stream
+        ref = []
+        for f in range(nf):
+            b = torch.zeros((rows, w), dtype=torch.int32, device="cuda")
+            r.render_temporal_rows_async(cams[f], ps[f], 1.0, row0, rows, step, b.data_ptr(), b.data_ptr(),
+                                         stream=s, row_block=block)
+            ref.append(b)
+        got = [torch.zeros((rows, w), dtype=torch.int32, device="cuda") for _ in range(nf)]
+        r.render_temporal_batch_async(cams, ps, row0, rows, step, [b.data_ptr() for b in got], stream=s,
+                                      row_block=block)
+        torch.cuda.synchronize()
+    for f in range(nf):
+        assert torch.equal(got[f], ref[f]), f"frame {f}"

@@ -1569,6 +1569,60 @@ __device__ __forceinline__ bool tree_refraction(const Ctx& c, const Ray& ray, co
   return tree_start(c, h, hh, ray.dir, t);
 }
 
+// One ray of a certified tree: the colour update of `ray`'s walk outcome h, its children, then the
+// walk of the ray the reference pops next (ray, h updated). kTreeDone: the tree is complete (colour
+// final); kTreeUnsure: it cannot be certified (colour meaningless); kTreeNext: continue with ray, h.
+constexpr int kTreeNext = 0, kTreeDone = 1, kTreeUnsure = -1;
+template <int NL>
+__device__ __forceinline__ int tree_step(const Ctx& c, int max_refl, int max_transp, Ray& ray, CertResult& h,
+                                         f3& color, bool& pending, float4* __restrict__ lta,
+                                         float* __restrict__ ltb) {
+  // the sun vector opaque per ray, as in the exact path's bounce loop (trace_with_shadow): else
+  // the shadow walk's per-sun products are hoisted into VGPRs live across the whole tree and
+  // spilled on its entry
+  Ctx lc = c;
+  asm volatile("" : "+s"(lc.sun_n.x), "+s"(lc.sun_n.y), "+s"(lc.sun_n.z), "+s"(lc.sun_rcp.x),
+               "+s"(lc.sun_rcp.y), "+s"(lc.sun_rcp.z));
+  bool next = false;
+  TreeRay t;
+  if (h.res == CERT_MISS) {
+    apply_sky_color(c, ray, color);
+  } else {
+    const Hit hh = cert_hit_record(ray, h);
+    if (!cert_shade_hit<false>(lc, ray, h, hh, color)) { CERT_DIAG(22); return kTreeUnsure; }
+    // children (:440-448): the reflection ray is pushed first, the refraction ray second and
+    // popped first; the stack (R + T + 1 entries) never fills with at most one ray waiting
+    const uint32_t m = mat_id(h.byte);
+    const bool pr = mat_reflective(m) && ray.rdepth < max_refl;
+    const bool pt = mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f;
+    if (pr && pt) {
+      if (pending) { CERT_DIAG(18); return kTreeUnsure; }
+      TreeRay r;
+      if (!tree_reflection<false>(c, ray, h, hh, r)) { CERT_DIAG(19); return kTreeUnsure; }
+      tree_put<NL>(lta, ltb, r);
+      pending = true;
+      if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return kTreeUnsure; }
+      next = true;
+    } else if (pr) {
+      if (!tree_reflection<false>(c, ray, h, hh, t)) { CERT_DIAG(19); return kTreeUnsure; }
+      next = true;
+    } else if (pt) {
+      if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return kTreeUnsure; }
+      next = true;
+    }
+  }
+  if (!next) {
+    if (!pending) { CERT_DIAG(17); return kTreeDone; }
+    pending = false;
+    t = tree_get<NL>(lta, ltb);
+  }
+  ray = t.ray;
+  h = cert_march(c, ray, t.cx, t.cy, t.cz, t.e0, t.ed);
+  if (h.res == CERT_UNSURE) { CERT_DIAG(21); return kTreeUnsure; }
+  CERT_DIAG(23);
+  return kTreeNext;
+}
+
 // The bounce tree of a glass primary hit h0 of ray0 (fragment main, voxel.glsl:425-452) by
 // certified walks, colour folded in the reference's DFS order as TraceWithShadow does (:395-423):
 // each ray's RayMarch by cert_march, its hit shaded with a certified shadow (none for glass), a
@@ -1587,51 +1641,10 @@ __device__ __forceinline__ bool cert_tree(const Ctx& c, int max_refl, int max_tr
   bool pending = false;  // a reflection ray waits in the LDS slot
   CERT_DIAG(16);
   for (;;) {
-    // the sun vector opaque per ray, as in the exact path's bounce loop (trace_with_shadow): else
-    // the shadow walk's per-sun products are hoisted into VGPRs live across the whole tree and
-    // spilled on its entry
-    Ctx lc = c;
-    asm volatile("" : "+s"(lc.sun_n.x), "+s"(lc.sun_n.y), "+s"(lc.sun_n.z), "+s"(lc.sun_rcp.x),
-                 "+s"(lc.sun_rcp.y), "+s"(lc.sun_rcp.z));
-    bool next = false;
-    TreeRay t;
-    if (h.res == CERT_MISS) {
-      apply_sky_color(c, ray, color);
-    } else {
-      const Hit hh = cert_hit_record(ray, h);
-      if (!cert_shade_hit<false>(lc, ray, h, hh, color)) { CERT_DIAG(22); return false; }
-      // children (:440-448): the reflection ray is pushed first, the refraction ray second and
-      // popped first; the stack (R + T + 1 entries) never fills with at most one ray waiting
-      const uint32_t m = mat_id(h.byte);
-      const bool pr = mat_reflective(m) && ray.rdepth < max_refl;
-      const bool pt = mat_transparent(m) && ray.tdepth < max_transp && get_color<false>(c, hh).w != 1.0f;
-      if (pr && pt) {
-        if (pending) { CERT_DIAG(18); return false; }
-        TreeRay r;
-        if (!tree_reflection<false>(c, ray, h, hh, r)) { CERT_DIAG(19); return false; }
-        tree_put<NL>(lta, ltb, r);
-        pending = true;
-        if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return false; }
-        next = true;
-      } else if (pr) {
-        if (!tree_reflection<false>(c, ray, h, hh, t)) { CERT_DIAG(19); return false; }
-        next = true;
-      } else if (pt) {
-        if (!tree_refraction<false>(c, ray, h, hh, t)) { CERT_DIAG(20); return false; }
-        next = true;
-      }
-    }
-    if (!next) {
-      if (!pending) break;
-      pending = false;
-      t = tree_get<NL>(lta, ltb);
-    }
-    ray = t.ray;
-    h = cert_march(c, ray, t.cx, t.cy, t.cz, t.e0, t.ed);
-    if (h.res == CERT_UNSURE) { CERT_DIAG(21); return false; }
-    CERT_DIAG(23);
+    const int r = tree_step<NL>(c, max_refl, max_transp, ray, h, color, pending, lta, ltb);
+    if (r == kTreeUnsure) return false;
+    if (r == kTreeDone) break;
   }
-  CERT_DIAG(17);
   color_out = color;
   return true;
 }
@@ -1650,6 +1663,41 @@ __device__ __forceinline__ bool exact_start_cell(const Ctx& c, const f3 P, const
   const uint32_t n = uint32_t(c.n);
   if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) return false;
   return wpx == float(cx + (sx > 0)) && wpy == float(cy + (sy > 0)) && wpz == float(cz + (sz > 0));
+}
+
+// The cells of layer `layer` on axis a (the start cell moved there) that the exact walk may enter
+// across an axis b != a whose first crossing comes before parameter off: each must be a non-event
+// (start_layers_clear's test for one axis; cert_continuation's start).
+template <bool SHADOW>
+__device__ __forceinline__ bool layer_clear(const Ctx& c, const float p[3], const float d[3], const int cell[3],
+                                            int a, int layer, float off, uint32_t medium) {
+  int q[3] = {cell[0], cell[1], cell[2]};
+  q[a] = layer;
+  bool early[3] = {false, false, false};
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    if (b == a) continue;
+    const float plane = float(cell[b] + (d[b] > 0.0f ? 1 : 0));
+    // first crossing of axis b, by the hardware reciprocal (<= 1 ulp) against a bound widened
+    // past its error: only ever more cells checked than the exact quotient would ask for
+    early[b] = (plane - p[b]) * __builtin_amdgcn_rcpf(d[b]) < off * 1.00001f;
+  }
+  const int b1 = a == 0 ? 1 : 0, b2 = a == 2 ? 1 : 2;
+  const int s1 = d[b1] > 0.0f ? 1 : -1, s2 = d[b2] > 0.0f ? 1 : -1;
+  int r[3];
+  if (early[b1]) {
+    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1;
+    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+  }
+  if (early[b2]) {
+    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b2] += s2;
+    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+  }
+  if (early[b1] && early[b2]) {
+    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1; r[b2] += s2;
+    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
+  }
+  return true;
 }
 
 // Cells the exact walk samples behind its start cell. A start coordinate P_a that is an integer k
@@ -1776,6 +1824,19 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
   }
   const uint32_t n = uint32_t(c.n);
   if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) return false;
+  // the start cell lies beyond plane k on axis fa, but P_fa may lie before it (by up to delta) or
+  // on it: until cur_fa = P_fa + s D_fa is past k, the exact walk samples the layer before k at
+  // every crossing of another axis (as start_layers_clear for a start on a plane). Those cells must
+  // be non-events (a glass cube's face voxel beside the refraction point, sampled 3.7e-6 after the
+  // start, made a lattice camera's pixel differ before this check).
+  {
+    const float p[3] = {P.x, P.y, P.z}, d[3] = {D.x, D.y, D.z};
+    const int cell[3] = {cx, cy, cz};
+    const float before = __builtin_fmaxf((k - pa) * sa, 0.0f);
+    const float off = (before + 0x1p-22f * __builtin_fmaxf(__builtin_fabsf(pa), 1.0f) + 1e-5f) / __builtin_fabsf(da);
+    const int ka = fa == 0 ? cx : (fa == 1 ? cy : cz);
+    if (!layer_clear<false>(c, p, d, cell, fa, ka - (da > 0.0f ? 1 : -1), off, 0u)) return false;
+  }
   f3 ed = mk(0.0f, 0.0f, 0.0f);
   set_comp(ed, fa, 2.0f * delta * __builtin_fabsf(__builtin_amdgcn_rcpf(da)) + 1e-6f);
   return cert_air_segment(c, ray, cx, cy, cz, ed, color);

@@ -25,7 +25,7 @@
 
 // Diagnostic instrumentation (per-wave timestamps, certified-walk outcome counts; images and
 // counters unchanged) exists only in `make variant` builds, never in the product library.
-#if (defined(VRT_STAMPS) || defined(VRT_CERT_DIAG)) && !defined(VRT_DIAGNOSTIC_BUILD)
+#if (defined(VRT_STAMPS) || defined(VRT_CERT_DIAG) || defined(VRT_CERT_TRACE)) && !defined(VRT_DIAGNOSTIC_BUILD)
 #error "VRT_STAMPS / VRT_CERT_DIAG are diagnostic builds: use make variant"
 #endif
 
@@ -255,7 +255,27 @@ struct Ctx {
   const uint32_t* atlas;  // textured instances only (TEX)
   uint32_t atlas_mask;   // atlas_size - 1 (power of two)
   float atlas_fs, atlas_fts;  // (float)u_AtlasSize, (float)u_AtlasTextureSize
+#ifdef VRT_CERT_TRACE
+  bool tr;  // diagnostic build: this lane's pixel is the traced one
+#endif
 };
+#ifdef VRT_CERT_TRACE  // diagnostic build: one pixel's certified walks, 8 floats per record
+__device__ float g_ctrace[1024][8];
+__device__ unsigned int g_ctrace_n;
+#define CTRACE(c, a0, a1, a2, a3, a4, a5, a6, a7)                                                   \
+  do {                                                                                              \
+    if ((c).tr) {                                                                                   \
+      const unsigned int q_ = atomicAdd(&g_ctrace_n, 1u);                                           \
+      if (q_ < 1024u) {                                                                             \
+        g_ctrace[q_][0] = float(a0); g_ctrace[q_][1] = float(a1); g_ctrace[q_][2] = float(a2);       \
+        g_ctrace[q_][3] = float(a3); g_ctrace[q_][4] = float(a4); g_ctrace[q_][5] = float(a5);       \
+        g_ctrace[q_][6] = float(a6); g_ctrace[q_][7] = float(a7);                                    \
+      }                                                                                             \
+    }                                                                                               \
+  } while (0)
+#else
+#define CTRACE(c, a0, a1, a2, a3, a4, a5, a6, a7) ((void)0)
+#endif
 
 // a*b + c on the low 24 bits of a and b: one v_mad_u32_u24 (operands < 2^24 for N <= 1024).
 // b is wave-uniform (the padded pitch) and goes in as the instruction's one SGPR operand.
@@ -780,7 +800,7 @@ __device__ __forceinline__ float4 get_color(const Ctx& c, const Hit& h) {
                      float((t >> 16) & 0xFFu) / 255.0f, float(t >> 24) / 255.0f);
 }
 
-__device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
+__device__ __forceinline__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
   Ray r;
   r.voxel = 0;
   r.pos = h.point;
@@ -794,7 +814,7 @@ __device__ Ray reflection_ray(const Ctx& c, const Ray& ray, const Hit& h) {
 
 // GetRefractionRay (voxel.glsl:217-246)
 template <bool TEX>
-__device__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counters& k) {
+__device__ __forceinline__ Ray refraction_ray(const Ctx& c, const Ray& ray, const Hit& h, Counters& k) {
   const uint32_t outv = get_voxel(c, h.point + h.normal * 0.5f);
   const uint32_t inv = get_voxel(c, h.point - h.normal * 0.5f);
   k.c[VRT_CNT_REFRACTION_PROBES]++;
@@ -841,7 +861,7 @@ __device__ __forceinline__ void walk_account(const WalkState& w, int r, int step
 
 // RayMarchShadow (voxel.glsl:259-300): true when an opaque voxel blocks the sun.
 template <bool STATS>
-__device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
+__device__ __forceinline__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t& steps,
                              uint32_t& flags) {
   WalkState w;
   walk_init(w, ray);
@@ -854,7 +874,7 @@ __device__ bool march_shadow(const Ctx& c, const Ray& ray, Counters& k, uint32_t
 // PRIMARY: the primary ray (len 0, medium air: every event is a hit, no in-volume refraction)
 // s_init (PRIMARY only): the certified prefix of the primary walk (skip_walk)
 template <bool STATS, bool TEX, bool PRIMARY = false>
-__device__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags,
+__device__ __forceinline__ Hit march(const Ctx& c, Ray& ray, Counters& k, uint32_t& steps, uint32_t& flags,
                      float s_init = -1.0f) {
   Hit h;
   h.found = false;
@@ -1095,7 +1115,7 @@ __device__ __forceinline__ bool cert_event(uint32_t b, uint32_t medium) {
 // cell's box need not cover a cell behind it: it is read from the diagonal neighbour's texel,
 // G(v + s) = F(v) - 1, i.e. the box [v, v + G s].
 template <bool SHADOW>
-__device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 rcp, const float U,
+__device__ __forceinline__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 rcp, const float U,
                                 int cx, int cy, int cz, const float e0, const f3 ed,
                                 const float len0b, const uint32_t medium, const uint32_t tex0 = ~0u) {
   CertResult r;
@@ -1135,6 +1155,8 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
   // start: the unguarded box from the diagonal neighbour (G(v + s) + 1 in the guarded formula)
   // (tex0: that texel, loaded by the caller beside an earlier load; ~0u: load it here)
   uint32_t tex = (tex0 != ~0u ? tex0 : path_texel(c, cx + sx, cy + sy, cz + sz, obase)) + (1u << kDistShift);
+  CTRACE(c, 100 + int(SHADOW), cx, cy, cz, P.x, P.y, P.z, U);
+  CTRACE(c, 101, D.x, D.y, D.z, e0, ed.x, ed.y, ed.z);
 #ifdef VRT_CERT_DIAG
   r.iters = 0;
 #endif
@@ -1164,6 +1186,7 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
       // parallel axis, |1/d_b| huge, stop every jump: ~90 us cell-by-cell walks at C3)
       const float uj = __builtin_fminf(__builtin_fminf(lx - gam.x, ly - gam.y),
                                        __builtin_fminf(lz - gam.z, U + 2.0f));
+      CTRACE(c, 102, G, s1, uj, gam.x, gam.y, gam.z, 0);
       if (uj > s1) {
         // the cell the exact walk is in there: floor(x) moving up, ceil(x) - 1 moving down
         const float x = Ps.x + uj * Da.x, y = Ps.y + uj * Da.y, z = Ps.z + uj * Da.z;
@@ -1213,6 +1236,8 @@ __device__ CertResult cert_walk(const Ctx& c, const f3 P, const f3 D, const f3 r
            uint32_t(bhy) << 4 | uint32_t(bhz) << 5;
     }
     const uint32_t nb = ntex & kVoxMask;
+    CTRACE(c, 103, nx, ny, nz, s1, a, nf, nb);
+    CTRACE(c, 104, cx, cy, cz, sig.x, sig.y, sig.z, ga);
     if (cert_event<SHADOW>(nb, medium)) {
       if (!(prev + gL < U)) return r;  // the length test might stop the walk first
       if (nf == 0u) {
@@ -1380,7 +1405,7 @@ __device__ __forceinline__ bool cert_shade_hit(const Ctx& c, const Ray& ray, con
 // march(): leaving a glass medium refracts it in place (:357-380), and the walk restarts from
 // that crossing. (cx, cy, cz), e0, ed: the start (cert_start). Returns the first non-air event
 // (CERT_HIT), CERT_MISS or CERT_UNSURE.
-__device__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz, float e0, f3 ed) {
+__device__ __forceinline__ CertResult cert_march(const Ctx& c, Ray& ray, int cx, int cy, int cz, float e0, f3 ed) {
   CertResult h;
   h.res = CERT_UNSURE;
   uint32_t medium = ray.voxel;
@@ -1665,41 +1690,6 @@ __device__ __forceinline__ bool exact_start_cell(const Ctx& c, const f3 P, const
   return wpx == float(cx + (sx > 0)) && wpy == float(cy + (sy > 0)) && wpz == float(cz + (sz > 0));
 }
 
-// The cells of layer `layer` on axis a (the start cell moved there) that the exact walk may enter
-// across an axis b != a whose first crossing comes before parameter off: each must be a non-event
-// (start_layers_clear's test for one axis; cert_continuation's start).
-template <bool SHADOW>
-__device__ __forceinline__ bool layer_clear(const Ctx& c, const float p[3], const float d[3], const int cell[3],
-                                            int a, int layer, float off, uint32_t medium) {
-  int q[3] = {cell[0], cell[1], cell[2]};
-  q[a] = layer;
-  bool early[3] = {false, false, false};
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    if (b == a) continue;
-    const float plane = float(cell[b] + (d[b] > 0.0f ? 1 : 0));
-    // first crossing of axis b, by the hardware reciprocal (<= 1 ulp) against a bound widened
-    // past its error: only ever more cells checked than the exact quotient would ask for
-    early[b] = (plane - p[b]) * __builtin_amdgcn_rcpf(d[b]) < off * 1.00001f;
-  }
-  const int b1 = a == 0 ? 1 : 0, b2 = a == 2 ? 1 : 2;
-  const int s1 = d[b1] > 0.0f ? 1 : -1, s2 = d[b2] > 0.0f ? 1 : -1;
-  int r[3];
-  if (early[b1]) {
-    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1;
-    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
-  }
-  if (early[b2]) {
-    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b2] += s2;
-    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
-  }
-  if (early[b1] && early[b2]) {
-    r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1; r[b2] += s2;
-    if (cert_event<SHADOW>(alt_byte(c, r[0], r[1], r[2], 0u), medium)) return false;
-  }
-  return true;
-}
-
 // Cells the exact walk samples behind its start cell. A start coordinate P_a that is an integer k
 // with D_a < 0 (a shadow or secondary ray from an exact hit point on its face plane) makes the
 // start cell k - 1 on axis a, but until cur_a = P_a + s D_a rounds off k the exact walk samples
@@ -1717,6 +1707,10 @@ __device__ __forceinline__ bool start_layers_clear(const Ctx& c, const f3 P, con
   for (int a = 0; a < 3; ++a) {
     if (!(d[a] < 0.0f) || p[a] != __builtin_floorf(p[a])) continue;
     const float off = (0x1p-22f * __builtin_fmaxf(__builtin_fabsf(p[a]), 1.0f) + 1e-5f) / __builtin_fabsf(d[a]);
+    // two crossings of one axis b in layer k (a nearly parallel D_a keeps cur_a on k: a
+    // straight-down lattice camera's ray at x = 64 with D_x = -2.2e-8 read plane N's GL_REPEAT
+    // copy for 170 units) need off >= 1 / |D_b| >= 1: more cells than checked here, unsure
+    if (off >= 1.0f) return false;
     int q[3] = {cell[0], cell[1], cell[2]};
     q[a] += 1;  // layer k
     bool early[3] = {false, false, false};
@@ -1728,6 +1722,12 @@ __device__ __forceinline__ bool start_layers_clear(const Ctx& c, const f3 P, con
     }
     const int b1 = a == 0 ? 1 : 0, b2 = a == 2 ? 1 : 2;
     const int s1 = d[b1] > 0.0f ? 1 : -1, s2 = d[b2] > 0.0f ? 1 : -1;
+    // shadow walks: the exact walk may cross b in layer k and so never sample the start layer's
+    // cell across b, which the certified walk reaches by that crossing and, if it blocks,
+    // reports as a hit "whichever way the walk goes" (a straight-down lattice camera's shadow
+    // from x = 33.0 going -x sampled (33, 30, 2) at its z crossing and never the solid (32, 30,
+    // 2)): unsure whenever a crossing falls in the sliver
+    if (SHADOW && (early[b1] || early[b2])) return false;
     int r[3];
     if (early[b1]) {
       r[0] = q[0]; r[1] = q[1]; r[2] = q[2]; r[b1] += s1;
@@ -1826,16 +1826,19 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
   if (uint32_t(cx) >= n || uint32_t(cy) >= n || uint32_t(cz) >= n) return false;
   // the start cell lies beyond plane k on axis fa, but P_fa may lie before it (by up to delta) or
   // on it: until cur_fa = P_fa + s D_fa is past k, the exact walk samples the layer before k at
-  // every crossing of another axis (as start_layers_clear for a start on a plane). Those cells must
-  // be non-events (a glass cube's face voxel beside the refraction point, sampled 3.7e-6 after the
-  // start, made a lattice camera's pixel differ before this check).
+  // every crossing of another axis (as start_layers_clear's layer k for a start on a plane), which
+  // the certified walk does not see (a glass cube's face voxel beside the refraction point,
+  // sampled 3.7e-6 after the start, made a lattice camera's pixel differ before this test):
+  // unsure when another axis is crossed that early. By the hardware reciprocal (<= 1 ulp) against
+  // a bound widened past its error: never fewer cases than the exact quotients would give.
   {
-    const float p[3] = {P.x, P.y, P.z}, d[3] = {D.x, D.y, D.z};
-    const int cell[3] = {cx, cy, cz};
     const float before = __builtin_fmaxf((k - pa) * sa, 0.0f);
-    const float off = (before + 0x1p-22f * __builtin_fmaxf(__builtin_fabsf(pa), 1.0f) + 1e-5f) / __builtin_fabsf(da);
-    const int ka = fa == 0 ? cx : (fa == 1 ? cy : cz);
-    if (!layer_clear<false>(c, p, d, cell, fa, ka - (da > 0.0f ? 1 : -1), off, 0u)) return false;
+    const float off = (before + 0x1p-22f * __builtin_fmaxf(__builtin_fabsf(pa), 1.0f) + 1e-5f) *
+                      __builtin_fabsf(__builtin_amdgcn_rcpf(da)) * 1.00002f;
+    const float tx = fa == 0 ? off : (float(cx + (D.x > 0.0f ? 1 : 0)) - P.x) * __builtin_amdgcn_rcpf(D.x);
+    const float ty = fa == 1 ? off : (float(cy + (D.y > 0.0f ? 1 : 0)) - P.y) * __builtin_amdgcn_rcpf(D.y);
+    const float tz = fa == 2 ? off : (float(cz + (D.z > 0.0f ? 1 : 0)) - P.z) * __builtin_amdgcn_rcpf(D.z);
+    if (__builtin_fminf(tx, __builtin_fminf(ty, tz)) < off) return false;
   }
   f3 ed = mk(0.0f, 0.0f, 0.0f);
   set_comp(ed, fa, 2.0f * delta * __builtin_fabsf(__builtin_amdgcn_rcpf(da)) + 1e-6f);
@@ -1847,7 +1850,7 @@ __device__ __forceinline__ bool cert_continuation(const Ctx& c, const Ray& ray, 
 // air — settled by certified walks where they can be (settled: colour updated, no secondary
 // rays); the exact march (as march()) otherwise.
 // (Out of line it costs C2-C4 +45 %, profiles/r01_v69_ab_noinline_w6.log.)
-__device__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k,
+__device__ __forceinline__ Hit march_cert(const Ctx& c, Ray& ray, f3& color, bool& settled, Counters& k,
                           uint32_t& steps, uint32_t& flags) {
   Hit h;
   h.found = false;
@@ -2192,6 +2195,9 @@ __device__ __forceinline__ void init_ctx(Ctx& c, const KArgs& a, const uint16_t*
   c.atlas_mask = uint32_t(a.atlas_size) - 1u;
   c.atlas_fs = float(a.atlas_size);
   c.atlas_fts = float(a.atlas_tex_size);
+#ifdef VRT_CERT_TRACE
+  c.tr = false;
+#endif
 }
 
 // The primary ray of pixel (px, frame row py): vertex stage (voxel.glsl:467-472) evaluated at the
@@ -2480,6 +2486,9 @@ __global__ void __launch_bounds__(kWgThreads, TREE ? VRT_TREE_WAVES : (DEFER ? V
   if (valid) {
     Ctx c;
     init_ctx(c, a, vox);
+#ifdef VRT_CERT_TRACE
+    c.tr = px == VRT_TRACE_PX && frame_row(a, li) == VRT_TRACE_PY;
+#endif
     if constexpr (FB) c.time = frame_view(a, fr).time;
     // one LDS pool: the exact path's axis table and bounce-stack bottom (in-lane instances), and
     // the certified tree's slots (TREE), which are live only before the exact path starts
@@ -3262,4 +3271,14 @@ int vrt_debug_cert_diag(uint64_t* out) { return out ? vrt::debug_cert_diag(out) 
 }  // extern "C"
 #elif defined(VRT_CERT_DIAG)
 extern "C" int vrt_debug_cert_diag(uint64_t* out) { return out ? vrt::debug_cert_diag(out) : VRT_ERR_INVALID; }
+#endif
+#ifdef VRT_CERT_TRACE
+// diagnostic build: the traced pixel's records (1024 x 8 floats) and their count; resets them
+extern "C" int vrt_debug_cert_trace(float* out, uint32_t* count) {
+  if (hipDeviceSynchronize() != hipSuccess) return VRT_ERR_DEVICE;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vrt::g_ctrace), 1024 * 8 * 4) != hipSuccess) return VRT_ERR_DEVICE;
+  if (hipMemcpyFromSymbol(count, HIP_SYMBOL(vrt::g_ctrace_n), 4) != hipSuccess) return VRT_ERR_DEVICE;
+  const uint32_t z = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(vrt::g_ctrace_n), &z, 4) == hipSuccess ? VRT_OK : VRT_ERR_DEVICE;
+}
 #endif

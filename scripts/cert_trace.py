@@ -3,7 +3,7 @@
 DEFS="-DVRT_CERT_TRACE -DVRT_TRACE_PX=x -DVRT_TRACE_PY=y", loaded by VRT_LIB), in lane with the
 given certified mode. Records: 100/101 walk start (shadow flag, cell, P, U / D, e0, ed), 102 an
 empty-space box (G, s1, uj, gam), 103/104 a crossing (next cell, s1, axis, near-edge flags, byte /
-cell, sig, gam of the axis). Usage: python scripts/cert_trace.py scene n w h px py pz rx ry R T cert"""
+cell, sig, gam of the axis). Usage: python scripts/cert_trace.py scene n w h px py pz rx ry R T cert [trees]"""
 import ctypes as C
 import os
 import sys
@@ -21,6 +21,7 @@ def main():
     pos = tuple(map(float, a[4:7]))
     rot = (float(a[7]), float(a[8]), 0.0)
     R, T, cert = int(a[9]), int(a[10]), int(a[11])
+    trees = int(a[12]) if len(a) > 12 else 0
     lib = vrt.lib()
     lib.vrt_debug_cert_trace.argtypes = [C.c_void_p, C.c_void_p]
     out = np.zeros((1024, 8), np.float32)
@@ -28,7 +29,7 @@ def main():
     with vrt.Renderer(0) as r:
         r.upload_volume(vrt.build_scene(scene, n), n)
         r.set_certified(cert)
-        r.set_cert_trees(0)
+        r.set_cert_trees(trees)
         r.set_exact_pass(0)
         cam = vrt.make_camera(w, h, pos=pos, rot=rot)
         p = vrt.default_params(R, T, time=1.0)

@@ -151,3 +151,34 @@ def test_cert_trees_frame_batches(built, ranks, rank, nf):
         torch.cuda.synchronize()
     for f in range(nf):
         assert torch.equal(got[f], ref[f]), f"frame {f}"
+
+
+@pytest.mark.parametrize("scene,n,pos,rot,R,T", [
+    ("terrain", 64, (1.0, 20.0, -22.0), (-90.0, 315.0, 0.0), 4, 4),
+    ("glass_cube", 128, (0.0, 50.0, -44.0), (-90.0, 315.0, 0.0), 4, 4),
+    ("refraction", 64, (0.0, 10.0, -8.5), (-90.0, 225.0, 0.0), 1, 2),
+    ("glass_cube", 64, (1.0, 2.0, -3.0), (0.0, 0.0, 0.0), 4, 4),
+])
+def test_certified_start_slivers(built, scene, n, pos, rot, R, T):
+    """The cameras scripts/lattice_stress.py found (HISTORY r06_s25-s34): straight-down views whose
+    rays have a zero or 2e-8 component, so shadow and primary walks start on a lattice plane (a
+    shadow from x = 33.0 going -x whose exact walk never sampled the solid cell the certified walk
+    blamed; a ray along x = 64 reading plane N's GL_REPEAT copy for 170 units), and a march
+    continuation started 8e-6 before a face plane. Every certified mode equals the exact instance."""
+    w, h = 320, 180
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        cam = vrt.make_camera(w, h, pos=pos, rot=rot)
+        ref = frames(r, cam, 1, R, T, 1.0, 0, h, 1, w, counters=True)
+        try:
+            for cert, trees, ep in ((1, 2, 2), (1, 2, 0), (1, 0, 2), (1, 0, 0), (0, 0, 0)):
+                r.set_certified(cert)
+                r.set_cert_trees(trees)
+                r.set_exact_pass(ep)
+                a = frames(r, cam, 1, R, T, 1.0, 0, h, 1, w)
+                bad = np.argwhere(np.any(a[0] != ref[0], axis=-1))
+                assert bad.size == 0, (cert, trees, ep, bad[:5].tolist())
+        finally:
+            r.set_certified(0)
+            r.set_cert_trees(1)
+            r.set_exact_pass(1)

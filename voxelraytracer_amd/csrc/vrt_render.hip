@@ -1205,6 +1205,11 @@ __device__ __forceinline__ CertResult cert_walk(const Ctx& c, const f3 P, const 
     const float prev = gmax(mback, 0.0f);
     const float gL = __builtin_fmaf(__builtin_fmaf(g2, uu, g1), uu, g0);
     if (prev > U + gL) {
+      // the length test stops the walk before this crossing, unless a tie merges it into the
+      // step of the one before (that step passed the test): then the exact walk still samples it
+      // (a tree ray whose y and z crossings tied at len 101.1 left the glass there, refracting,
+      // before its length ended the march; its sky colour took the refracted direction)
+      if (s1 - mback < 2.0f * gmax(gam.x, gmax(gam.y, gam.z))) return r;
       r.res = CERT_MISS;
       return r;
     }
@@ -1610,6 +1615,9 @@ __device__ __forceinline__ int tree_step(const Ctx& c, int max_refl, int max_tra
                "+s"(lc.sun_rcp.y), "+s"(lc.sun_rcp.z));
   bool next = false;
   TreeRay t;
+  CTRACE(c, 200, h.res, h.byte, h.axis, h.u, h.eu, ray.rdepth, ray.tdepth);
+  CTRACE(c, 201, ray.pos.x, ray.pos.y, ray.pos.z, ray.dir.x, ray.dir.y, ray.dir.z, ray.len);
+  CTRACE(c, 202, color.x, color.y, color.z, ray.energy, h.cx, h.cy, h.cz);
   if (h.res == CERT_MISS) {
     apply_sky_color(c, ray, color);
   } else {

@@ -182,3 +182,35 @@ def test_certified_start_slivers(built, scene, n, pos, rot, R, T):
             r.set_certified(0)
             r.set_cert_trees(1)
             r.set_exact_pass(1)
+
+
+@pytest.mark.parametrize("scene,n", [("glass_cube", 64), ("refraction", 64), ("terrain", 64)])
+def test_lattice_camera_sample(built, scene, n):
+    """A sample of scripts/lattice_stress.py (its full runs: 19 200 frames, HISTORY r06_s36): 40
+    lattice-aligned cameras (integer / half-integer positions; axis, diagonal, (1,1,1) and
+    straight-down views) per scene, every certified mode against the exact instance."""
+    rng = np.random.default_rng(sum(map(ord, scene)) + n)
+    pitches = [0.0, -45.0, 45.0, -35.26439, -90.0, 90.0, -30.0, -60.0, -89.99]
+    yaws = [0.0, 45.0, 90.0, 135.0, 180.0, 225.0, 270.0, 315.0, 30.0, 60.0]
+    w, h = 160, 90
+    with vrt.Renderer(0) as r:
+        r.upload_volume(vrt.build_scene(scene, n), n)
+        r.set_certified(1)
+        try:
+            for k in range(40):
+                pos = tuple(float(x) for x in np.round(rng.uniform(-n / 2.5, n / 2.5, 3) * 2) / 2)
+                if k % 3 == 0:
+                    pos = tuple(float(round(x)) for x in pos)
+                rot = (float(rng.choice(pitches)), float(rng.choice(yaws)), 0.0)
+                R, T = [(4, 4), (1, 2), (2, 6)][k % 3]
+                cam = vrt.make_camera(w, h, pos=pos, rot=rot)
+                ref = frames(r, cam, 1, R, T, 1.0, 0, h, 1, w, counters=True)
+                for trees, ep in ((2, 2), (2, 0), (0, 2), (0, 0)):
+                    r.set_cert_trees(trees)
+                    r.set_exact_pass(ep)
+                    a = frames(r, cam, 1, R, T, 1.0, 0, h, 1, w)
+                    bad = np.argwhere(np.any(a[0] != ref[0], axis=-1))
+                    assert bad.size == 0, (pos, rot, (R, T), trees, ep, bad[:3].tolist())
+        finally:
+            r.set_cert_trees(1)
+            r.set_exact_pass(1)
